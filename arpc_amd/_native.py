@@ -1,0 +1,107 @@
+"""ctypes binding of libsymphony_hip.so (the C ABI in include/symphony_hip.h).
+
+This is the same binding a cgo shim makes.  There is no fallback:
+if the HIP library has not been built, importing the codec raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libsymphony_hip.so")
+CSRC = os.path.join(HERE, "csrc")
+
+SYM_OK = 0
+SYM_ERR_INVALID = -1
+SYM_ERR_HIP = -2
+SYM_ERR_NOMEM = -3
+SYM_ERR_CAPACITY = -4
+SYM_ERR_DEVICE = -5
+
+# every symbol include/symphony_hip.h declares, with its ctypes signature
+_u8p = ctypes.c_void_p
+_u64p = ctypes.c_void_p
+_vp = ctypes.c_void_p
+_u32 = ctypes.c_uint32
+_u64 = ctypes.c_uint64
+_int = ctypes.c_int
+_ctx = ctypes.c_void_p
+
+SIGNATURES = {
+    "sym_abi_version": (_int, []),
+    "sym_last_error": (ctypes.c_char_p, []),
+    "sym_ctx_create": (_int, [_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "sym_ctx_destroy": (_int, [_ctx]),
+    "sym_ctx_reserve": (_int, [_ctx, _u64]),
+    "sym_ctx_check": (_int, [_ctx, _vp]),
+    "sym_schema_info": (_int, [_int, ctypes.POINTER(_int), ctypes.POINTER(_int)]),
+    "sym_record_overhead": (_u64, [_int]),
+    "sym_encoded_size": (_u64, [_int, _u64, _u64]),
+    "sym_encode": (_int, [_ctx, _int, _u64, _vp, _vp, _vp, _u32, _u32, _u8p, _u64p, _vp]),
+    "sym_decode": (_int, [_ctx, _int, _u64, _u8p, _u64p, _vp, _vp, _vp, _vp, _u8p, _vp]),
+    "sym_encode_kv_set": (_int, [_ctx, _u8p, _u64p, _u8p, _u64p, _u64, _u32, _u32, _u8p, _u64p, _vp]),
+    "sym_encode_kv_get": (_int, [_ctx, _u8p, _u64p, _u64, _u32, _u32, _u8p, _u64p, _vp]),
+    "sym_encode_kv_response": (_int, [_ctx, _int, _u8p, _u64p, _u64, _u32, _u32, _u8p, _u64p, _vp]),
+    "sym_encode_echo": (_int, [_ctx, _vp, _vp, _u8p, _u64p, _u8p, _u64p, _u64, _u32, _u32, _u8p, _u64p, _vp]),
+    "sym_decode_kv_set": (_int, [_ctx, _u8p, _u64p, _u64, _u8p, _u64, _u64p, _u8p, _u64, _u64p, _u8p, _vp]),
+    "sym_decode_kv_get": (_int, [_ctx, _u8p, _u64p, _u64, _u8p, _u64, _u64p, _u8p, _vp]),
+    "sym_decode_kv_response": (_int, [_ctx, _int, _u8p, _u64p, _u64, _u8p, _u64, _u64p, _u8p, _vp]),
+    "sym_decode_echo": (_int, [_ctx, _u8p, _u64p, _u64, _vp, _vp, _u8p, _u64, _u64p, _u8p, _u64, _u64p, _u8p,
+                               _vp]),
+    "sym_encode_host": (_int, [_ctx, _int, _u64, _vp, _vp, _vp, _u32, _u32, _u8p, _u64p]),
+    "sym_decode_host": (_int, [_ctx, _int, _u64, _u8p, _u64p, _vp, _vp, _vp, _vp, _u8p]),
+}
+
+_lib = None
+
+
+class SymphonyHipError(RuntimeError):
+    def __init__(self, code: int, what: str):
+        super().__init__(f"{what} failed with code {code}: {last_error()}")
+        self.code = code
+
+
+def lib() -> ctypes.CDLL:
+    """Load the HIP codec library; raises if it was never built (no CPU fallback exists)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"HIP Symphony codec not built ({LIB_PATH} missing); run `make -C {CSRC}` "
+                "or `python -c 'import __graft_entry__ as g; g.build()'`")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        if L.sym_abi_version() != 1:
+            raise ImportError(f"unexpected ABI version {L.sym_abi_version()} in {LIB_PATH}")
+        _lib = L
+    return _lib
+
+
+def last_error() -> str:
+    if _lib is None:
+        return ""
+    msg = _lib.sym_last_error()
+    return msg.decode(errors="replace") if msg else ""
+
+
+def check(rc: int, what: str) -> None:
+    if rc != SYM_OK:
+        raise SymphonyHipError(rc, what)
+
+
+def ptr_array(values) -> ctypes.Array:
+    arr = (ctypes.c_void_p * max(1, len(values)))()
+    for i, v in enumerate(values):
+        arr[i] = v
+    return arr
+
+
+def u64_array(values) -> ctypes.Array:
+    arr = (ctypes.c_uint64 * max(1, len(values)))()
+    for i, v in enumerate(values):
+        arr[i] = v
+    return arr

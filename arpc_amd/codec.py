@@ -1,0 +1,154 @@
+"""Device-resident batched Symphony codec over torch tensors.
+
+PyTorch is plumbing here: it owns device memory and the current HIP stream; every
+byte is produced by the gfx950 kernels behind the C ABI (arpc_amd/csrc).
+
+Layout (matches include/symphony_hip.h): a string field is a uint8 column plus an
+int64 offset tensor of n+1 entries (uint64 on the C side); an int32 field is an
+int32 column; the encoded stream is a uint8 tensor plus its n+1 record offsets.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import torch
+
+from . import _native, schemas
+
+
+def _stream_handle(device: torch.device, stream=None) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream(device)
+    return s.cuda_stream
+
+
+def _dptr(t: torch.Tensor | None) -> int:
+    return 0 if t is None or t.numel() == 0 else t.data_ptr()
+
+
+def _check_col(t: torch.Tensor, dtype, what: str, device: torch.device):
+    if t.dtype != dtype:
+        raise TypeError(f"{what}: expected {dtype}, got {t.dtype}")
+    if t.device != device:
+        raise ValueError(f"{what}: expected device {device}, got {t.device}")
+    if not t.is_contiguous():
+        raise ValueError(f"{what}: must be contiguous")
+
+
+@dataclass
+class EncodedBatch:
+    data: torch.Tensor     # uint8 [total]
+    offsets: torch.Tensor  # int64 [n+1]
+
+
+@dataclass
+class DecodedBatch:
+    fixed: list            # int32 [n] per fixed field
+    var: list              # (uint8 column, int64 offsets [n+1]) per string field
+    status: torch.Tensor   # uint8 [n], SYM_STATUS_*
+
+
+class Codec:
+    """One C-ABI context (decode workspace + device error word) bound to one GPU.
+
+    Not safe for concurrent calls from several threads: use one Codec per thread/stream.
+    """
+
+    def __init__(self, device: int | torch.device = 0):
+        self.device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+        if self.device.type != "cuda":
+            raise ValueError("Codec needs a GPU device")
+        self._lib = _native.lib()
+        h = ctypes.c_void_p()
+        _native.check(self._lib.sym_ctx_create(self.device.index or 0, ctypes.byref(h)), "sym_ctx_create")
+        self._ctx = h
+
+    def close(self):
+        if getattr(self, "_ctx", None):
+            self._lib.sym_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reserve(self, max_records: int):
+        _native.check(self._lib.sym_ctx_reserve(self._ctx, max_records), "sym_ctx_reserve")
+
+    def check(self, stream=None):
+        """Synchronize and raise if a decode reported a capacity overflow or a look-back timeout."""
+        _native.check(self._lib.sym_ctx_check(self._ctx, _stream_handle(self.device, stream)), "sym_ctx_check")
+
+    # ------------------------------------------------------------------ encode
+    def encode(self, schema: schemas.Schema | str, fixed, var, service_id: int = 0, method_id: int = 0,
+               out: torch.Tensor | None = None, out_off: torch.Tensor | None = None,
+               var_total: int | None = None, stream=None) -> EncodedBatch:
+        """Marshal n records (n = len(offsets) - 1).  `var_total` (sum of string bytes) avoids a sync
+        when `out` is not given."""
+        s = schemas.BY_NAME[schema] if isinstance(schema, str) else schema
+        if len(fixed) != s.nfixed or len(var) != s.nvar:
+            raise ValueError(f"{s.name}: expected {s.nfixed} int32 and {s.nvar} string columns")
+        n = (var[0][1].numel() - 1) if s.nvar else fixed[0].numel()
+        for i, c in enumerate(fixed):
+            _check_col(c, torch.int32, f"fixed[{i}]", self.device)
+            if c.numel() < n:
+                raise ValueError(f"fixed[{i}] has {c.numel()} < {n} values")
+        for i, (b, o) in enumerate(var):
+            _check_col(b, torch.uint8, f"var[{i}] bytes", self.device)
+            _check_col(o, torch.int64, f"var[{i}] offsets", self.device)
+            if o.numel() != n + 1:
+                raise ValueError(f"var[{i}] offsets must have n+1={n + 1} entries")
+        if out is None:
+            if var_total is None:
+                var_total = sum(int(o[-1].item() - o[0].item()) for _, o in var) if n else 0
+            out = torch.empty(max(1, n * s.overhead + var_total), dtype=torch.uint8, device=self.device)
+        if out_off is None:
+            out_off = torch.empty(n + 1, dtype=torch.int64, device=self.device)
+        rc = self._lib.sym_encode(
+            self._ctx, s.schema_id, n, _native.ptr_array([_dptr(c) for c in fixed]),
+            _native.ptr_array([_dptr(b) if b.numel() else 1 for b, _ in var]),
+            _native.ptr_array([_dptr(o) for _, o in var]), service_id, method_id, _dptr(out), _dptr(out_off),
+            _stream_handle(self.device, stream))
+        _native.check(rc, f"sym_encode({s.name})")
+        return EncodedBatch(out, out_off)
+
+    # ------------------------------------------------------------------ decode
+    def decode(self, schema: schemas.Schema | str, data: torch.Tensor, rec_off: torch.Tensor,
+               caps: list | None = None, outputs: DecodedBatch | None = None, stream=None) -> DecodedBatch:
+        """Unmarshal n records (n = len(rec_off) - 1) into packed columns.  Default column capacity is
+        rec_off[n] - rec_off[0] (always sufficient; costs one sync to read)."""
+        s = schemas.BY_NAME[schema] if isinstance(schema, str) else schema
+        _check_col(data, torch.uint8, "data", self.device)
+        _check_col(rec_off, torch.int64, "rec_off", self.device)
+        n = rec_off.numel() - 1
+        if outputs is None:
+            if caps is None:
+                span = int(rec_off[-1].item() - rec_off[0].item()) if n else 0
+                caps = [span] * s.nvar
+            outputs = DecodedBatch(
+                fixed=[torch.empty(max(1, n), dtype=torch.int32, device=self.device) for _ in range(s.nfixed)],
+                var=[(torch.empty(max(1, caps[f]), dtype=torch.uint8, device=self.device),
+                      torch.empty(n + 1, dtype=torch.int64, device=self.device)) for f in range(s.nvar)],
+                status=torch.empty(max(1, n), dtype=torch.uint8, device=self.device))
+        elif caps is None:
+            caps = [b.numel() for b, _ in outputs.var]
+        rc = self._lib.sym_decode(
+            self._ctx, s.schema_id, n, _dptr(data) if data.numel() else 1, _dptr(rec_off),
+            _native.ptr_array([_dptr(c) for c in outputs.fixed]),
+            _native.ptr_array([_dptr(b) for b, _ in outputs.var]), _native.u64_array(caps),
+            _native.ptr_array([_dptr(o) for _, o in outputs.var]), _dptr(outputs.status),
+            _stream_handle(self.device, stream))
+        _native.check(rc, f"sym_decode({s.name})")
+        return outputs
+
+
+def to_device(batch, device) -> tuple[list, list]:
+    """datagen.Batch (numpy) -> (fixed int32 tensors, [(uint8 tensor, int64 offsets tensor)]) on device."""
+    fixed = [torch.from_numpy(c).to(device) for c in batch.fixed]
+    var = []
+    for b, o in batch.var:
+        bt = torch.from_numpy(b) if b.size else torch.zeros(1, dtype=torch.uint8)
+        var.append((bt.to(device), torch.from_numpy(o.view("int64")).to(device)))
+    return fixed, var

@@ -1,0 +1,453 @@
+// capi.cpp -- the extern "C" boundary declared in include/symphony_hip.h.
+//
+// Argument checking, schema dispatch, the per-ctx decode workspace, device error
+// reporting and the host-memory entry points.  All compute goes to the HIP kernels in
+// encode.hip / decode.hip; there is no CPU codec in this library.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+
+#include "../../include/symphony_hip.h"
+#include "codec.hpp"
+
+using symhip::DecodeParams;
+using symhip::EncodeParams;
+using symhip::Layout;
+
+struct sym_ctx {
+    int device = 0;
+    void* ws = nullptr;  // decode look-back workspace
+    size_t ws_bytes = 0;
+    unsigned* err = nullptr;  // device error word (kErr* bits)
+    // host entry points: device staging pool and a private stream
+    void* pool = nullptr;
+    size_t pool_bytes = 0;
+    hipStream_t stream = nullptr;
+};
+
+namespace {
+
+thread_local char g_err[512] = "";
+
+int fail(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    return fail(SYM_ERR_HIP, "%s: %s (%d)", what, hipGetErrorString(e), (int)e);
+}
+
+const Layout kLayouts[SYM_SCHEMA_COUNT] = {
+    {0, 1},  // GetRequest{Key}
+    {0, 2},  // SetRequest{Key, Value}
+    {0, 1},  // GetResponse{Value}
+    {0, 1},  // SetResponse{Value}
+    {2, 2},  // EchoRequest{Id, Score, Username, Content}
+    {2, 2},  // EchoResponse
+};
+
+bool schema_ok(int schema) { return schema >= 0 && schema < SYM_SCHEMA_COUNT; }
+
+// Runs the body with ctx->device current, restoring the caller's device after.
+struct DeviceGuard {
+    int prev = -1;
+    hipError_t err = hipSuccess;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) err = hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+int ensure_ws(sym_ctx* ctx, int nvar, uint64_t n) {
+    const size_t need = symhip::decode_workspace_bytes(nvar, n);
+    if (need <= ctx->ws_bytes) return SYM_OK;
+    if (ctx->ws) (void)hipFree(ctx->ws);
+    ctx->ws = nullptr;
+    ctx->ws_bytes = 0;
+    hipError_t e = hipMalloc(&ctx->ws, need);
+    if (e != hipSuccess) return fail(SYM_ERR_NOMEM, "decode workspace of %zu bytes: %s", need, hipGetErrorString(e));
+    ctx->ws_bytes = need;
+    return SYM_OK;
+}
+
+int ensure_pool(sym_ctx* ctx, size_t need) {
+    if (need <= ctx->pool_bytes) return SYM_OK;
+    if (ctx->pool) (void)hipFree(ctx->pool);
+    ctx->pool = nullptr;
+    ctx->pool_bytes = 0;
+    hipError_t e = hipMalloc(&ctx->pool, need);
+    if (e != hipSuccess) return fail(SYM_ERR_NOMEM, "staging pool of %zu bytes: %s", need, hipGetErrorString(e));
+    ctx->pool_bytes = need;
+    return SYM_OK;
+}
+
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+}  // namespace
+
+extern "C" {
+
+int sym_abi_version(void) { return SYMPHONY_HIP_ABI_VERSION; }
+
+const char* sym_last_error(void) { return g_err; }
+
+int sym_ctx_create(int device, sym_ctx** out_ctx) {
+    if (!out_ctx) return fail(SYM_ERR_INVALID, "sym_ctx_create: out_ctx is NULL");
+    *out_ctx = nullptr;
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDeviceCount");
+    if (device < 0 || device >= ndev) return fail(SYM_ERR_INVALID, "device %d out of range (%d devices)", device, ndev);
+    DeviceGuard g(device);
+    if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
+    sym_ctx* c = new (std::nothrow) sym_ctx;
+    if (!c) return fail(SYM_ERR_NOMEM, "sym_ctx_create: out of host memory");
+    c->device = device;
+    if ((e = hipMalloc(&c->err, 16)) != hipSuccess || (e = hipMemset(c->err, 0, 16)) != hipSuccess ||
+        (e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
+        sym_ctx_destroy(c);
+        return hip_fail(e, "sym_ctx_create");
+    }
+    *out_ctx = c;
+    return SYM_OK;
+}
+
+int sym_ctx_destroy(sym_ctx* ctx) {
+    if (!ctx) return SYM_OK;
+    DeviceGuard g(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->ws) (void)hipFree(ctx->ws);
+    if (ctx->err) (void)hipFree(ctx->err);
+    if (ctx->pool) (void)hipFree(ctx->pool);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return SYM_OK;
+}
+
+int sym_ctx_reserve(sym_ctx* ctx, uint64_t max_records) {
+    if (!ctx) return fail(SYM_ERR_INVALID, "sym_ctx_reserve: ctx is NULL");
+    DeviceGuard g(ctx->device);
+    return ensure_ws(ctx, symhip::kMaxVar, max_records);
+}
+
+int sym_ctx_check(sym_ctx* ctx, void* stream) {
+    if (!ctx) return fail(SYM_ERR_INVALID, "sym_ctx_check: ctx is NULL");
+    DeviceGuard g(ctx->device);
+    hipError_t e = hipStreamSynchronize((hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+    unsigned bits = 0;
+    if ((e = hipMemcpy(&bits, ctx->err, sizeof(bits), hipMemcpyDeviceToHost)) != hipSuccess)
+        return hip_fail(e, "reading device error word");
+    if (bits == 0) return SYM_OK;
+    if ((e = hipMemset(ctx->err, 0, sizeof(bits))) != hipSuccess) return hip_fail(e, "clearing device error word");
+    if (bits & symhip::kErrTimeout) return fail(SYM_ERR_DEVICE, "decode look-back timed out (device error bits 0x%x)", bits);
+    return fail(SYM_ERR_CAPACITY, "decode output column capacity exceeded (device error bits 0x%x)", bits);
+}
+
+int sym_schema_info(int schema, int* nfixed, int* nvar) {
+    if (!schema_ok(schema)) return fail(SYM_ERR_INVALID, "unknown schema %d", schema);
+    if (nfixed) *nfixed = kLayouts[schema].nfixed;
+    if (nvar) *nvar = kLayouts[schema].nvar;
+    return SYM_OK;
+}
+
+uint64_t sym_record_overhead(int schema) {
+    if (!schema_ok(schema)) return 0;
+    const Layout& l = kLayouts[schema];
+    return 14u + 4u * (uint64_t)(l.nfixed + l.nvar) + 4u * (uint64_t)l.nvar;
+}
+
+uint64_t sym_encoded_size(int schema, uint64_t n, uint64_t var_total) {
+    return n * sym_record_overhead(schema) + var_total;
+}
+
+int sym_encode(sym_ctx* ctx, int schema, uint64_t n, const int32_t* const* d_fixed, const uint8_t* const* d_bytes,
+               const uint64_t* const* d_offs, uint32_t service_id, uint32_t method_id, uint8_t* d_out,
+               uint64_t* d_out_off, void* stream) {
+    if (!ctx) return fail(SYM_ERR_INVALID, "sym_encode: ctx is NULL");
+    if (!schema_ok(schema)) return fail(SYM_ERR_INVALID, "sym_encode: unknown schema %d", schema);
+    const Layout lay = kLayouts[schema];
+    if (!d_out_off) return fail(SYM_ERR_INVALID, "sym_encode: d_out_off is NULL");
+    if (n > 0) {
+        if (!d_out) return fail(SYM_ERR_INVALID, "sym_encode: d_out is NULL");
+        if (lay.nfixed && !d_fixed) return fail(SYM_ERR_INVALID, "sym_encode: d_fixed is NULL");
+        if (!d_bytes || !d_offs) return fail(SYM_ERR_INVALID, "sym_encode: d_bytes/d_offs is NULL");
+        for (int f = 0; f < lay.nfixed; ++f)
+            if (!d_fixed[f]) return fail(SYM_ERR_INVALID, "sym_encode: fixed column %d is NULL", f);
+        for (int f = 0; f < lay.nvar; ++f)
+            if (!d_offs[f] || !d_bytes[f]) return fail(SYM_ERR_INVALID, "sym_encode: var column %d is NULL", f);
+    }
+    EncodeParams p{};
+    p.lay = lay;
+    p.n = n;
+    for (int f = 0; f < lay.nfixed; ++f) p.fixed[f] = d_fixed[f];
+    for (int f = 0; f < lay.nvar && n; ++f) {
+        p.bytes[f] = d_bytes[f];
+        p.offs[f] = d_offs[f];
+    }
+    p.service_id = service_id;
+    p.method_id = method_id;
+    p.out = d_out;
+    p.out_off = d_out_off;
+    DeviceGuard g(ctx->device);
+    if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
+    hipError_t e = symhip::launch_encode(p, (hipStream_t)stream);
+    return e == hipSuccess ? SYM_OK : hip_fail(e, "encode launch");
+}
+
+int sym_decode(sym_ctx* ctx, int schema, uint64_t n, const uint8_t* d_in, const uint64_t* d_rec_off,
+               int32_t* const* d_fixed, uint8_t* const* d_bytes, const uint64_t* caps, uint64_t* const* d_offs,
+               uint8_t* d_status, void* stream) {
+    if (!ctx) return fail(SYM_ERR_INVALID, "sym_decode: ctx is NULL");
+    if (!schema_ok(schema)) return fail(SYM_ERR_INVALID, "sym_decode: unknown schema %d", schema);
+    const Layout lay = kLayouts[schema];
+    if (!d_offs) return fail(SYM_ERR_INVALID, "sym_decode: d_offs is NULL");
+    for (int f = 0; f < lay.nvar; ++f)
+        if (!d_offs[f]) return fail(SYM_ERR_INVALID, "sym_decode: offset column %d is NULL", f);
+    if (n > 0) {
+        if (!d_in || !d_rec_off || !d_status) return fail(SYM_ERR_INVALID, "sym_decode: d_in/d_rec_off/d_status is NULL");
+        if (lay.nfixed && !d_fixed) return fail(SYM_ERR_INVALID, "sym_decode: d_fixed is NULL");
+        for (int f = 0; f < lay.nfixed; ++f)
+            if (!d_fixed[f]) return fail(SYM_ERR_INVALID, "sym_decode: fixed column %d is NULL", f);
+        if (!d_bytes || !caps) return fail(SYM_ERR_INVALID, "sym_decode: d_bytes/caps is NULL");
+        for (int f = 0; f < lay.nvar; ++f)
+            if (!d_bytes[f] && caps[f]) return fail(SYM_ERR_INVALID, "sym_decode: byte column %d is NULL", f);
+    }
+    DeviceGuard g(ctx->device);
+    if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
+    int rc = ensure_ws(ctx, lay.nvar, n);
+    if (rc != SYM_OK) return rc;
+    DecodeParams p{};
+    p.lay = lay;
+    p.n = n;
+    p.in = d_in;
+    p.rec_off = d_rec_off;
+    for (int f = 0; f < lay.nfixed; ++f) p.fixed[f] = d_fixed[f];
+    for (int f = 0; f < lay.nvar; ++f) {
+        p.bytes[f] = n ? d_bytes[f] : nullptr;
+        p.cap[f] = n ? caps[f] : 0;
+        p.offs[f] = d_offs[f];
+    }
+    p.status = d_status;
+    p.ws = ctx->ws;
+    p.err = ctx->err;
+    hipError_t e = symhip::launch_decode(p, (hipStream_t)stream);
+    return e == hipSuccess ? SYM_OK : hip_fail(e, "decode launch");
+}
+
+// ---- typed entry points ----
+
+int sym_encode_kv_set(sym_ctx* ctx, const uint8_t* d_key, const uint64_t* d_key_off, const uint8_t* d_val,
+                      const uint64_t* d_val_off, uint64_t n, uint32_t service_id, uint32_t method_id,
+                      uint8_t* d_out, uint64_t* d_out_off, void* stream) {
+    const uint8_t* b[2] = {d_key, d_val};
+    const uint64_t* o[2] = {d_key_off, d_val_off};
+    return sym_encode(ctx, SYM_SCHEMA_KV_SET_REQUEST, n, nullptr, b, o, service_id, method_id, d_out, d_out_off, stream);
+}
+
+int sym_encode_kv_get(sym_ctx* ctx, const uint8_t* d_key, const uint64_t* d_key_off, uint64_t n,
+                      uint32_t service_id, uint32_t method_id, uint8_t* d_out, uint64_t* d_out_off, void* stream) {
+    const uint8_t* b[1] = {d_key};
+    const uint64_t* o[1] = {d_key_off};
+    return sym_encode(ctx, SYM_SCHEMA_KV_GET_REQUEST, n, nullptr, b, o, service_id, method_id, d_out, d_out_off, stream);
+}
+
+int sym_encode_kv_response(sym_ctx* ctx, int schema, const uint8_t* d_val, const uint64_t* d_val_off, uint64_t n,
+                           uint32_t service_id, uint32_t method_id, uint8_t* d_out, uint64_t* d_out_off,
+                           void* stream) {
+    if (schema != SYM_SCHEMA_KV_GET_RESPONSE && schema != SYM_SCHEMA_KV_SET_RESPONSE)
+        return fail(SYM_ERR_INVALID, "sym_encode_kv_response: schema %d is not a KV response", schema);
+    const uint8_t* b[1] = {d_val};
+    const uint64_t* o[1] = {d_val_off};
+    return sym_encode(ctx, schema, n, nullptr, b, o, service_id, method_id, d_out, d_out_off, stream);
+}
+
+int sym_encode_echo(sym_ctx* ctx, const int32_t* d_id, const int32_t* d_score, const uint8_t* d_user,
+                    const uint64_t* d_user_off, const uint8_t* d_content, const uint64_t* d_content_off, uint64_t n,
+                    uint32_t service_id, uint32_t method_id, uint8_t* d_out, uint64_t* d_out_off, void* stream) {
+    const int32_t* fx[2] = {d_id, d_score};
+    const uint8_t* b[2] = {d_user, d_content};
+    const uint64_t* o[2] = {d_user_off, d_content_off};
+    return sym_encode(ctx, SYM_SCHEMA_ECHO_REQUEST, n, fx, b, o, service_id, method_id, d_out, d_out_off, stream);
+}
+
+int sym_decode_kv_set(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_off, uint64_t n, uint8_t* d_key,
+                      uint64_t key_cap, uint64_t* d_key_off, uint8_t* d_val, uint64_t val_cap, uint64_t* d_val_off,
+                      uint8_t* d_status, void* stream) {
+    uint8_t* b[2] = {d_key, d_val};
+    const uint64_t caps[2] = {key_cap, val_cap};
+    uint64_t* o[2] = {d_key_off, d_val_off};
+    return sym_decode(ctx, SYM_SCHEMA_KV_SET_REQUEST, n, d_in, d_rec_off, nullptr, b, caps, o, d_status, stream);
+}
+
+int sym_decode_kv_get(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_off, uint64_t n, uint8_t* d_key,
+                      uint64_t key_cap, uint64_t* d_key_off, uint8_t* d_status, void* stream) {
+    uint8_t* b[1] = {d_key};
+    const uint64_t caps[1] = {key_cap};
+    uint64_t* o[1] = {d_key_off};
+    return sym_decode(ctx, SYM_SCHEMA_KV_GET_REQUEST, n, d_in, d_rec_off, nullptr, b, caps, o, d_status, stream);
+}
+
+int sym_decode_kv_response(sym_ctx* ctx, int schema, const uint8_t* d_in, const uint64_t* d_rec_off, uint64_t n,
+                           uint8_t* d_val, uint64_t val_cap, uint64_t* d_val_off, uint8_t* d_status, void* stream) {
+    if (schema != SYM_SCHEMA_KV_GET_RESPONSE && schema != SYM_SCHEMA_KV_SET_RESPONSE)
+        return fail(SYM_ERR_INVALID, "sym_decode_kv_response: schema %d is not a KV response", schema);
+    uint8_t* b[1] = {d_val};
+    const uint64_t caps[1] = {val_cap};
+    uint64_t* o[1] = {d_val_off};
+    return sym_decode(ctx, schema, n, d_in, d_rec_off, nullptr, b, caps, o, d_status, stream);
+}
+
+int sym_decode_echo(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_off, uint64_t n, int32_t* d_id,
+                    int32_t* d_score, uint8_t* d_user, uint64_t user_cap, uint64_t* d_user_off, uint8_t* d_content,
+                    uint64_t content_cap, uint64_t* d_content_off, uint8_t* d_status, void* stream) {
+    int32_t* fx[2] = {d_id, d_score};
+    uint8_t* b[2] = {d_user, d_content};
+    const uint64_t caps[2] = {user_cap, content_cap};
+    uint64_t* o[2] = {d_user_off, d_content_off};
+    return sym_decode(ctx, SYM_SCHEMA_ECHO_REQUEST, n, d_in, d_rec_off, fx, b, caps, o, d_status, stream);
+}
+
+// ---- host-memory entry points ----
+// Stage through one device pool: inputs H2D, kernel, outputs D2H, all on the ctx stream.
+// Offsets are passed through unchanged; the device column base is shifted by -offs[0] so
+// the kernels see the same absolute offsets the caller used.
+
+int sym_encode_host(sym_ctx* ctx, int schema, uint64_t n, const int32_t* const* h_fixed,
+                    const uint8_t* const* h_bytes, const uint64_t* const* h_offs, uint32_t service_id,
+                    uint32_t method_id, uint8_t* h_out, uint64_t* h_out_off) {
+    if (!ctx) return fail(SYM_ERR_INVALID, "sym_encode_host: ctx is NULL");
+    if (!schema_ok(schema)) return fail(SYM_ERR_INVALID, "sym_encode_host: unknown schema %d", schema);
+    if (!h_out_off) return fail(SYM_ERR_INVALID, "sym_encode_host: h_out_off is NULL");
+    const Layout lay = kLayouts[schema];
+    if (n == 0) {
+        h_out_off[0] = 0;
+        return SYM_OK;
+    }
+    if (!h_out || !h_bytes || !h_offs || (lay.nfixed && !h_fixed))
+        return fail(SYM_ERR_INVALID, "sym_encode_host: NULL column");
+    uint64_t col_lo[2] = {0, 0}, col_len[2] = {0, 0}, var_total = 0;
+    for (int f = 0; f < lay.nvar; ++f) {
+        if (!h_offs[f] || !h_bytes[f]) return fail(SYM_ERR_INVALID, "sym_encode_host: NULL var column %d", f);
+        col_lo[f] = h_offs[f][0];
+        if (h_offs[f][n] < col_lo[f]) return fail(SYM_ERR_INVALID, "sym_encode_host: offsets of field %d decrease", f);
+        col_len[f] = h_offs[f][n] - col_lo[f];
+        var_total += col_len[f];
+    }
+    const uint64_t out_bytes = sym_encoded_size(schema, n, var_total);
+    size_t at = 0, o_fixed[2], o_bytes[2], o_offs[2];
+    for (int f = 0; f < lay.nfixed; ++f) { o_fixed[f] = at; at = align256(at + 4 * n); }
+    for (int f = 0; f < lay.nvar; ++f) {
+        o_bytes[f] = at; at = align256(at + col_len[f] + 16);
+        o_offs[f] = at; at = align256(at + 8 * (n + 1));
+    }
+    const size_t o_out = at; at = align256(at + out_bytes + 16);
+    const size_t o_out_off = at; at = align256(at + 8 * (n + 1));
+    DeviceGuard g(ctx->device);
+    if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
+    int rc = ensure_pool(ctx, at);
+    if (rc != SYM_OK) return rc;
+    char* base = (char*)ctx->pool;
+    hipStream_t s = ctx->stream;
+    hipError_t e = hipSuccess;
+    const int32_t* d_fixed[2] = {nullptr, nullptr};
+    const uint8_t* d_bytes[2] = {nullptr, nullptr};
+    const uint64_t* d_offs[2] = {nullptr, nullptr};
+    for (int f = 0; f < lay.nfixed && e == hipSuccess; ++f) {
+        e = hipMemcpyAsync(base + o_fixed[f], h_fixed[f], 4 * n, hipMemcpyHostToDevice, s);
+        d_fixed[f] = (const int32_t*)(base + o_fixed[f]);
+    }
+    for (int f = 0; f < lay.nvar && e == hipSuccess; ++f) {
+        if (col_len[f]) e = hipMemcpyAsync(base + o_bytes[f], h_bytes[f] + col_lo[f], col_len[f], hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(base + o_offs[f], h_offs[f], 8 * (n + 1), hipMemcpyHostToDevice, s);
+        d_bytes[f] = (const uint8_t*)(base + o_bytes[f]) - col_lo[f];
+        d_offs[f] = (const uint64_t*)(base + o_offs[f]);
+    }
+    if (e != hipSuccess) return hip_fail(e, "sym_encode_host H2D");
+    rc = sym_encode(ctx, schema, n, d_fixed, d_bytes, d_offs, service_id, method_id, (uint8_t*)(base + o_out),
+                    (uint64_t*)(base + o_out_off), s);
+    if (rc != SYM_OK) return rc;
+    if ((e = hipMemcpyAsync(h_out, base + o_out, out_bytes, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+        (e = hipMemcpyAsync(h_out_off, base + o_out_off, 8 * (n + 1), hipMemcpyDeviceToHost, s)) != hipSuccess ||
+        (e = hipStreamSynchronize(s)) != hipSuccess)
+        return hip_fail(e, "sym_encode_host D2H");
+    return SYM_OK;
+}
+
+int sym_decode_host(sym_ctx* ctx, int schema, uint64_t n, const uint8_t* h_in, const uint64_t* h_rec_off,
+                    int32_t* const* h_fixed, uint8_t* const* h_bytes, const uint64_t* caps, uint64_t* const* h_offs,
+                    uint8_t* h_status) {
+    if (!ctx) return fail(SYM_ERR_INVALID, "sym_decode_host: ctx is NULL");
+    if (!schema_ok(schema)) return fail(SYM_ERR_INVALID, "sym_decode_host: unknown schema %d", schema);
+    const Layout lay = kLayouts[schema];
+    if (!h_offs) return fail(SYM_ERR_INVALID, "sym_decode_host: h_offs is NULL");
+    for (int f = 0; f < lay.nvar; ++f)
+        if (!h_offs[f]) return fail(SYM_ERR_INVALID, "sym_decode_host: h_offs[%d] is NULL", f);
+    if (n == 0) {
+        for (int f = 0; f < lay.nvar; ++f) h_offs[f][0] = 0;
+        return SYM_OK;
+    }
+    if (!h_in || !h_rec_off || !h_status || !h_bytes || !caps || (lay.nfixed && !h_fixed))
+        return fail(SYM_ERR_INVALID, "sym_decode_host: NULL argument");
+    const uint64_t in_lo = h_rec_off[0];
+    if (h_rec_off[n] < in_lo) return fail(SYM_ERR_INVALID, "sym_decode_host: record offsets decrease");
+    const uint64_t in_len = h_rec_off[n] - in_lo;
+    size_t at = 0;
+    const size_t o_in = at; at = align256(at + in_len + 16);
+    const size_t o_rec = at; at = align256(at + 8 * (n + 1));
+    const size_t o_status = at; at = align256(at + n);
+    size_t o_fixed[2], o_bytes[2], o_offs[2];
+    for (int f = 0; f < lay.nfixed; ++f) { o_fixed[f] = at; at = align256(at + 4 * n); }
+    for (int f = 0; f < lay.nvar; ++f) {
+        o_bytes[f] = at; at = align256(at + caps[f] + 16);
+        o_offs[f] = at; at = align256(at + 8 * (n + 1));
+    }
+    DeviceGuard g(ctx->device);
+    if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
+    int rc = ensure_pool(ctx, at);
+    if (rc != SYM_OK) return rc;
+    char* base = (char*)ctx->pool;
+    hipStream_t s = ctx->stream;
+    hipError_t e = hipSuccess;
+    if (in_len) e = hipMemcpyAsync(base + o_in, h_in + in_lo, in_len, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(base + o_rec, h_rec_off, 8 * (n + 1), hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return hip_fail(e, "sym_decode_host H2D");
+    int32_t* d_fixed[2] = {nullptr, nullptr};
+    uint8_t* d_bytes[2] = {nullptr, nullptr};
+    uint64_t* d_offs[2] = {nullptr, nullptr};
+    for (int f = 0; f < lay.nfixed; ++f) d_fixed[f] = (int32_t*)(base + o_fixed[f]);
+    for (int f = 0; f < lay.nvar; ++f) {
+        d_bytes[f] = (uint8_t*)(base + o_bytes[f]);
+        d_offs[f] = (uint64_t*)(base + o_offs[f]);
+    }
+    rc = sym_decode(ctx, schema, n, (const uint8_t*)(base + o_in) - in_lo, (const uint64_t*)(base + o_rec), d_fixed,
+                    d_bytes, caps, d_offs, (uint8_t*)(base + o_status), s);
+    if (rc != SYM_OK) return rc;
+    for (int f = 0; f < lay.nvar && e == hipSuccess; ++f)
+        e = hipMemcpyAsync(h_offs[f], d_offs[f], 8 * (n + 1), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return hip_fail(e, "sym_decode_host D2H offsets");
+    rc = sym_ctx_check(ctx, s);
+    if (rc != SYM_OK) return rc;
+    for (int f = 0; f < lay.nfixed && e == hipSuccess; ++f)
+        e = hipMemcpyAsync(h_fixed[f], d_fixed[f], 4 * n, hipMemcpyDeviceToHost, s);
+    for (int f = 0; f < lay.nvar && e == hipSuccess; ++f)
+        if (h_offs[f][n]) e = hipMemcpyAsync(h_bytes[f], d_bytes[f], h_offs[f][n], hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(h_status, base + o_status, n, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    return e == hipSuccess ? SYM_OK : hip_fail(e, "sym_decode_host D2H");
+}
+
+}  // extern "C"

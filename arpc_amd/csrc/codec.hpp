@@ -1,0 +1,60 @@
+// codec.hpp -- internal interface between the C ABI (capi.cpp) and the gfx950 kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace symhip {
+
+constexpr int kMaxFixed = 2;
+constexpr int kMaxVar = 2;
+
+// Records per workgroup tile (one record per thread in the per-record phases).
+constexpr int kTile = 256;
+
+struct Layout {
+    int nfixed;
+    int nvar;
+};
+
+struct EncodeParams {
+    Layout lay;
+    uint64_t n;
+    const int32_t* fixed[kMaxFixed];
+    const uint8_t* bytes[kMaxVar];
+    const uint64_t* offs[kMaxVar];
+    uint32_t service_id;
+    uint32_t method_id;
+    uint8_t* out;
+    uint64_t* out_off;
+};
+
+struct DecodeParams {
+    Layout lay;
+    uint64_t n;
+    const uint8_t* in;
+    const uint64_t* rec_off;
+    int32_t* fixed[kMaxFixed];
+    uint8_t* bytes[kMaxVar];
+    uint64_t cap[kMaxVar];
+    uint64_t* offs[kMaxVar];
+    uint8_t* status;
+    void* ws;       // decode_workspace_bytes() bytes, zeroed by launch_decode on the stream
+    unsigned* err;  // persistent device error word (kErr* bits), cleared by the host
+};
+
+// Device workspace for the single-pass decode scan: [0,16) tile ticket, then per var
+// field one u64 look-back word per tile.  Zeroed (as one block from its start) per call.
+struct DecodeWsHeader {
+    unsigned int ticket;
+    unsigned int pad[3];
+};
+constexpr unsigned kErrCapacity = 1u;
+constexpr unsigned kErrTimeout = 2u;
+
+size_t decode_workspace_bytes(int nvar, uint64_t n);
+
+hipError_t launch_encode(const EncodeParams& p, hipStream_t stream);
+hipError_t launch_decode(const DecodeParams& p, hipStream_t stream);
+
+}  // namespace symhip

@@ -1,0 +1,161 @@
+// device_util.hpp -- byte-shuffle primitives for the gfx950 Symphony kernels.
+//
+// The codec is an HBM-bound byte shuffle: records start at arbitrary byte offsets,
+// so every output 16-byte chunk is assembled in registers from (a) aligned 16-byte
+// global loads funnel-shifted with v_alignbyte_b32 and (b) header bytes synthesized
+// per record and staged in LDS.  No byte-granular global stores except at the two
+// edges of a workgroup's output range.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace symhip {
+
+typedef uint32_t u32;
+typedef uint64_t u64;
+typedef int64_t i64;
+
+// Explicit global address space so loads/stores lower to global_* (not flat_*).
+typedef u32 u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const u32x4 gc_u4;
+typedef __attribute__((address_space(1))) const u32 gc_u32;
+typedef __attribute__((address_space(1))) const uint8_t gc_u8;
+typedef __attribute__((address_space(1))) u32x4 g_u4;
+typedef __attribute__((address_space(1))) uint8_t g_u8;
+
+__device__ __forceinline__ u32 alignbyte(u32 hi, u32 lo, u32 sh) { return __builtin_amdgcn_alignbyte(hi, lo, sh); }
+
+// Mask selecting chunk bytes [lo, hi) inside dword k (lo, hi in [-inf, +inf], clamped).
+__device__ __forceinline__ u32 dword_mask(int lo, int hi, int k) {
+    const int a = min(max(lo - 4 * k, 0), 4);
+    const int b = min(max(hi - 4 * k, 0), 4);
+    const u64 m = ((1ull << (8 * b)) - 1ull) & ~((1ull << (8 * a)) - 1ull);
+    return (u32)m;
+}
+
+// OR into r the chunk bytes t in [t_lo, t_hi) (0 <= t_lo < t_hi <= 16) taken from
+// global memory at X + t.  Only the aligned 16-byte blocks that hold at least one
+// of those bytes are loaded, so a caller whose [X+t_lo, X+t_hi) lies inside a
+// buffer never touches memory past that buffer's last 16-byte block.
+__device__ __forceinline__ void or_window_global(uintptr_t X, int t_lo, int t_hi, u32 r[4]) {
+    const uintptr_t B0 = X & ~(uintptr_t)15;
+    u32x4 a = {0, 0, 0, 0}, b = {0, 0, 0, 0};
+    if (X + (uintptr_t)t_lo < B0 + 16) a = *(gc_u4*)B0;
+    if (X + (uintptr_t)t_hi > B0 + 16) b = *(gc_u4*)(B0 + 16);
+    const u32 s = (u32)(X & 15);
+    const u32 d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    // Two-stage dword barrel shift by s>>2 written as bit-selects (v_bfi_b32): a
+    // `c ? d[k+2] : d[k]` form gets folded into a dynamic index and spilled to scratch.
+    const u32 m2 = (s & 8) ? ~0u : 0u, m1 = (s & 4) ? ~0u : 0u;
+    u32 e[6], f[5];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) e[k] = (d[k + 2] & m2) | (d[k] & ~m2);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) f[k] = (e[k + 1] & m1) | (e[k] & ~m1);
+    const u32 sh = s & 3;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r[k] |= alignbyte(f[k + 1], f[k], sh) & dword_mask(t_lo, t_hi, k);
+}
+
+// OR into r the 16 bytes of an LDS byte image starting at byte address `addr`
+// (dword-aligned reads + alignbyte).  Callers keep the image zero outside the
+// bytes they want, so no mask is needed.
+__device__ __forceinline__ void or_window_lds(const u32* img, int addr, u32 r[4]) {
+    const int q = addr >> 2;
+    const u32 sh = (u32)addr & 3u;
+    u32 d[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) d[k] = img[q + k];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r[k] |= alignbyte(d[k + 1], d[k], sh);
+}
+
+// OR a little-endian u32 into chunk bytes [t, t+4) clipped to [0, 16); t in (-4, 16).
+__device__ __forceinline__ void or_u32_at(u32 v, int t, u32 r[4]) {
+    const u64 vv = (u64)v << 32;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int sh = t - 4 * k;  // byte position of v's byte 0 relative to dword k
+        if (sh > -4 && sh < 4) r[k] |= (u32)(vv >> (32 - 8 * sh));
+    }
+}
+
+// Compile-time-positioned byte writes into a small dword image.
+template <int POS>
+__device__ __forceinline__ void img_put_u32(u32* h, u32 v) {
+    constexpr int q = POS >> 2, sh = (POS & 3) * 8;
+    h[q] |= v << sh;
+    if constexpr (sh != 0) h[q + 1] |= v >> (32 - sh);
+}
+template <int POS>
+__device__ __forceinline__ void img_put_u8(u32* h, u32 v) {
+    h[POS >> 2] |= (v & 0xffu) << ((POS & 3) * 8);
+}
+
+__device__ __forceinline__ uint8_t chunk_byte(const u32 r[4], int t) {
+    const u32 m1 = t >= 4 ? ~0u : 0u, m2 = t >= 8 ? ~0u : 0u, m3 = t >= 12 ? ~0u : 0u;
+    u32 w = (r[1] & m1) | (r[0] & ~m1);
+    w = (r[2] & m2) | (w & ~m2);
+    w = (r[3] & m3) | (w & ~m3);
+    return (uint8_t)(w >> ((t & 3) * 8));
+}
+
+// Store a 16-byte chunk at dst (absolute, 16-byte aligned) keeping only the bytes
+// whose position P+t lies in [lo, hi).  Full chunks use one global_store_dwordx4;
+// the partial chunks at a workgroup's range edges fall back to byte stores.
+__device__ __forceinline__ void store_chunk(uint8_t* base, i64 P, i64 lo, i64 hi, const u32 r[4]) {
+    if (P >= lo && P + 16 <= hi) {
+        *(g_u4*)(base + P) = u32x4{r[0], r[1], r[2], r[3]};
+    } else {
+        for (int t = 0; t < 16; ++t) {
+            const i64 q = P + t;
+            if (q >= lo && q < hi) *(g_u8*)(base + q) = chunk_byte(r, t);
+        }
+    }
+}
+
+// Largest j in [0, cnt) with a[j] <= key (a ascending, a[0] <= key); cnt <= 256.
+__device__ __forceinline__ int lds_search_256(const u64* a, int cnt, u64 key) {
+    int j = 0;
+#pragma unroll
+    for (int step = 128; step > 0; step >>= 1) {
+        const int c = j + step;
+        if (c < cnt && a[c] <= key) j = c;
+    }
+    return j;
+}
+
+// Unaligned reads inside a record: only dwords holding at least one of the four
+// requested bytes are touched.
+__device__ __forceinline__ u32 ld_u8(uintptr_t p) { return *(gc_u8*)p; }
+__device__ __forceinline__ u32 ld_u32(uintptr_t p) {
+    const uintptr_t a = p & ~(uintptr_t)3;
+    const u32 sh = (u32)(p & 3);
+    const u32 lo = *(gc_u32*)a;
+    const u32 hi = sh ? *(gc_u32*)(a + 4) : 0u;
+    return alignbyte(hi, lo, sh);
+}
+
+// 64-lane inclusive scan of a u64 (two 32-bit shuffles per step).
+__device__ __forceinline__ u64 wave_incl_scan_u64(u64 v, int lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const u32 lo = __shfl_up((u32)v, d, 64);
+        const u32 hi = __shfl_up((u32)(v >> 32), d, 64);
+        if (lane >= d) v += ((u64)hi << 32) | lo;
+    }
+    return v;
+}
+
+__device__ __forceinline__ u64 wave_sum_u64(u64 v) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) {
+        const u32 lo = __shfl_xor((u32)v, d, 64);
+        const u32 hi = __shfl_xor((u32)(v >> 32), d, 64);
+        v += ((u64)hi << 32) | lo;
+    }
+    return v;
+}
+
+}  // namespace symhip

@@ -1,0 +1,113 @@
+"""Seeded synthetic record batches for tests and bench.py.
+
+Bytes are splitmix64 output (uniform 0-255): Symphony stores arbitrary bytes with no
+UTF-8 check (kv.syn.go:725), so random bytes exercise the same path as text.
+
+Field f of a batch draws its bytes from splitmix64 seeded with `seed + 0x100000000*(f+1)`
+and its lengths (when variable) from the stream seeded with `seed + 0x10000*(f+1)`.
+Config seeds: 0x5EED0001 (config 2, K=64/V=256), 0x5EED0002 (config 3, log-uniform
+V in [16, 4096]), 0x5EED0003+g (config 4 shard g).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import schemas
+
+GAMMA = np.uint64(0x9E3779B97F4A7C15)
+M1 = np.uint64(0xBF58476D1CE4E5B9)
+M2 = np.uint64(0x94D049BB133111EB)
+
+
+def splitmix64(seed: int, count: int) -> np.ndarray:
+    """`count` outputs of splitmix64 started at `seed` (state advances by GAMMA before each output)."""
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed & 0xFFFFFFFFFFFFFFFF) + (np.arange(1, count + 1, dtype=np.uint64) * GAMMA)
+        z = (z ^ (z >> np.uint64(30))) * M1
+        z = (z ^ (z >> np.uint64(27))) * M2
+        return z ^ (z >> np.uint64(31))
+
+
+def random_bytes(seed: int, nbytes: int) -> np.ndarray:
+    words = splitmix64(seed, (nbytes + 7) // 8)
+    return words.view(np.uint8)[:nbytes].copy()
+
+
+def lengths(spec, n: int, seed: int) -> np.ndarray:
+    """spec: int (every record), ("uniform", lo, hi) inclusive, ("loguniform", lo, hi) = floor(exp(U(ln lo, ln(hi+1))))."""
+    if isinstance(spec, (int, np.integer)):
+        return np.full(n, int(spec), dtype=np.uint64)
+    kind, lo, hi = spec
+    u = (splitmix64(seed, n) >> np.uint64(11)).astype(np.float64) * (1.0 / (1 << 53))
+    if kind == "uniform":
+        return np.minimum(lo + np.floor(u * (hi - lo + 1)), hi).astype(np.uint64)
+    if kind == "loguniform":
+        v = np.floor(np.exp(np.log(lo) + u * (np.log(hi + 1) - np.log(lo))))
+        return np.clip(v, lo, hi).astype(np.uint64)
+    raise ValueError(spec)
+
+
+@dataclass
+class Batch:
+    schema: schemas.Schema
+    fixed: list = field(default_factory=list)  # int32 [n] per fixed field
+    var: list = field(default_factory=list)    # (u8 bytes, u64 offs[n+1]) per var field
+
+    @property
+    def n(self) -> int:
+        return len(self.var[0][1]) - 1 if self.var else len(self.fixed[0])
+
+    def encoded_size(self) -> int:
+        return self.n * self.schema.overhead + sum(int(o[-1] - o[0]) for _, o in self.var)
+
+    def payload_bytes(self) -> int:
+        return sum(int(o[-1] - o[0]) for _, o in self.var) + 4 * self.n * self.schema.nfixed
+
+
+def make_batch(schema: str, n: int, lens: tuple, seed: int, **_ignored) -> Batch:
+    s = schemas.BY_NAME[schema]
+    fixed = [splitmix64(seed + 0x1000 * (f + 1), n).astype(np.uint32).view(np.int32) for f in range(s.nfixed)]
+    var = []
+    for f in range(s.nvar):
+        ln = lengths(lens[f], n, seed + 0x10000 * (f + 1))
+        offs = np.zeros(n + 1, dtype=np.uint64)
+        np.cumsum(ln, out=offs[1:])
+        var.append((random_bytes(seed + 0x100000000 * (f + 1), int(offs[-1])), offs))
+    return Batch(s, fixed, var)
+
+
+def from_records(schema: str, records) -> Batch:
+    """records: iterable of (fixed tuple, var tuple of bytes)."""
+    s = schemas.BY_NAME[schema]
+    records = list(records)
+    fixed = [np.array([r[0][f] for r in records], dtype=np.int32) for f in range(s.nfixed)]
+    var = []
+    for f in range(s.nvar):
+        vals = [bytes(r[1][f]) for r in records]
+        offs = np.zeros(len(vals) + 1, dtype=np.uint64)
+        np.cumsum([len(v) for v in vals], out=offs[1:])
+        var.append((np.frombuffer(b"".join(vals), dtype=np.uint8).copy(), offs))
+    return Batch(s, fixed, var)
+
+
+# Configs of BASELINE.json (record counts as there) and small golden corpora.
+CONFIG2 = dict(schema="kv_set_request", n=1 << 20, lens=(64, 256), seed=0x5EED0001)
+CONFIG3 = dict(schema="kv_set_request", n=1 << 20, lens=(64, ("loguniform", 16, 4096)), seed=0x5EED0002)
+
+
+def config4_shard(g: int, records_per_gpu: int = 1 << 23) -> dict:
+    return dict(schema="kv_set_request", n=records_per_gpu, lens=(64, 256), seed=0x5EED0003 + g)
+
+
+CORPORA = {
+    "set_64_256": dict(schema="kv_set_request", n=4096, lens=(64, 256), seed=0x5EED0001),
+    "set_mixed": dict(schema="kv_set_request", n=2048, lens=(64, ("loguniform", 16, 4096)), seed=0x5EED0002),
+    "set_tiny": dict(schema="kv_set_request", n=5000, lens=(("uniform", 0, 7), ("uniform", 0, 20)), seed=7),
+    "set_ids": dict(schema="kv_set_request", n=1000, lens=(64, 256), seed=11, service_id=1, method_id=2),
+    "get_64": dict(schema="kv_get_request", n=4096, lens=(64,), seed=0x5EED0004),
+    "get_response_mixed": dict(schema="kv_get_response", n=3000, lens=(("loguniform", 1, 2048),), seed=5),
+    "set_response_256": dict(schema="kv_set_response", n=3000, lens=(256,), seed=6),
+    "echo_small": dict(schema="echo_request", n=2048, lens=(("uniform", 0, 32), ("uniform", 0, 200)), seed=13),
+}

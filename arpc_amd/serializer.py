@@ -1,0 +1,255 @@
+"""Host-side mirror of aRPC's serializer plugin interface, backed by the HIP codec.
+
+Reference (Go):
+  type Serializer interface {                       pkg/serializer/serializer.go:3-6
+      Marshal(msg any) ([]byte, error)
+      Unmarshal(data []byte, out any) error
+  }
+  type SymphonyMessage interface {                  pkg/serializer/symphony.go:3-6
+      MarshalSymphony() ([]byte, error)
+      UnmarshalSymphony([]byte) error
+  }
+  SymphonySerializer.Marshal / Unmarshal            pkg/serializer/symphony.go:10-16
+
+Same names, argument meaning and error behaviour:
+  * marshal(msg) -> bytes; a message type the codec does not know raises TypeError
+    (Go panics on the failed type assertion, symphony.go:11).
+  * unmarshal(data, out) fills `out` in place like UnmarshalSymphony into a FRESH
+    struct (every aRPC call site passes one: server.go:152's `dec` target and the
+    client's resp), and raises SymphonyError carrying Go's exact error text.  As in
+    Go, int32 fields read before the error keep their values (echo.syn.go:223-231);
+    fields Go skips or never reaches come back zero / empty.
+  * The serializer is stateless from the caller's view and safe to share across
+    threads (one codec context per thread; pkg/serializer/symphony.go:8).
+
+The reference is one record per call.  `marshal_batch` / `unmarshal_batch` are the
+batched extension that the GPU is built for; the per-record methods run the same
+kernels on a batch of one (through the C ABI's host entry points).
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+from dataclasses import dataclass, fields
+
+import numpy as np
+
+from . import _native, schemas
+
+ERROR_TEXT = {
+    1: "invalid data: too short",
+    2: "invalid data: wrong public version",
+    3: "missing private segment",
+    4: "invalid data: too short for field",
+}
+
+
+class SymphonyError(ValueError):
+    """An UnmarshalSymphony error (Go `error` value) with its status code."""
+
+    def __init__(self, status: int):
+        super().__init__(ERROR_TEXT.get(status, f"status {status}"))
+        self.status = status
+
+
+def _b(v) -> bytes:
+    return v.encode() if isinstance(v, str) else bytes(v)
+
+
+# ----------------------------------------------------------------- message types
+# Go structs of the generated code (string fields hold arbitrary bytes; Symphony does
+# no UTF-8 check, kv.syn.go:725).  Field names follow the Go identifiers.
+@dataclass
+class GetRequest:
+    Key: bytes = b""
+    SCHEMA = schemas.KV_GET_REQUEST
+
+
+@dataclass
+class SetRequest:
+    Key: bytes = b""
+    Value: bytes = b""
+    SCHEMA = schemas.KV_SET_REQUEST
+
+
+@dataclass
+class GetResponse:
+    Value: bytes = b""
+    SCHEMA = schemas.KV_GET_RESPONSE
+
+
+@dataclass
+class SetResponse:
+    Value: bytes = b""
+    SCHEMA = schemas.KV_SET_RESPONSE
+
+
+@dataclass
+class EchoRequest:
+    Id: int = 0
+    Score: int = 0
+    Username: bytes = b""
+    Content: bytes = b""
+    SCHEMA = schemas.ECHO_REQUEST
+
+
+@dataclass
+class EchoResponse:
+    Id: int = 0
+    Score: int = 0
+    Username: bytes = b""
+    Content: bytes = b""
+    SCHEMA = schemas.ECHO_RESPONSE
+
+
+MESSAGE_TYPES = (GetRequest, SetRequest, GetResponse, SetResponse, EchoRequest, EchoResponse)
+
+
+def _schema_of(msg) -> schemas.Schema:
+    s = getattr(type(msg), "SCHEMA", None)
+    if s is None:
+        # Go: msg.(SymphonyMessage) panics for a non-Symphony type (symphony.go:11)
+        raise TypeError(f"{type(msg).__name__} is not a SymphonyMessage")
+    return s
+
+
+def _i32(v: int) -> int:
+    v = int(v) & 0xFFFFFFFF
+    return v - (1 << 32) if v & 0x80000000 else v
+
+
+# ----------------------------------------------------------------- host staging
+class _HostCodec(threading.local):
+    """Per-thread C-ABI context for the host entry points (sym_encode_host / sym_decode_host)."""
+
+    def __init__(self):
+        self.ctx = None
+        self.device = None
+
+    def get(self, device: int):
+        if self.ctx is None or self.device != device:
+            L = _native.lib()
+            h = ctypes.c_void_p()
+            _native.check(L.sym_ctx_create(device, ctypes.byref(h)), "sym_ctx_create")
+            self.ctx, self.device = h, device
+        return self.ctx
+
+
+def _np_ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def encode_columns_host(ctx, s: schemas.Schema, fixed_cols, var_cols, service_id=0, method_id=0):
+    """numpy columns -> (stream u8, offsets u64) via the HIP codec (H2D, kernel, D2H)."""
+    L = _native.lib()
+    n = len(var_cols[0][1]) - 1 if s.nvar else len(fixed_cols[0])
+    fixed_cols = [np.ascontiguousarray(c, dtype=np.int32) for c in fixed_cols]
+    vb = [np.ascontiguousarray(b, dtype=np.uint8) if len(b) else np.zeros(1, np.uint8) for b, _ in var_cols]
+    vo = [np.ascontiguousarray(o, dtype=np.uint64) for _, o in var_cols]
+    total = int(L.sym_encoded_size(s.schema_id, n, sum(int(o[-1] - o[0]) for o in vo)))
+    out = np.empty(max(1, total), dtype=np.uint8)
+    out_off = np.empty(n + 1, dtype=np.uint64)
+    rc = L.sym_encode_host(ctx, s.schema_id, n, _native.ptr_array([_np_ptr(c) for c in fixed_cols]),
+                           _native.ptr_array([_np_ptr(b) for b in vb]), _native.ptr_array([_np_ptr(o) for o in vo]),
+                           service_id, method_id, _np_ptr(out), _np_ptr(out_off))
+    _native.check(rc, f"sym_encode_host({s.name})")
+    return out[:total], out_off
+
+
+def decode_columns_host(ctx, s: schemas.Schema, data: np.ndarray, rec_off: np.ndarray):
+    L = _native.lib()
+    data = np.ascontiguousarray(data, dtype=np.uint8) if len(data) else np.zeros(1, np.uint8)
+    rec_off = np.ascontiguousarray(rec_off, dtype=np.uint64)
+    n = len(rec_off) - 1
+    cap = int(rec_off[-1] - rec_off[0]) if n else 0
+    fixed = [np.zeros(max(1, n), dtype=np.int32) for _ in range(s.nfixed)]
+    cols = [np.empty(max(1, cap), dtype=np.uint8) for _ in range(s.nvar)]
+    offs = [np.empty(n + 1, dtype=np.uint64) for _ in range(s.nvar)]
+    status = np.empty(max(1, n), dtype=np.uint8)
+    rc = L.sym_decode_host(ctx, s.schema_id, n, _np_ptr(data), _np_ptr(rec_off),
+                           _native.ptr_array([_np_ptr(c) for c in fixed]), _native.ptr_array([_np_ptr(c) for c in cols]),
+                           _native.u64_array([cap] * s.nvar), _native.ptr_array([_np_ptr(o) for o in offs]),
+                           _np_ptr(status))
+    _native.check(rc, f"sym_decode_host({s.name})")
+    return [f[:n] for f in fixed], [(cols[i], offs[i]) for i in range(s.nvar)], status[:n]
+
+
+# ----------------------------------------------------------------- the plugin
+class SymphonySerializer:
+    """GPU-backed drop-in for pkg/serializer.SymphonySerializer."""
+
+    def __init__(self, device: int = 0, service_id: int = 0, method_id: int = 0):
+        self.device = device
+        # MarshalSymphony writes zeros into [5:13]; the client patches IDs afterwards
+        # (client.go:267-271).  Nonzero IDs here produce the patched bytes directly.
+        self.service_id = service_id
+        self.method_id = method_id
+        self._tls = _HostCodec()
+
+    # --- pkg/serializer.Serializer -------------------------------------------------
+    def marshal(self, msg) -> bytes:
+        return self.marshal_batch([msg])[0]
+
+    def unmarshal(self, data: bytes, out) -> None:
+        err = self.unmarshal_batch([data], [out])[0]
+        if err is not None:
+            raise err
+
+    # --- batched extension ---------------------------------------------------------
+    def marshal_batch(self, msgs) -> list[bytes]:
+        msgs = list(msgs)
+        out: list = [None] * len(msgs)
+        for s, idx in _group_by_schema(msgs).items():
+            group = [msgs[i] for i in idx]
+            fixed = [np.array([_i32(getattr(m, f)) for m in group], dtype=np.int32) for f in s.fixed_fields]
+            var = []
+            for f in s.var_fields:
+                vals = [_b(getattr(m, f)) for m in group]
+                offs = np.zeros(len(vals) + 1, dtype=np.uint64)
+                np.cumsum([len(v) for v in vals], out=offs[1:])
+                var.append((np.frombuffer(b"".join(vals), dtype=np.uint8), offs))
+            data, off = encode_columns_host(self._tls.get(self.device), s, fixed, var, self.service_id,
+                                            self.method_id)
+            raw = data.tobytes()
+            for k, i in enumerate(idx):
+                out[i] = raw[int(off[k]):int(off[k + 1])]
+        return out
+
+    def unmarshal_batch(self, datas, outs) -> list:
+        """Fills each out in place; returns per record None or the SymphonyError Go would return."""
+        datas, outs = list(datas), list(outs)
+        if len(datas) != len(outs):
+            raise ValueError("datas and outs differ in length")
+        errs: list = [None] * len(outs)
+        for s, idx in _group_by_schema(outs).items():
+            blobs = [bytes(datas[i]) for i in idx]
+            rec_off = np.zeros(len(blobs) + 1, dtype=np.uint64)
+            np.cumsum([len(b) for b in blobs], out=rec_off[1:])
+            stream = np.frombuffer(b"".join(blobs), dtype=np.uint8)
+            fixed, var, status = decode_columns_host(self._tls.get(self.device), s, stream, rec_off)
+            for k, i in enumerate(idx):
+                m = outs[i]
+                for f, name in enumerate(s.fixed_fields):
+                    setattr(m, name, int(fixed[f][k]))
+                for f, name in enumerate(s.var_fields):
+                    col, off = var[f]
+                    setattr(m, name, col[int(off[k]):int(off[k + 1])].tobytes())
+                if status[k]:
+                    errs[i] = SymphonyError(int(status[k]))
+        return errs
+
+
+def _group_by_schema(msgs) -> dict:
+    groups: dict = {}
+    for i, m in enumerate(msgs):
+        groups.setdefault(_schema_of(m), []).append(i)
+    return groups
+
+
+def message_fields(msg) -> dict:
+    return {f.name: getattr(msg, f.name) for f in fields(msg)}
+
+
+__all__ = ["SymphonySerializer", "SymphonyError", "ERROR_TEXT", "GetRequest", "SetRequest", "GetResponse",
+           "SetResponse", "EchoRequest", "EchoResponse", "MESSAGE_TYPES", "encode_columns_host",
+           "decode_columns_host", "message_fields"]

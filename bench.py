@@ -1,0 +1,288 @@
+"""Symphony encode+decode throughput on MI355X (BASELINE.json metric), one process per GPU.
+
+One step = one device-resident Symphony encode of a record batch plus one decode of an
+encoded batch (BASELINE.json configs[1]: 2^20 kv-store SetRequest records, 64 B keys,
+256 B values, per GPU).  Inputs are resident in HBM before the timed region.  Four
+buffer sets rotate so the 256 MiB Infinity Cache cannot serve a step from a previous
+one: step s encodes set s%4 and decodes the stream encoded two steps earlier.
+
+  python bench.py [--gpus N --steps K --warmup W] [--config 2|3] [--records R]
+  torchrun --nproc-per-node N bench.py --gpus N ...   (weak scaling, no data-path collective)
+
+Prints ONE JSON line on rank 0.  `value` = algorithmic GB/s over all ranks (SURVEY.md
+section 8d: 694 B encode + 695 B decode per 64/256 record), timed with a barrier +
+device sync on both sides, max over ranks.  `roofline` uses HIP events on the stream
+the kernels run on; `cpu_baseline` times the C oracle (a restatement of the Go codec,
+single thread) on a bounded sample on this host.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from arpc_amd import datagen, schemas  # noqa: E402
+from arpc_amd.codec import Codec, DecodedBatch, to_device  # noqa: E402
+
+METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
+NSETS = 4
+
+
+def alg_bytes(n: int, nvar: int, var_total: int, stream_total: int) -> tuple[int, int]:
+    """Algorithmic bytes of one encode and one decode launch."""
+    enc = var_total + 8 * nvar * n + stream_total + 8 * n
+    dec = stream_total + 8 * n + var_total + 8 * nvar * n + n
+    return enc, dec
+
+
+def dist_setup():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(x: float, world: int, dev) -> float:
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def workload(args, world, rank):
+    base = dict(datagen.CONFIG2 if args.config == 2 else datagen.CONFIG3)
+    if args.records:
+        base["n"] = args.records
+    if world > 1:  # config 4 sharding: one seeded contiguous shard per GPU
+        base["seed"] = 0x5EED0003 + rank if args.config == 2 else base["seed"] + 0x100 * rank
+    return base
+
+
+def cpu_baseline(kw: dict, seconds: float) -> dict:
+    """Time the CPU oracle (C restatement of the Go codec, 1 thread) on a bounded sample."""
+    from oracle import oracle
+    sample = dict(kw, n=min(kw["n"], 1 << 16))
+    b = datagen.make_batch(**sample)
+    s = b.schema
+    stream, off = oracle.encode_batch(b.fixed, b.var)  # warm
+    var_total = sum(int(o[-1] - o[0]) for _, o in b.var)
+    enc_b, dec_b = alg_bytes(b.n, s.nvar, var_total, int(off[-1]))
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        oracle.encode_batch(b.fixed, b.var)
+        oracle.decode_batch(s.nfixed, s.nvar, stream, off)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": round((enc_b + dec_b) * reps / el / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
+            "mrecords_per_s": round(2 * b.n * reps / el / 1e6, 4),
+            "sample": f"{b.n} {s.go_type} records of the same workload (seed {sample['seed']:#x}), "
+                      f"encode+decode x{reps} in {el:.1f} s by oracle/symphony_oracle.c (-O2, 1 thread): "
+                      "C restatement of the Go codec, not Go (no Go toolchain)"}
+
+
+def load_traffic(kernel: str):
+    """Per-launch HBM bytes of `kernel` from the committed PMC summary (profiles/), else None."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+        return d.get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")
+    except (ValueError, OSError):
+        return None
+
+
+def host_inclusive(codec: Codec, kw: dict, dev, steps: int) -> dict:
+    """Pinned host -> H2D -> encode -> D2H, then H2D -> decode -> D2H (serial, one stream)."""
+    b = datagen.make_batch(**kw)
+    s = b.schema
+    var_total = sum(int(o[-1] - o[0]) for _, o in b.var)
+    total = b.encoded_size()
+    h_var = [(torch.from_numpy(by).pin_memory(), torch.from_numpy(o.view(np.int64)).pin_memory()) for by, o in b.var]
+    h_out = torch.empty(total, dtype=torch.uint8).pin_memory()
+    h_off = torch.empty(b.n + 1, dtype=torch.int64).pin_memory()
+    d_var = [(torch.empty_like(x, device=dev), torch.empty_like(o, device=dev)) for x, o in h_var]
+    d_out = torch.empty(total, dtype=torch.uint8, device=dev)
+    d_off = torch.empty(b.n + 1, dtype=torch.int64, device=dev)
+    h_dec = [(torch.empty(int(o[-1]), dtype=torch.uint8).pin_memory(), torch.empty(b.n + 1, dtype=torch.int64).pin_memory())
+             for _, o in b.var]
+    dec = DecodedBatch(fixed=[], var=[(torch.empty(int(o[-1]), dtype=torch.uint8, device=dev),
+                                       torch.empty(b.n + 1, dtype=torch.int64, device=dev)) for _, o in b.var],
+                       status=torch.empty(b.n, dtype=torch.uint8, device=dev))
+    h_status = torch.empty(b.n, dtype=torch.uint8).pin_memory()
+
+    def one():
+        for (hx, ho), (dx, do) in zip(h_var, d_var):
+            dx.copy_(hx, non_blocking=True)
+            do.copy_(ho, non_blocking=True)
+        codec.encode(s, [], d_var, out=d_out, out_off=d_off)
+        h_out.copy_(d_out, non_blocking=True)
+        h_off.copy_(d_off, non_blocking=True)
+        d_out.copy_(h_out, non_blocking=True)
+        d_off.copy_(h_off, non_blocking=True)
+        codec.decode(s, d_out, d_off, outputs=dec)
+        for (hx, ho), (dx, do) in zip(h_dec, dec.var):
+            hx.copy_(dx, non_blocking=True)
+            ho.copy_(do, non_blocking=True)
+        h_status.copy_(dec.status, non_blocking=True)
+
+    one()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    enc_b, dec_b = alg_bytes(b.n, s.nvar, var_total, total)
+    return {"gbps_algorithmic": round((enc_b + dec_b) * steps / el / 1e9, 2),
+            "ms_per_step": round(el / steps * 1e3, 3),
+            "note": "pinned H2D + encode + D2H + H2D + decode + D2H, serial on one stream"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", type=int, default=2, choices=(2, 3))
+    ap.add_argument("--records", type=int, default=0, help="records per GPU (default: the config's 2^20)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
+    ap.add_argument("--host-steps", type=int, default=5, help="host-inclusive steps (0 = skip)")
+    args = ap.parse_args()
+
+    world, rank, local = dist_setup()
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    kw = workload(args, world, rank)
+    s = schemas.BY_NAME[kw["schema"]]
+    codec = Codec(dev)
+
+    # ---- synthetic inputs, resident in HBM: NSETS distinct buffer sets ----
+    b = datagen.make_batch(**kw)
+    n = b.n
+    var_total = sum(int(o[-1] - o[0]) for _, o in b.var)
+    total = b.encoded_size()
+    fixed0, var0 = to_device(b, dev)
+    del b
+    sets = []
+    for k in range(NSETS):
+        var_k = [((x ^ (0x3B * k)) if k else x, o) for x, o in var0]
+        sets.append(([f ^ k for f in fixed0], var_k))
+    enc = [(torch.empty(total, dtype=torch.uint8, device=dev), torch.empty(n + 1, dtype=torch.int64, device=dev))
+           for _ in range(NSETS)]
+    caps = [int(o[-1].item() - o[0].item()) for _, o in var0]
+    dec = [DecodedBatch(fixed=[torch.empty(n, dtype=torch.int32, device=dev) for _ in range(s.nfixed)],
+                        var=[(torch.empty(max(1, c), dtype=torch.uint8, device=dev),
+                              torch.empty(n + 1, dtype=torch.int64, device=dev)) for c in caps],
+                        status=torch.empty(n, dtype=torch.uint8, device=dev)) for _ in range(NSETS)]
+    codec.reserve(n)
+
+    ev = {"enc": [], "dec": []}
+
+    def step(i: int, timed: bool):
+        a, d = i % NSETS, (i + 2) % NSETS
+        fx, vr = sets[a]
+        if timed:
+            e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+            e0.record()
+        codec.encode(s, fx, vr, out=enc[a][0], out_off=enc[a][1])
+        if timed:
+            e1.record()
+        codec.decode(s, enc[d][0], enc[d][1], outputs=dec[d])
+        if timed:
+            e2.record()
+            ev["enc"].append((e0, e1))
+            ev["dec"].append((e1, e2))
+
+    for k in range(NSETS):  # every set encoded once before any decode reads it
+        fx, vr = sets[k]
+        codec.encode(s, fx, vr, out=enc[k][0], out_off=enc[k][1])
+    for i in range(args.warmup):
+        step(i, False)
+    codec.check()
+
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i, True)
+    torch.cuda.synchronize()
+    barrier(world)
+    elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
+    codec.check()
+    # correctness spot check of the last decode (outside the timed region)
+    d_last = (args.steps - 1 + 2) % NSETS
+    assert int(dec[d_last].status.sum().item()) == 0, "decode reported errors"
+    assert torch.equal(dec[d_last].var[-1][0][:caps[-1]], sets[d_last][1][-1][0]), "round trip mismatch"
+
+    enc_ms = float(np.mean([a.elapsed_time(b_) for a, b_ in ev["enc"]]))
+    dec_ms = float(np.mean([a.elapsed_time(b_) for a, b_ in ev["dec"]]))
+    enc_b, dec_b = alg_bytes(n, s.nvar, var_total, total)
+    value = world * (enc_b + dec_b) * args.steps / elapsed / 1e9
+    dom, dom_ms, dom_bytes = ("encode", enc_ms, enc_b) if enc_ms >= dec_ms else ("decode", dec_ms, dec_b)
+    kname = {"encode": f"encode_kernel<{s.nfixed}, {s.nvar}>", "decode": f"decode_kernel<{s.nfixed}, {s.nvar}>"}[dom]
+    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+    traffic = load_traffic(kname)
+
+    if rank != 0:
+        return
+    line = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": f"synthetic: splitmix64 bytes, seed {kw['seed']:#x}"
+                + (" + rank (config 4 shard seeds)" if world > 1 else "") + f"; {NSETS} rotating buffer sets",
+        "config": {"workload": ("config2: kv-store SetRequest K=64 B, V=256 B" if args.config == 2 else
+                                "config3: kv-store SetRequest K=64 B, V log-uniform 16-4096 B")
+                   + ", device-resident encode+decode",
+                   "records_per_gpu": n, "global_records": n * world, "parallelism": f"shard{world}",
+                   "bytes_per_record_algorithmic": round((enc_b + dec_b) / n, 3)},
+        "mrecords_per_s": round(world * 2 * n * args.steps / elapsed / 1e6, 2),
+        "wire_gbps": round(world * 2 * total * args.steps / elapsed / 1e9, 2),
+        "kernels": {"encode": {"avg_ms": round(enc_ms, 4), "alg_bytes": enc_b,
+                               "gbps": round(enc_b / enc_ms / 1e6, 1)},
+                    "decode": {"avg_ms": round(dec_ms, 4), "alg_bytes": dec_b,
+                               "gbps": round(dec_b / dec_ms / 1e6, 1)}},
+        "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic},
+    }
+    if world == 1 and args.host_steps > 0:
+        line["host_inclusive"] = host_inclusive(codec, kw, dev, args.host_steps)
+    if world == 1 and args.cpu_seconds > 0:
+        line["cpu_baseline"] = cpu_baseline(kw, args.cpu_seconds)
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,160 @@
+/*
+ * symphony_hip.h -- C ABI of the MI355X (gfx950) batched Symphony codec.
+ *
+ * This is the drop-in boundary for aRPC's serializer hot path.  The reference
+ * interface it replaces is the per-record Go plugin
+ *
+ *   type Serializer interface {                     pkg/serializer/serializer.go:3-6
+ *       Marshal(msg any) ([]byte, error)
+ *       Unmarshal(data []byte, out any) error
+ *   }
+ *   SymphonySerializer.Marshal   -> msg.(SymphonyMessage).MarshalSymphony()     pkg/serializer/symphony.go:10-12
+ *   SymphonySerializer.Unmarshal -> out.(SymphonyMessage).UnmarshalSymphony()   pkg/serializer/symphony.go:14-16
+ *
+ * whose byte work lives in the generated per-schema methods, e.g.
+ * (*SetRequest).MarshalSymphony / UnmarshalSymphony
+ * (benchmark/kv-store-symphony/symphony/kv.syn.go:611-678 / :680-745).
+ *
+ * The reference has no batch API; this ABI is the batched, device-resident form of
+ * those methods (one call = n records).  A cgo binding a maintainer would add is
+ * shown in INTEGRATION.md.  Only C types cross the boundary: plain pointers, sizes
+ * and a `void*` HIP stream (NULL = the legacy default stream).
+ *
+ * Column layout (struct-of-arrays, caller-owned device memory):
+ *   string/bytes field f: a packed byte column `bytes` plus `offs[n+1]` (u64);
+ *     record i's value is bytes[offs[i] .. offs[i+1]).  offs[0] need not be 0.
+ *   int32 field: an int32 column of n values.
+ *   encoded stream: `out` plus `out_off[n+1]`; record i is out[out_off[i] .. out_off[i+1]),
+ *     out_off[0] = 0 on encode; rec_off[0] may be nonzero on decode.
+ * Decode writes packed columns with offs[0] = 0.
+ *
+ * Byte parity: with service_id = method_id = 0 the encoded bytes equal the
+ * reference MarshalSymphony output; nonzero IDs reproduce the client's on-wire
+ * bytes after its in-place patch of [5:13] (pkg/rpc/client.go:267-271).
+ * Decode follows UnmarshalSymphony into a fresh struct: skipped fields decode as
+ * empty, and the per-record status says which error Go would have returned.
+ *
+ * Memory rules: every device pointer must be readable up to the 16-byte boundary
+ * past its last byte (any hipMalloc / torch allocation is).  Kernels never write
+ * outside the bytes the call defines.
+ *
+ * Threading: a sym_ctx owns a decode workspace; one ctx must not run two calls
+ * concurrently.  Create one ctx per host thread / stream.  All entry points are
+ * asynchronous on `stream` except the *_host variants and sym_ctx_check.
+ */
+#ifndef SYMPHONY_HIP_H
+#define SYMPHONY_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SYMPHONY_HIP_ABI_VERSION 1
+
+/* Return codes (0 = ok, negative = error); text via sym_last_error(). */
+#define SYM_OK 0
+#define SYM_ERR_INVALID (-1)  /* bad argument */
+#define SYM_ERR_HIP (-2)      /* HIP runtime error */
+#define SYM_ERR_NOMEM (-3)    /* device / pinned allocation failed */
+#define SYM_ERR_CAPACITY (-4) /* a decode output column was too small (reported by sym_ctx_check) */
+#define SYM_ERR_DEVICE (-5)   /* kernel-side fault report, e.g. look-back timeout (sym_ctx_check) */
+
+/* Per-record decode status, the error UnmarshalSymphony would return
+ * (benchmark/kv-store-symphony/symphony/kv.syn.go:681-698; examples/echo_symphony/symphony/echo.syn.go:223-231). */
+#define SYM_STATUS_OK 0
+#define SYM_STATUS_TOO_SHORT 1        /* "invalid data: too short"           */
+#define SYM_STATUS_BAD_VERSION 2      /* "invalid data: wrong public version" */
+#define SYM_STATUS_NO_PRIVATE 3       /* "missing private segment"           */
+#define SYM_STATUS_FIELD_TOO_SHORT 4  /* "invalid data: too short for field" (int32 fields) */
+
+/* Flat schemas on the hot path: nfixed int32 fields followed by nvar string fields. */
+#define SYM_SCHEMA_KV_GET_REQUEST 0  /* GetRequest{Key}        kv.syn.go:74-185   (0 fixed, 1 var) */
+#define SYM_SCHEMA_KV_SET_REQUEST 1  /* SetRequest{Key,Value}  kv.syn.go:611-745  (0 fixed, 2 var) */
+#define SYM_SCHEMA_KV_GET_RESPONSE 2 /* GetResponse{Value}     kv.syn.go:333-444  (0 fixed, 1 var) */
+#define SYM_SCHEMA_KV_SET_RESPONSE 3 /* SetResponse{Value}     kv.syn.go:963-1074 (0 fixed, 1 var) */
+#define SYM_SCHEMA_ECHO_REQUEST 4    /* EchoRequest{Id,Score,Username,Content} echo.syn.go:111-263 (2 fixed, 2 var) */
+#define SYM_SCHEMA_ECHO_RESPONSE 5   /* EchoResponse, same fields as EchoRequest (examples/echo_symphony/symphony/echo.proto) */
+#define SYM_SCHEMA_COUNT 6
+
+typedef struct sym_ctx sym_ctx;
+
+/* ---- context ---------------------------------------------------------------- */
+int sym_abi_version(void);
+const char* sym_last_error(void); /* thread-local text of the last error */
+int sym_ctx_create(int device, sym_ctx** out_ctx);
+int sym_ctx_destroy(sym_ctx* ctx);
+/* Pre-size the decode workspace for up to max_records per call (so later calls never allocate). */
+int sym_ctx_reserve(sym_ctx* ctx, uint64_t max_records);
+/* Synchronize `stream` and report device-side errors of this ctx's calls since the last check
+ * (SYM_ERR_CAPACITY, SYM_ERR_DEVICE); clears them. */
+int sym_ctx_check(sym_ctx* ctx, void* stream);
+
+/* ---- schema metadata (host-side, no GPU needed) -------------------------------- */
+int sym_schema_info(int schema, int* nfixed, int* nvar);
+/* Fixed bytes per record: 14 + 4*(nfixed+nvar) + 4*nvar.  A record's size is that plus its string lengths. */
+uint64_t sym_record_overhead(int schema);
+/* Encoded stream size for n records whose string fields total var_total bytes (all fields). */
+uint64_t sym_encoded_size(int schema, uint64_t n, uint64_t var_total);
+
+/* ---- generic columnar entry points (device memory, async on stream) ------------ */
+/* d_fixed: nfixed int32 column pointers; d_bytes/d_offs: nvar column pointers (host arrays of device pointers).
+ * Replaces n calls of MarshalSymphony (kv.syn.go:611-678) + the client ID patch (client.go:267-271). */
+int sym_encode(sym_ctx* ctx, int schema, uint64_t n, const int32_t* const* d_fixed, const uint8_t* const* d_bytes,
+               const uint64_t* const* d_offs, uint32_t service_id, uint32_t method_id, uint8_t* d_out,
+               uint64_t* d_out_off, void* stream);
+/* Replaces n calls of UnmarshalSymphony into fresh structs (kv.syn.go:680-745).  caps[f] = capacity in bytes of
+ * d_bytes[f]; rec_off[n]-rec_off[0] always suffices.  d_status: n bytes (SYM_STATUS_*). */
+int sym_decode(sym_ctx* ctx, int schema, uint64_t n, const uint8_t* d_in, const uint64_t* d_rec_off,
+               int32_t* const* d_fixed, uint8_t* const* d_bytes, const uint64_t* caps, uint64_t* const* d_offs,
+               uint8_t* d_status, void* stream);
+
+/* ---- typed entry points (what a cgo binding calls) ------------------------------ */
+/* (*SetRequest).MarshalSymphony x n -- kv.syn.go:611-678 */
+int sym_encode_kv_set(sym_ctx* ctx, const uint8_t* d_key, const uint64_t* d_key_off, const uint8_t* d_val,
+                      const uint64_t* d_val_off, uint64_t n, uint32_t service_id, uint32_t method_id,
+                      uint8_t* d_out, uint64_t* d_out_off, void* stream);
+/* (*GetRequest).MarshalSymphony x n -- kv.syn.go:74-132 */
+int sym_encode_kv_get(sym_ctx* ctx, const uint8_t* d_key, const uint64_t* d_key_off, uint64_t n,
+                      uint32_t service_id, uint32_t method_id, uint8_t* d_out, uint64_t* d_out_off, void* stream);
+/* (*GetResponse|*SetResponse).MarshalSymphony x n -- kv.syn.go:333-391 / :963-1021 */
+int sym_encode_kv_response(sym_ctx* ctx, int schema, const uint8_t* d_val, const uint64_t* d_val_off, uint64_t n,
+                           uint32_t service_id, uint32_t method_id, uint8_t* d_out, uint64_t* d_out_off,
+                           void* stream);
+/* (*EchoRequest).MarshalSymphony x n -- echo.syn.go:111-184 */
+int sym_encode_echo(sym_ctx* ctx, const int32_t* d_id, const int32_t* d_score, const uint8_t* d_user,
+                    const uint64_t* d_user_off, const uint8_t* d_content, const uint64_t* d_content_off, uint64_t n,
+                    uint32_t service_id, uint32_t method_id, uint8_t* d_out, uint64_t* d_out_off, void* stream);
+/* (*SetRequest).UnmarshalSymphony x n -- kv.syn.go:680-745 */
+int sym_decode_kv_set(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_off, uint64_t n, uint8_t* d_key,
+                      uint64_t key_cap, uint64_t* d_key_off, uint8_t* d_val, uint64_t val_cap, uint64_t* d_val_off,
+                      uint8_t* d_status, void* stream);
+/* (*GetRequest).UnmarshalSymphony x n -- kv.syn.go:134-185 */
+int sym_decode_kv_get(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_off, uint64_t n, uint8_t* d_key,
+                      uint64_t key_cap, uint64_t* d_key_off, uint8_t* d_status, void* stream);
+/* (*GetResponse|*SetResponse).UnmarshalSymphony x n -- kv.syn.go:393-444 / :1023-1074 */
+int sym_decode_kv_response(sym_ctx* ctx, int schema, const uint8_t* d_in, const uint64_t* d_rec_off, uint64_t n,
+                           uint8_t* d_val, uint64_t val_cap, uint64_t* d_val_off, uint8_t* d_status, void* stream);
+/* (*EchoRequest).UnmarshalSymphony x n -- echo.syn.go:186-263 */
+int sym_decode_echo(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_off, uint64_t n, int32_t* d_id,
+                    int32_t* d_score, uint8_t* d_user, uint64_t user_cap, uint64_t* d_user_off, uint8_t* d_content,
+                    uint64_t content_cap, uint64_t* d_content_off, uint8_t* d_status, void* stream);
+
+/* ---- host-memory entry points (synchronous) ------------------------------------- */
+/* Same contracts with every pointer in host memory.  Staged through the ctx's pinned buffers
+ * (H2D, kernel, D2H pipelined in chunks of records).  These are what the per-record Go
+ * Serializer adapter and the UDP buffers of pkg/transport hand over. */
+int sym_encode_host(sym_ctx* ctx, int schema, uint64_t n, const int32_t* const* h_fixed,
+                    const uint8_t* const* h_bytes, const uint64_t* const* h_offs, uint32_t service_id,
+                    uint32_t method_id, uint8_t* h_out, uint64_t* h_out_off);
+int sym_decode_host(sym_ctx* ctx, int schema, uint64_t n, const uint8_t* h_in, const uint64_t* h_rec_off,
+                    int32_t* const* h_fixed, uint8_t* const* h_bytes, const uint64_t* caps, uint64_t* const* h_offs,
+                    uint8_t* h_status);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SYMPHONY_HIP_H */

@@ -1,0 +1,123 @@
+"""ctypes wrapper around the CPU Symphony oracle (oracle/symphony_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py, as the checker.  The product (arpc_amd) never
+imports this module.
+
+The functions take numpy arrays in the same columnar layout as the C-ABI in
+include/symphony_hip.h: per var field a packed byte column plus a u64 offset
+array of n+1 entries; per fixed field an int32 column.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle_symphony.so")
+_lib = None
+
+STATUS_OK = 0
+STATUS_TOO_SHORT = 1
+STATUS_BAD_VERSION = 2
+STATUS_NO_PRIVATE = 3
+STATUS_FIELD_TOO_SHORT = 4
+
+
+def build() -> str:
+    """Compile the oracle with gcc (oracle/Makefile)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        u64, i32, vp = ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p
+        L.sym_oracle_record_size.restype = u64
+        L.sym_oracle_record_size.argtypes = [i32, i32, vp]
+        L.sym_oracle_marshal.restype = u64
+        L.sym_oracle_marshal.argtypes = [i32, i32, vp, vp, vp, ctypes.c_uint32, ctypes.c_uint32, vp]
+        L.sym_oracle_unmarshal.restype = i32
+        L.sym_oracle_unmarshal.argtypes = [i32, i32, vp, u64, vp, vp, vp]
+        L.sym_oracle_encode_batch.restype = u64
+        L.sym_oracle_encode_batch.argtypes = [i32, i32, u64, vp, vp, vp, ctypes.c_uint32, ctypes.c_uint32, vp, vp]
+        L.sym_oracle_decode_batch.restype = None
+        L.sym_oracle_decode_batch.argtypes = [i32, i32, u64, vp, vp, vp, vp, vp, vp]
+        _lib = L
+    return _lib
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data if a.size else 0
+
+
+def _ptr_array(arrays) -> ctypes.Array:
+    arr = (ctypes.c_void_p * max(1, len(arrays)))()
+    for i, a in enumerate(arrays):
+        arr[i] = _ptr(a)
+    return arr
+
+
+# ---------------------------------------------------------------- single record
+def marshal(fixed: list[int], fields: list[bytes], service_id: int = 0, method_id: int = 0) -> bytes:
+    """One record, as the generated MarshalSymphony (+ client ID patch)."""
+    nf, nv = len(fixed), len(fields)
+    fx = np.array(fixed, dtype=np.int32)
+    bufs = [np.frombuffer(f, dtype=np.uint8) if len(f) else np.zeros(1, np.uint8) for f in fields]
+    lens = np.array([len(f) for f in fields], dtype=np.uint64)
+    size = lib().sym_oracle_record_size(nf, nv, _ptr(lens))
+    out = np.zeros(size, dtype=np.uint8)
+    lib().sym_oracle_marshal(nf, nv, _ptr(fx), _ptr_array(bufs), _ptr(lens), service_id, method_id, _ptr(out))
+    return out.tobytes()
+
+
+def unmarshal(nfixed: int, nvar: int, data: bytes):
+    """One record into a fresh struct -> (status, fixed values, var field bytes)."""
+    buf = np.frombuffer(data, dtype=np.uint8) if len(data) else np.zeros(1, np.uint8)
+    fx = np.zeros(max(1, nfixed), dtype=np.int32)
+    pos = np.zeros(max(1, nvar), dtype=np.uint64)
+    ln = np.zeros(max(1, nvar), dtype=np.uint64)
+    st = lib().sym_oracle_unmarshal(nfixed, nvar, _ptr(buf), len(data), _ptr(fx), _ptr(pos), _ptr(ln))
+    fields = [bytes(data[int(pos[f]):int(pos[f]) + int(ln[f])]) for f in range(nvar)]
+    return st, [int(v) for v in fx[:nfixed]], fields
+
+
+# ---------------------------------------------------------------- batches
+def encode_batch(fixed_cols, var_cols, service_id: int = 0, method_id: int = 0):
+    """fixed_cols: list of int32 arrays [n]; var_cols: list of (bytes u8 array, offs u64 array [n+1]).
+
+    Returns (out u8 array, out_off u64 array [n+1])."""
+    nf, nv = len(fixed_cols), len(var_cols)
+    n = len(var_cols[0][1]) - 1 if nv else len(fixed_cols[0])
+    fixed_cols = [np.ascontiguousarray(c, dtype=np.int32) for c in fixed_cols]
+    vb = [np.ascontiguousarray(b, dtype=np.uint8) for b, _ in var_cols]
+    vo = [np.ascontiguousarray(o, dtype=np.uint64) for _, o in var_cols]
+    total = n * (14 + 4 * (nf + nv) + 4 * nv) + sum(int(o[-1] - o[0]) for o in vo)
+    out = np.zeros(max(1, total), dtype=np.uint8)
+    out_off = np.zeros(n + 1, dtype=np.uint64)
+    got = lib().sym_oracle_encode_batch(nf, nv, n, _ptr_array(fixed_cols), _ptr_array(vb), _ptr_array(vo),
+                                        service_id, method_id, _ptr(out), _ptr(out_off))
+    assert got == total, (got, total)
+    return out[:total], out_off
+
+
+def decode_batch(nfixed: int, nvar: int, data: np.ndarray, rec_off: np.ndarray):
+    """Returns (fixed_cols, [(bytes, offs)], status)."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    rec_off = np.ascontiguousarray(rec_off, dtype=np.uint64)
+    n = len(rec_off) - 1
+    cap = max(1, int(rec_off[-1] - rec_off[0]))
+    fixed = [np.zeros(max(1, n), dtype=np.int32) for _ in range(nfixed)]
+    cols = [np.zeros(cap, dtype=np.uint8) for _ in range(nvar)]
+    offs = [np.zeros(n + 1, dtype=np.uint64) for _ in range(nvar)]
+    status = np.zeros(max(1, n), dtype=np.uint8)
+    lib().sym_oracle_decode_batch(nfixed, nvar, n, _ptr(data) if data.size else 0, _ptr(rec_off),
+                                  _ptr_array(fixed), _ptr_array(cols), _ptr_array(offs), _ptr(status))
+    return ([f[:n] for f in fixed], [(cols[i][:int(offs[i][-1])], offs[i]) for i in range(nvar)], status[:n])
