@@ -7,6 +7,7 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -97,6 +98,11 @@ size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 }  // namespace
 
+int symhip::tuning_variant(const char* env_name) {
+    const char* v = getenv(env_name);
+    return v ? atoi(v) : 0;
+}
+
 extern "C" {
 
 int sym_abi_version(void) { return SYMPHONY_HIP_ABI_VERSION; }
@@ -153,6 +159,8 @@ int sym_ctx_check(sym_ctx* ctx, void* stream) {
     if (bits == 0) return SYM_OK;
     if ((e = hipMemset(ctx->err, 0, sizeof(bits))) != hipSuccess) return hip_fail(e, "clearing device error word");
     if (bits & symhip::kErrTimeout) return fail(SYM_ERR_DEVICE, "decode look-back timed out (device error bits 0x%x)", bits);
+    if (bits & symhip::kErrTooLarge)
+        return fail(SYM_ERR_INVALID, "64 consecutive records span >= 2 GiB; split the batch (device error bits 0x%x)", bits);
     return fail(SYM_ERR_CAPACITY, "decode output column capacity exceeded (device error bits 0x%x)", bits);
 }
 
@@ -201,6 +209,8 @@ int sym_encode(sym_ctx* ctx, int schema, uint64_t n, const int32_t* const* d_fix
     p.method_id = method_id;
     p.out = d_out;
     p.out_off = d_out_off;
+    p.err = ctx->err;
+    p.variant = symhip::tuning_variant("SYMHIP_ENCODE_VARIANT");
     DeviceGuard g(ctx->device);
     if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
     hipError_t e = symhip::launch_encode(p, (hipStream_t)stream);
@@ -243,6 +253,7 @@ int sym_decode(sym_ctx* ctx, int schema, uint64_t n, const uint8_t* d_in, const 
     p.status = d_status;
     p.ws = ctx->ws;
     p.err = ctx->err;
+    p.variant = symhip::tuning_variant("SYMHIP_DECODE_VARIANT");
     hipError_t e = symhip::launch_decode(p, (hipStream_t)stream);
     return e == hipSuccess ? SYM_OK : hip_fail(e, "decode launch");
 }

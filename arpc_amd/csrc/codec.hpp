@@ -27,6 +27,8 @@ struct EncodeParams {
     uint32_t method_id;
     uint8_t* out;
     uint64_t* out_off;
+    unsigned* err;  // persistent device error word (kErr* bits), cleared by the host
+    int variant;    // kernel tuning variant (tuning_variant("SYMHIP_ENCODE_VARIANT"))
 };
 
 struct DecodeParams {
@@ -41,6 +43,7 @@ struct DecodeParams {
     uint8_t* status;
     void* ws;       // decode_workspace_bytes() bytes, zeroed by launch_decode on the stream
     unsigned* err;  // persistent device error word (kErr* bits), cleared by the host
+    int variant;    // kernel tuning variant (tuning_variant("SYMHIP_DECODE_VARIANT"))
 };
 
 // Device workspace for the single-pass decode scan: [0,16) tile ticket, then per var
@@ -51,8 +54,13 @@ struct DecodeWsHeader {
 };
 constexpr unsigned kErrCapacity = 1u;
 constexpr unsigned kErrTimeout = 2u;
+constexpr unsigned kErrTooLarge = 4u;  // 64 consecutive records spanning >= 2 GiB
 
 size_t decode_workspace_bytes(int nvar, uint64_t n);
+
+// Kernel variant selected by an environment variable (0 = default); lets tools/kbench.py
+// compare variants inside one process.
+int tuning_variant(const char* env_name);
 
 hipError_t launch_encode(const EncodeParams& p, hipStream_t stream);
 hipError_t launch_decode(const DecodeParams& p, hipStream_t stream);

@@ -34,6 +34,22 @@ __device__ __forceinline__ u32 dword_mask(int lo, int hi, int k) {
     return (u32)m;
 }
 
+// Bytes [s, s+16) of the 32-byte concatenation a|b (s in [0,16)).  The dword barrel
+// shift by s>>2 is written as bit-selects (v_bfi_b32): a `c ? d[k+2] : d[k]` form gets
+// folded into a dynamic index and spilled to scratch.
+__device__ __forceinline__ void funnel16(const u32x4 a, const u32x4 b, u32 s, u32 out[4]) {
+    const u32 d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    const u32 m2 = (s & 8) ? ~0u : 0u, m1 = (s & 4) ? ~0u : 0u;
+    u32 e[6], f[5];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) e[k] = (d[k + 2] & m2) | (d[k] & ~m2);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) f[k] = (e[k + 1] & m1) | (e[k] & ~m1);
+    const u32 sh = s & 3;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) out[k] = alignbyte(f[k + 1], f[k], sh);
+}
+
 // OR into r the chunk bytes t in [t_lo, t_hi) (0 <= t_lo < t_hi <= 16) taken from
 // global memory at X + t.  Only the aligned 16-byte blocks that hold at least one
 // of those bytes are loaded, so a caller whose [X+t_lo, X+t_hi) lies inside a
@@ -43,19 +59,47 @@ __device__ __forceinline__ void or_window_global(uintptr_t X, int t_lo, int t_hi
     u32x4 a = {0, 0, 0, 0}, b = {0, 0, 0, 0};
     if (X + (uintptr_t)t_lo < B0 + 16) a = *(gc_u4*)B0;
     if (X + (uintptr_t)t_hi > B0 + 16) b = *(gc_u4*)(B0 + 16);
-    const u32 s = (u32)(X & 15);
-    const u32 d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    // Two-stage dword barrel shift by s>>2 written as bit-selects (v_bfi_b32): a
-    // `c ? d[k+2] : d[k]` form gets folded into a dynamic index and spilled to scratch.
-    const u32 m2 = (s & 8) ? ~0u : 0u, m1 = (s & 4) ? ~0u : 0u;
-    u32 e[6], f[5];
+    u32 w[4];
+    funnel16(a, b, (u32)(X & 15), w);
 #pragma unroll
-    for (int k = 0; k < 6; ++k) e[k] = (d[k + 2] & m2) | (d[k] & ~m2);
+    for (int k = 0; k < 4; ++k) r[k] |= w[k] & dword_mask(t_lo, t_hi, k);
+}
+
+// The two aligned blocks an interior chunk (all 16 bytes at X valid) needs; the second
+// only when X is unaligned (so it holds valid bytes too).
+__device__ __forceinline__ void load_interior(uintptr_t X, u32x4& a, u32x4& b) {
+    const uintptr_t B0 = X & ~(uintptr_t)15;
+    a = *(gc_u4*)B0;
+    b = u32x4{0, 0, 0, 0};
+    if (X & 15) b = *(gc_u4*)(B0 + 16);
+}
+
+// Byte-unaligned 16-byte global load (gfx950 handles byte-aligned global_load_dwordx4 at
+// full rate; tools/ubench_unaligned.hip).  The caller guarantees [X, X+16) is readable.
+__device__ __forceinline__ u32x4 ld16u(uintptr_t X) { return *(gc_u4*)X; }
+
+// Byte-unaligned 16-byte LDS read (ds_read_b128 at any byte address).
+__device__ __forceinline__ u32x4 lds16u(const void* base, int byte_off) {
+    return *(const u32x4*)((const char*)base + byte_off);
+}
+
+// Chunk byte masks from a 17-entry table: lowmask[n] has bytes [0, n) set.
+struct MaskTable {
+    u32x4 lm[17];
+};
+__device__ __forceinline__ void mask_table_init(MaskTable& t, int tid) {
+    if (tid < 17) {
+        u32 w[4];
 #pragma unroll
-    for (int k = 0; k < 5; ++k) f[k] = (e[k + 1] & m1) | (e[k] & ~m1);
-    const u32 sh = s & 3;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) r[k] |= alignbyte(f[k + 1], f[k], sh) & dword_mask(t_lo, t_hi, k);
+        for (int k = 0; k < 4; ++k) w[k] = dword_mask(0, tid, k);
+        t.lm[tid] = u32x4{w[0], w[1], w[2], w[3]};
+    }
+}
+// bytes [lo, hi) of a chunk, lo/hi clamped to [0, 16]
+__device__ __forceinline__ u32x4 range_mask(const MaskTable& t, int lo, int hi) {
+    lo = min(max(lo, 0), 16);
+    hi = min(max(hi, 0), 16);
+    return t.lm[hi] & ~t.lm[lo];
 }
 
 // OR into r the 16 bytes of an LDS byte image starting at byte address `addr`
@@ -135,6 +179,42 @@ __device__ __forceinline__ u32 ld_u32(uintptr_t p) {
     const u32 lo = *(gc_u32*)a;
     const u32 hi = sh ? *(gc_u32*)(a + 4) : 0u;
     return alignbyte(hi, lo, sh);
+}
+
+// Broadcast lane 0's value as a provably wave-uniform (SGPR) value.
+__device__ __forceinline__ i64 uniform_i64(i64 x) {
+    const u32 lo = __builtin_amdgcn_readfirstlane((u32)(u64)x);
+    const u32 hi = __builtin_amdgcn_readfirstlane((u32)((u64)x >> 32));
+    return (i64)(((u64)hi << 32) | lo);
+}
+
+// Order LDS traffic between lanes of ONE wave (no workgroup barrier).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// 64-lane inclusive scan of a u32.
+__device__ __forceinline__ u32 wave_incl_scan_u32(u32 v, int lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const u32 t = __shfl_up(v, d, 64);
+        if (lane >= d) v += t;
+    }
+    return v;
+}
+
+// Largest j in [0, cnt) with a[j] <= key (a ascending, a[0] <= key); cnt <= 64.
+template <typename T>
+__device__ __forceinline__ int lds_search_64(const T* a, int cnt, T key) {
+    int j = 0;
+#pragma unroll
+    for (int step = 32; step > 0; step >>= 1) {
+        const int c = j + step;
+        if (c < cnt && a[c] <= key) j = c;
+    }
+    return j;
 }
 
 // 64-lane inclusive scan of a u64 (two 32-bit shuffles per step).
