@@ -6,16 +6,18 @@
 // generator's rules cmd/symphony-gen-arpc/protoc-gen-symphony/main.go:622-694, :734-793.
 //
 // Design (single pass, one tile of kWaveRecs=64 records per wave, decoupled look-back):
-//  * Waves take tiles in ticket order (atomic counter), so every tile a wave waits on is
-//    already held by a running wave; the 4 waves of a workgroup never synchronize.
+//  * Workgroups (16 waves, 1024 records) take look-back tiles in ticket order (one atomic
+//    per workgroup: a single counter word sustains only ~88 increments/us), so every tile a
+//    workgroup waits on is already held by a running workgroup.  Tiles of 1024 records keep
+//    the look-back shallow even when hundreds of workgroups start together.
 //  * Parse (lane = record): the record's first 48 bytes land in LDS with three byte-unaligned
 //    16-byte loads; Go's header checks and, per field, the table-entry / length-prefix bounds
 //    checks (64-bit arithmetic, as Go's int) read from there, or from global memory for
 //    offsets past the window.  Emits the status byte, int32 fields, and each string
 //    field's (source position, length).
-//  * Scan: 64-lane shuffle scan of the field lengths; the wave publishes its tile aggregate,
-//    looks back over predecessors' 8-byte {flag, value} words (agent-scope relaxed atomics;
-//    the word IS the flag) and publishes its inclusive prefix.
+//  * Scan: 64-lane DPP scan of the field lengths per wave, wave aggregates through LDS; wave 0
+//    publishes the tile aggregate, looks back over predecessors' 8-byte {flag, value} words
+//    (agent-scope relaxed atomics; the word IS the flag) and publishes the inclusive prefix.
 //  * Copy (lane = aligned 16-byte chunk of an output column, natural order): a chunk inside
 //    one field is one byte-unaligned 16-byte load from the record stream; chunks spanning
 //    field ends merge masked windows.  One global_store_dwordx4 per chunk; byte stores only
@@ -25,8 +27,9 @@
 
 namespace symhip {
 
-constexpr int kWaveRecs = 64;
-constexpr int kWaves = 4;
+constexpr int kWaveRecs = 64;                    // records per wave (parse / copy unit)
+constexpr int kWaves = 16;                       // waves per 1024-thread workgroup
+constexpr int kTileRecs = kWaveRecs * kWaves;    // records per look-back tile (one per workgroup)
 constexpr int kWin = 48;  // header bytes staged per record
 constexpr u64 kFlagAgg = 1ull << 62;
 constexpr u64 kFlagInc = 2ull << 62;
@@ -34,7 +37,7 @@ constexpr u64 kValMask = (1ull << 62) - 1;
 constexpr unsigned kSpinLimit = 1u << 22;
 
 size_t decode_workspace_bytes(int nvar, uint64_t n) {
-    const uint64_t tiles = (n + kWaveRecs - 1) / kWaveRecs;
+    const uint64_t tiles = (n + kTileRecs - 1) / kTileRecs;
     const size_t bytes = sizeof(DecodeWsHeader) + (size_t)nvar * tiles * sizeof(uint64_t);
     return (bytes + 15) & ~(size_t)15;
 }
@@ -82,27 +85,30 @@ struct alignas(16) DecWaveLds {
     uint8_t win[kWaveRecs * kWin];  // first kWin bytes of each record (parse)
     int dst[NV][kWaveRecs + 1];     // field start in the tile's column range; [cnt] = tile aggregate
     u64 src[NV][kWaveRecs];         // payload position in the input stream
+    u32 counts[64];                 // record starts per chunk of one copy step
 };
 
-template <int NF, int NV>
-__global__ __launch_bounds__(256) void decode_kernel(DecodeParams p) {
+// DIAG (timing diagnostics only, tools/kbench.py): 1 = skip the copy, 2 = skip the look-back.
+template <int NF, int NV, int DIAG>
+__global__ __launch_bounds__(1024) void decode_kernel(DecodeParams p) {
     __shared__ DecWaveLds<NV> lds_all[kWaves];
     __shared__ MaskTable masks;
-    mask_table_init(masks, threadIdx.x);
-    __syncthreads();  // the only workgroup barrier
+    __shared__ u64 s_wagg[NV][kWaves];  // wave aggregates
+    __shared__ u64 s_tile_prefix[NV];
+    __shared__ u32 s_ticket;
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     DecWaveLds<NV>& S = lds_all[wave];
-    const u64 ntiles = (p.n + kWaveRecs - 1) / kWaveRecs;
+    const u64 ntiles = (p.n + kTileRecs - 1) / kTileRecs;
     DecodeWsHeader* hdr = (DecodeWsHeader*)p.ws;
     u64* look = (u64*)((char*)p.ws + sizeof(DecodeWsHeader));
 
-    u32 ticket = 0;
-    if (lane == 0) ticket = atomicAdd(&hdr->ticket, 1u);
-    const u64 tile = (u64)__shfl((int)ticket, 0, 64);
-    if (tile >= ntiles) return;  // surplus wave of the last workgroup
-    const u64 r0 = tile * kWaveRecs;
-    const int cnt = (int)min((u64)kWaveRecs, p.n - r0);
+    if (threadIdx.x == 0) s_ticket = atomicAdd(&hdr->ticket, 1u);
+    mask_table_init(masks, threadIdx.x);
+    __syncthreads();
+    const u64 tile = (u64)__builtin_amdgcn_readfirstlane(s_ticket);  // grid size == ntiles
+    const u64 r0 = tile * kTileRecs + (u64)wave * kWaveRecs;
+    const int cnt = r0 < p.n ? (int)min((u64)kWaveRecs, p.n - r0) : 0;  // 0: wave past the end
 
     // ---------------- parse: Go's UnmarshalSymphony checks, one record per lane ----------------
     u64 flen[NV], fsrc[NV];
@@ -174,16 +180,44 @@ __global__ __launch_bounds__(256) void decode_kernel(DecodeParams p) {
 
     // ---------------- scan + look-back ----------------
     u64 prefix[NV], agg[NV], excl[NV];
+    // 32-bit DPP scan unless some field in the tile is >= 2^26 bytes (then 64-bit shuffles)
+    bool small = true;
+#pragma unroll
+    for (int f = 0; f < NV; ++f) small = small && flen[f] < (1u << 26);
+    const bool all_small = __ballot(!small) == 0;
 #pragma unroll
     for (int f = 0; f < NV; ++f) {
-        const u64 inc = wave_incl_scan_u64(flen[f], lane);
-        agg[f] = (u64)__shfl((long long)inc, 63, 64);
+        const u64 inc = all_small ? (u64)wave_incl_scan_u32_dpp((u32)flen[f]) : wave_incl_scan_u64(flen[f], lane);
+        agg[f] = (u64)uniform_i64((i64)__shfl((long long)inc, 63, 64));
         excl[f] = inc - flen[f];
     }
+    // tile scan: wave aggregates -> wave 0 looks back once for the whole workgroup
+    if (lane == 0) {
+#pragma unroll
+        for (int f = 0; f < NV; ++f) s_wagg[f][wave] = agg[f];
+    }
+    __syncthreads();
+    if (wave == 0) {
+#pragma unroll
+        for (int f = 0; f < NV; ++f) {
+            const u64 tile_agg = lane < kWaves ? s_wagg[f][lane] : 0;
+            const u64 tsum = (u64)uniform_i64((i64)wave_sum_u64(tile_agg));
+            u64 pre;
+            if constexpr (DIAG == 2) {
+                pre = tile * tsum;  // timing only: no look-back (offsets wrong unless tiles are equal)
+            } else {
+                pre = lookback(look + (u64)f * ntiles, tile, tsum, p.err, lane);
+            }
+            if (lane == 0) s_tile_prefix[f] = pre;
+        }
+    }
+    __syncthreads();
     bool too_large = false;
 #pragma unroll
     for (int f = 0; f < NV; ++f) {
-        prefix[f] = lookback(look + (u64)f * ntiles, tile, agg[f], p.err, lane);
+        u64 pre = s_tile_prefix[f];
+        for (int w = 0; w < wave; ++w) pre += s_wagg[f][w];
+        prefix[f] = (u64)uniform_i64((i64)pre);
         too_large |= agg[f] >= ((u64)1 << 31);
     }
     if (lane < cnt) {
@@ -198,6 +232,7 @@ __global__ __launch_bounds__(256) void decode_kernel(DecodeParams p) {
         if (lane == 0) atomicOr(p.err, kErrTooLarge);
         return;
     }
+    if constexpr (DIAG == 1) return;  // timing only: no copy
 #pragma unroll
     for (int f = 0; f < NV; ++f) {
         S.dst[f][lane] = (int)excl[f];  // lanes >= cnt hold the aggregate
@@ -207,6 +242,7 @@ __global__ __launch_bounds__(256) void decode_kernel(DecodeParams p) {
 #pragma unroll
         for (int f = 0; f < NV; ++f) S.dst[f][kWaveRecs] = (int)agg[f];
     }
+    S.counts[lane] = 0;
     wave_sync();
 
     // ---------------- copy: natural-order chunks of each output column ----------------
@@ -224,13 +260,31 @@ __global__ __launch_bounds__(256) void decode_kernel(DecodeParams p) {
         const int first = (int)(((C0 + mis) & ~(i64)15) - mis - C0);  // in (-16, 0]
         uint8_t* const out_t = p.bytes[f] + C0;
         const int* dst = S.dst[f];
-        for (int P = first + 16 * lane; P < lim; P += 16 * 64) {
-            const int j = lds_search_64(dst, cnt, max(P, 0));
+        // record-role registers: lane k = record k's column start (tile-relative)
+        const i64 my_d = lane < cnt ? (i64)excl[f] : ((i64)1 << 40);
+        for (int B = first; B < lim; B += 16 * 64) {  // wave-uniform loop
+            // Chunk l's record = (#records with start <= P_l) - 1.  Record k is first counted at
+            // chunk ceil((d_k - B)/16); short fields can put several starts in one chunk, so
+            // the marks are counts (LDS atomics) and a DPP scan turns them into prefix counts.
+            const i64 ck = (my_d - B + 15) >> 4;
+            const u64 before = __ballot(ck <= 0);
+            if (ck >= 1 && ck <= 63) atomicAdd(&S.counts[ck], 1u);
+            wave_sync();
+            const u32 c = S.counts[lane];
+            S.counts[lane] = 0;
+            const u32 inc = __ballot(c > 1) == 0
+                ? (u32)__builtin_amdgcn_mbcnt_hi((u32)(__ballot(c != 0) >> 32),
+                                                 __builtin_amdgcn_mbcnt_lo((u32)__ballot(c != 0), 0u)) + c
+                : wave_incl_scan_u32_dpp(c);
+            const int counted = (int)__popcll(before) + (int)inc;
+            const int j = counted > 0 ? counted - 1 : 0;  // 0 only for the chunk straddling the tile start
+            const int P = B + 16 * lane;
+            if (P >= lim) continue;
             const int dj = dst[j], Lj = dst[j + 1] - dj;
-            const uintptr_t Xj = (uintptr_t)(p.in + S.src[f][j]) + (uintptr_t)(i64)(P - dj);
             u32x4 r;
             if (P >= dj && P + 16 <= dj + Lj) {
-                r = ld16u(Xj);  // the whole chunk comes from one field: [Xj, Xj+16) is in the record
+                // the whole chunk comes from one field: [X, X+16) lies inside the record
+                r = ld16u((uintptr_t)(p.in + S.src[f][j]) + (uintptr_t)(i64)(P - dj));
             } else {
                 r = u32x4{0, 0, 0, 0};
                 for (int k = j; k < cnt; ++k) {
@@ -256,6 +310,16 @@ __global__ __launch_bounds__(256) void decode_kernel(DecodeParams p) {
     }
 }
 
+template <int NF, int NV>
+static void launch_layout(const DecodeParams& p, dim3 grid, dim3 block, hipStream_t stream) {
+    if (p.variant == 101)
+        hipLaunchKernelGGL((decode_kernel<NF, NV, 1>), grid, block, 0, stream, p);
+    else if (p.variant == 102)
+        hipLaunchKernelGGL((decode_kernel<NF, NV, 2>), grid, block, 0, stream, p);
+    else
+        hipLaunchKernelGGL((decode_kernel<NF, NV, 0>), grid, block, 0, stream, p);
+}
+
 hipError_t launch_decode(const DecodeParams& p, hipStream_t stream) {
     hipError_t e;
     if (p.n == 0) {
@@ -264,15 +328,14 @@ hipError_t launch_decode(const DecodeParams& p, hipStream_t stream) {
         return hipSuccess;
     }
     if ((e = hipMemsetAsync(p.ws, 0, decode_workspace_bytes(p.lay.nvar, p.n), stream)) != hipSuccess) return e;
-    const u64 tiles = (p.n + kWaveRecs - 1) / kWaveRecs;
-    const dim3 grid((unsigned)((tiles + kWaves - 1) / kWaves));
+    const dim3 grid((unsigned)((p.n + kTileRecs - 1) / kTileRecs));  // one look-back tile per workgroup
     const dim3 block(64 * kWaves);
     if (p.lay.nfixed == 0 && p.lay.nvar == 1)
-        hipLaunchKernelGGL((decode_kernel<0, 1>), grid, block, 0, stream, p);
+        launch_layout<0, 1>(p, grid, block, stream);
     else if (p.lay.nfixed == 0 && p.lay.nvar == 2)
-        hipLaunchKernelGGL((decode_kernel<0, 2>), grid, block, 0, stream, p);
+        launch_layout<0, 2>(p, grid, block, stream);
     else if (p.lay.nfixed == 2 && p.lay.nvar == 2)
-        hipLaunchKernelGGL((decode_kernel<2, 2>), grid, block, 0, stream, p);
+        launch_layout<2, 2>(p, grid, block, stream);
     else
         return hipErrorInvalidValue;
     return hipGetLastError();

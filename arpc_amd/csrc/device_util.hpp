@@ -195,6 +195,22 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// 64-lane inclusive scan of a u32 with DPP row shifts and row broadcasts (GFX9 wave64):
+// six VALU ops, no LDS round trips.
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ u32 dpp_add(u32 v) {
+    return v + (u32)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWMASK, 0xf, false);
+}
+__device__ __forceinline__ u32 wave_incl_scan_u32_dpp(u32 v) {
+    v = dpp_add<0x111, 0xf>(v);  // row_shr:1
+    v = dpp_add<0x112, 0xf>(v);  // row_shr:2
+    v = dpp_add<0x114, 0xf>(v);  // row_shr:4
+    v = dpp_add<0x118, 0xf>(v);  // row_shr:8
+    v = dpp_add<0x142, 0xa>(v);  // row_bcast:15 into rows 1, 3
+    v = dpp_add<0x143, 0xc>(v);  // row_bcast:31 into rows 2, 3
+    return v;
+}
+
 // 64-lane inclusive scan of a u32.
 __device__ __forceinline__ u32 wave_incl_scan_u32(u32 v, int lane) {
 #pragma unroll
