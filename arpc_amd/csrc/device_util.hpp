@@ -211,6 +211,29 @@ __device__ __forceinline__ u32 wave_incl_scan_u32_dpp(u32 v) {
     return v;
 }
 
+// 64-lane inclusive max-scan of a u32 (same DPP pattern; shifted-in lanes read 0).
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ u32 dpp_max(u32 v) {
+    return max(v, (u32)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWMASK, 0xf, false));
+}
+__device__ __forceinline__ u32 wave_incl_max_u32_dpp(u32 v) {
+    v = dpp_max<0x111, 0xf>(v);
+    v = dpp_max<0x112, 0xf>(v);
+    v = dpp_max<0x114, 0xf>(v);
+    v = dpp_max<0x118, 0xf>(v);
+    v = dpp_max<0x142, 0xa>(v);
+    v = dpp_max<0x143, 0xc>(v);
+    return v;
+}
+
+// 64-lane inclusive scan of values < 2^32 with a 64-bit result: two 32-bit DPP scans over a
+// 25/7-bit split (64 * 2^25 fits in 32 bits), no shuffles, no branches.
+__device__ __forceinline__ u64 wave_incl_scan_u32w_dpp(u32 v) {
+    const u32 lo = wave_incl_scan_u32_dpp(v & 0x1FFFFFFu);
+    const u32 hi = wave_incl_scan_u32_dpp(v >> 25);
+    return ((u64)hi << 25) + lo;
+}
+
 // 64-lane inclusive scan of a u32.
 __device__ __forceinline__ u32 wave_incl_scan_u32(u32 v, int lane) {
 #pragma unroll

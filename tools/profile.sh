@@ -8,12 +8,13 @@
 set -u
 OUT=${OUT:-gpurun_out/prof}
 ARGS=${BENCH_ARGS:---steps 10 --warmup 2 --cpu-seconds 0 --host-steps 0}
+PROG=${PROG:-bench.py}   # e.g. PROG=tools/kbench.py BENCH_ARGS="--enc 0 --dec 0,102 --rounds 3"
 REPO=$(pwd)
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 run() {  # name, rocprof args...
   local name=$1; shift
-  (cd /tmp && timeout -k 10 300 rocprofv3 "$@" --output-format csv -d "$REPO/$OUT/$name" -o run -- python3 "$REPO/bench.py" $ARGS) \
+  (cd /tmp && timeout -k 10 300 rocprofv3 "$@" --output-format csv -d "$REPO/$OUT/$name" -o run -- python3 "$REPO/$PROG" $ARGS) \
      > "$OUT/$name.log" 2>&1
   local rc=$?
   echo "$name rc=$rc"
