@@ -21,8 +21,11 @@ using symhip::Layout;
 
 struct sym_ctx {
     int device = 0;
-    void* ws = nullptr;  // decode look-back workspace
+    void* ws = nullptr;  // three-kernel decode workspace
     size_t ws_bytes = 0;
+    void* flags = nullptr;  // single-pass decode look-back words (epoch-tagged)
+    size_t flag_bytes = 0;
+    unsigned epoch = 0;     // tag of the last decode call's look-back words
     unsigned* err = nullptr;  // device error word (kErr* bits)
     // host entry points: device staging pool and a private stream
     void* pool = nullptr;
@@ -83,6 +86,33 @@ int ensure_ws(sym_ctx* ctx, int nvar, uint64_t n) {
     return SYM_OK;
 }
 
+// Look-back words for n records; zeroed when allocated, so every word starts with epoch 0,
+// which no call uses.
+int ensure_flags(sym_ctx* ctx, uint64_t n) {
+    const size_t need = symhip::decode_fused_flag_bytes(symhip::kMaxVar, n);
+    if (need <= ctx->flag_bytes) return SYM_OK;
+    if (ctx->flags) (void)hipFree(ctx->flags);
+    ctx->flags = nullptr;
+    ctx->flag_bytes = 0;
+    hipError_t e = hipMalloc(&ctx->flags, need);
+    if (e != hipSuccess) return fail(SYM_ERR_NOMEM, "decode look-back words of %zu bytes: %s", need, hipGetErrorString(e));
+    if ((e = hipMemset(ctx->flags, 0, need)) != hipSuccess) return hip_fail(e, "zeroing look-back words");
+    ctx->flag_bytes = need;
+    ctx->epoch = 0;
+    return SYM_OK;
+}
+
+// The next call's epoch; on wrap-around every word is zeroed again (stream-ordered) first.
+int next_epoch(sym_ctx* ctx, hipStream_t stream, unsigned* epoch) {
+    if (++ctx->epoch >= symhip::kEpochLimit) {
+        hipError_t e = hipMemsetAsync(ctx->flags, 0, ctx->flag_bytes, stream);
+        if (e != hipSuccess) return hip_fail(e, "zeroing look-back words");
+        ctx->epoch = 1;
+    }
+    *epoch = ctx->epoch;
+    return SYM_OK;
+}
+
 int ensure_pool(sym_ctx* ctx, size_t need) {
     if (need <= ctx->pool_bytes) return SYM_OK;
     if (ctx->pool) (void)hipFree(ctx->pool);
@@ -135,6 +165,7 @@ int sym_ctx_destroy(sym_ctx* ctx) {
     DeviceGuard g(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->ws) (void)hipFree(ctx->ws);
+    if (ctx->flags) (void)hipFree(ctx->flags);
     if (ctx->err) (void)hipFree(ctx->err);
     if (ctx->pool) (void)hipFree(ctx->pool);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -145,7 +176,8 @@ int sym_ctx_destroy(sym_ctx* ctx) {
 int sym_ctx_reserve(sym_ctx* ctx, uint64_t max_records) {
     if (!ctx) return fail(SYM_ERR_INVALID, "sym_ctx_reserve: ctx is NULL");
     DeviceGuard g(ctx->device);
-    return ensure_ws(ctx, symhip::kMaxVar, max_records);
+    const int rc = ensure_ws(ctx, symhip::kMaxVar, max_records);
+    return rc != SYM_OK ? rc : ensure_flags(ctx, max_records);
 }
 
 int sym_ctx_check(sym_ctx* ctx, void* stream) {
@@ -238,6 +270,9 @@ int sym_decode(sym_ctx* ctx, int schema, uint64_t n, const uint8_t* d_in, const 
     DeviceGuard g(ctx->device);
     if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
     int rc = ensure_ws(ctx, lay.nvar, n);
+    if (rc == SYM_OK) rc = ensure_flags(ctx, n);
+    unsigned epoch = 0;
+    if (rc == SYM_OK) rc = next_epoch(ctx, (hipStream_t)stream, &epoch);
     if (rc != SYM_OK) return rc;
     DecodeParams p{};
     p.lay = lay;
@@ -252,8 +287,11 @@ int sym_decode(sym_ctx* ctx, int schema, uint64_t n, const uint8_t* d_in, const 
     }
     p.status = d_status;
     p.ws = ctx->ws;
+    p.flags = ctx->flags;
+    p.epoch = epoch;
     p.err = ctx->err;
     p.variant = symhip::tuning_variant("SYMHIP_DECODE_VARIANT");
+    if (const char* d = getenv("SYMHIP_DEBUG_PTR")) p.dbg = (uint64_t*)(uintptr_t)strtoull(d, nullptr, 16);
     hipError_t e = symhip::launch_decode(p, (hipStream_t)stream);
     return e == hipSuccess ? SYM_OK : hip_fail(e, "decode launch");
 }

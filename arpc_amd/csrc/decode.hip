@@ -68,10 +68,10 @@ constexpr int kParseRecs = 2;
 template <int NF>
 constexpr int parse_win() { return NF > 0 ? 48 : 32; }  // table + first length prefix fit
 
-template <int NF, int NV>
+template <int NF, int NV, int kWin = 0, int kR = kParseRecs>
 __global__ __launch_bounds__(kThreads) void decode_parse_kernel(DecodeParams p, DecodeWs w) {
-    constexpr int kW = parse_win<NF>();
-    constexpr int R = kParseRecs;
+    constexpr int kW = kWin ? kWin : parse_win<NF>();
+    constexpr int R = kR;
     __shared__ uint8_t win_all[kWaves][R][kWaveRecs * kW];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const u64 ntiles = num_tiles(p.n);
@@ -412,16 +412,38 @@ __global__ __launch_bounds__(kThreads) void decode_copy_kernel(DecodeParams p, D
 
 // ------------------------------------------------------------------ launch
 template <int NF, int NV>
+static hipError_t launch_prefix_layout(const DecodeParams& p, const DecodeWs& w, hipStream_t stream) {
+    const u64 ntiles = num_tiles(p.n);
+    const dim3 pgrid((unsigned)((ntiles + kWaves * kParseRecs - 1) / (kWaves * kParseRecs)));
+    hipLaunchKernelGGL((decode_parse_kernel<NF, NV>), pgrid, dim3(kThreads), 0, stream, p, w);
+    hipLaunchKernelGGL(decode_scan_kernel, dim3(NV), dim3(kScanThreads), 0, stream, p, w);
+    return hipGetLastError();
+}
+static hipError_t launch_prefix(const DecodeParams& p, const DecodeWs& w, hipStream_t stream) {
+    if (p.lay.nfixed == 0 && p.lay.nvar == 1) return launch_prefix_layout<0, 1>(p, w, stream);
+    if (p.lay.nfixed == 0 && p.lay.nvar == 2) return launch_prefix_layout<0, 2>(p, w, stream);
+    if (p.lay.nfixed == 2 && p.lay.nvar == 2) return launch_prefix_layout<2, 2>(p, w, stream);
+    return hipErrorInvalidValue;
+}
+
+template <int NF, int NV>
 static hipError_t launch_layout(const DecodeParams& p, const DecodeWs& w, hipStream_t stream) {
     const u64 ntiles = num_tiles(p.n);
     const dim3 grid((unsigned)((ntiles + kWaves - 1) / kWaves));
     const dim3 pgrid((unsigned)((ntiles + kWaves * kParseRecs - 1) / (kWaves * kParseRecs)));
-    hipLaunchKernelGGL((decode_parse_kernel<NF, NV>), pgrid, dim3(kThreads), 0, stream, p, w);
+    const int pv = p.variant % 100 >= 20 && p.variant % 100 < 30 ? p.variant % 100 : 0;
+    auto pg = [&](int r) { return dim3((unsigned)((ntiles + kWaves * r - 1) / (kWaves * r))); };
+    if (pv == 20) hipLaunchKernelGGL((decode_parse_kernel<NF, NV, 96, 1>), pg(1), dim3(kThreads), 0, stream, p, w);
+    else if (pv == 21) hipLaunchKernelGGL((decode_parse_kernel<NF, NV, 64, 2>), pg(2), dim3(kThreads), 0, stream, p, w);
+    else if (pv == 22) hipLaunchKernelGGL((decode_parse_kernel<NF, NV, 0, 4>), pg(4), dim3(kThreads), 0, stream, p, w);
+    else if (pv == 23) hipLaunchKernelGGL((decode_parse_kernel<NF, NV, 0, 1>), pg(1), dim3(kThreads), 0, stream, p, w);
+    else if (pv == 24) hipLaunchKernelGGL((decode_parse_kernel<NF, NV, 96, 2>), pg(2), dim3(kThreads), 0, stream, p, w);
+    else hipLaunchKernelGGL((decode_parse_kernel<NF, NV>), pgrid, dim3(kThreads), 0, stream, p, w);
     hipLaunchKernelGGL(decode_scan_kernel, dim3(NV), dim3(kScanThreads), 0, stream, p, w);
-    if (p.variant == 201) return hipGetLastError();  // timing only: parse + scan
-    if (p.variant == 206)
+    if (p.variant == 301) return hipGetLastError();  // timing only: parse + scan
+    if (p.variant == 306)
         hipLaunchKernelGGL((decode_copy_kernel<NV, 6>), grid, dim3(kThreads), 0, stream, p, w);
-    else if (p.variant == 208)
+    else if (p.variant == 308)
         hipLaunchKernelGGL((decode_copy_kernel<NV, 8>), grid, dim3(kThreads), 0, stream, p, w);
     else
         hipLaunchKernelGGL((decode_copy_kernel<NV>), grid, dim3(kThreads), 0, stream, p, w);
@@ -437,6 +459,15 @@ hipError_t launch_decode(const DecodeParams& p, hipStream_t stream) {
         return hipSuccess;
     }
     const DecodeWs w = ws_layout(p.ws, p.lay.nvar, p.n);
+    if (p.variant == 700 || p.variant == 710 || p.variant == 800 || p.variant == 810) {
+        // parse + scan kernels for the tile prefixes, then the LDS-staged stage/parse/copy kernel
+        DecodeParams q = p;
+        q.tile_pre = w.pre;
+        q.variant = (p.variant % 100 == 10 ? 417 : 407) + (p.variant >= 800 ? 100 : 0);
+        hipError_t e = launch_prefix(p, w, stream);
+        return e != hipSuccess ? e : launch_decode_fused(q, p.flags, p.epoch, stream);
+    }
+    if (p.variant >= 400) return launch_decode_fused(p, p.flags, p.epoch, stream);  // experimental single-pass
     if (p.lay.nfixed == 0 && p.lay.nvar == 1) return launch_layout<0, 1>(p, w, stream);
     if (p.lay.nfixed == 0 && p.lay.nvar == 2) return launch_layout<0, 2>(p, w, stream);
     if (p.lay.nfixed == 2 && p.lay.nvar == 2) return launch_layout<2, 2>(p, w, stream);

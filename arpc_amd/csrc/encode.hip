@@ -210,17 +210,83 @@ __global__ __launch_bounds__(256) void encode_kernel(EncodeParams p) {
         store_chunk(out_t, P, 0, span, rr);
     };
 
-    for (int B = first; B < span; B += 16 * 64) {  // wave-uniform loop
-        const int j = locate(B);
-        const int P = B + 16 * lane;
-        if (P < span) chunk(P, j, !tile_safe);
+    if constexpr (kVariant == 0) {
+        for (int B = first; B < span; B += 16 * 64) {  // wave-uniform loop
+            const int j = locate(B);
+            const int P = B + 16 * lane;
+            if (P < span) chunk(P, j, !tile_safe);
+        }
+        return;
+    }
+    if (!tile_safe) {  // batch-edge tiles (two per batch): the careful one-step path
+        for (int B = first; B < span; B += 16 * 64) {
+            const int j = locate(B);
+            const int P = B + 16 * lane;
+            if (P < span) chunk(P, j, true);
+        }
+        return;
+    }
+    // Interior tiles: kU steps per round.  Every payload load of the round is issued before the
+    // first store (unconditional loads, so the compiler waits only once), keeping kU KiB of
+    // loads in flight per wave instead of one.
+    constexpr int kU = kVariant > 0 ? kVariant : 1;
+    for (int B0 = first; B0 < span; B0 += 16 * 64 * kU) {  // wave-uniform loop
+        int jj[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) jj[u] = locate(B0 + 16 * 64 * u);
+        u32x4 w[kU][NV];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int P = B0 + 16 * 64 * u + 16 * lane;
+            const int j = jj[u];
+            int t = H0 - (P - S.o[j]);
+#pragma unroll
+            for (int f = 0; f < NV; ++f) {
+                const int Lf = (int)S.len[f][j];
+                const bool need = P < span && t < 16 && t + Lf > 0;
+                w[u][f] = ld16u(need ? (uintptr_t)(S.delta[f][j] + (u64)(i64)P) : dummy);
+                t += Lf + 4;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int P = B0 + 16 * 64 * u + 16 * lane;
+            if (P >= span) continue;
+            const int j = jj[u];
+            const int b = P - S.o[j];
+            u32x4 r = {0, 0, 0, 0};
+            if (b < H0) r = lds16u(S.hdr, (j + 1) * SLOT + b);
+            int t = H0 - b;
+#pragma unroll
+            for (int f = 0; f < NV; ++f) {
+                const int Lf = (int)S.len[f][j];
+                if (f > 0 && t > 0 && t < 20) {  // inner length prefix of field f at [t-4, t)
+                    u32 tmp[4] = {r.x, r.y, r.z, r.w};
+                    or_u32_at((u32)Lf, t - 4, tmp);
+                    r = u32x4{tmp[0], tmp[1], tmp[2], tmp[3]};
+                }
+                if (t < 16 && t + Lf > 0) r |= w[u][f] & range_mask(masks, t, t + Lf);
+                t += Lf + 4;
+            }
+            if (j + 1 < cnt) {
+                const int nb = P - S.o[j + 1];
+                if (nb > -16) r |= lds16u(S.hdr, (j + 2) * SLOT + nb);
+            }
+            const u32 rr[4] = {r.x, r.y, r.z, r.w};
+            store_chunk(out_t, P, 0, span, rr);
+        }
     }
 }
 
 template <int NF, int NV>
 static void launch_layout(const EncodeParams& p, dim3 grid, dim3 block, hipStream_t stream) {
-    (void)p.variant;  // one variant at present
-    hipLaunchKernelGGL((encode_kernel<NF, NV, 0>), grid, block, 0, stream, p);
+    // variants 2/4: that many steps' loads in flight per wave (measured no faster on MI355X: the
+    // one-step loop already runs at ~92 % of a plain 350 MB copy, tools/ubench_copy.hip)
+    switch (p.variant) {
+        case 2: hipLaunchKernelGGL((encode_kernel<NF, NV, 2>), grid, block, 0, stream, p); break;
+        case 4: hipLaunchKernelGGL((encode_kernel<NF, NV, 4>), grid, block, 0, stream, p); break;
+        default: hipLaunchKernelGGL((encode_kernel<NF, NV, 0>), grid, block, 0, stream, p); break;
+    }
 }
 
 hipError_t launch_encode(const EncodeParams& p, hipStream_t stream) {

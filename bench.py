@@ -251,10 +251,10 @@ def main():
     dec_ms = float(np.mean([a.elapsed_time(b_) for a, b_ in ev["dec"]]))
     enc_b, dec_b = alg_bytes(n, s.nvar, var_total, total)
     value = world * (enc_b + dec_b) * args.steps / elapsed / 1e9
-    # decode = parse + scan + copy kernels; time parse + scan alone (decode variant 201, outside
+    # decode = parse + scan + copy kernels; time parse + scan alone (decode variant 301, outside
     # the timed region, same buffers and stream) so the copy kernel's share is a live number too
     ps_ev = []
-    os.environ["SYMHIP_DECODE_VARIANT"] = "201"
+    os.environ["SYMHIP_DECODE_VARIANT"] = "301"
     for i in range(max(5, args.steps // 2)):
         d = (i + 2) % NSETS
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
