@@ -23,7 +23,7 @@ struct sym_ctx {
     int device = 0;
     void* ws = nullptr;  // three-kernel decode workspace
     size_t ws_bytes = 0;
-    void* flags = nullptr;  // single-pass decode look-back words (epoch-tagged)
+    void* flags = nullptr;  // default decode's aggregate / prefix words (epoch-tagged)
     size_t flag_bytes = 0;
     unsigned epoch = 0;     // tag of the last decode call's look-back words
     unsigned* err = nullptr;  // device error word (kErr* bits)
@@ -89,7 +89,7 @@ int ensure_ws(sym_ctx* ctx, int nvar, uint64_t n) {
 // Look-back words for n records; zeroed when allocated, so every word starts with epoch 0,
 // which no call uses.
 int ensure_flags(sym_ctx* ctx, uint64_t n) {
-    const size_t need = symhip::decode_fused_flag_bytes(symhip::kMaxVar, n);
+    const size_t need = symhip::decode_pipe_flag_bytes(symhip::kMaxVar, n);
     if (need <= ctx->flag_bytes) return SYM_OK;
     if (ctx->flags) (void)hipFree(ctx->flags);
     ctx->flags = nullptr;

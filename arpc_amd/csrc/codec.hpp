@@ -43,11 +43,11 @@ struct DecodeParams {
     uint64_t cap[kMaxVar];
     uint64_t* offs[kMaxVar];
     uint8_t* status;
-    void* ws;       // decode_workspace_bytes() bytes (three-kernel decode)
-    void* flags;    // decode_fused_flag_bytes() bytes of look-back words (single-pass decode)
-    unsigned epoch; // look-back word tag of this call, in [1, kEpochLimit)
-    u64_t* dbg;     // diagnostics only (tools/decode_timeline.py): per-tile timestamps, else null
-    const u64_t* tile_pre;  // per-column exclusive prefix of every 64-record tile (from the scan kernel)
+    void* ws;       // decode_workspace_bytes() bytes (three-kernel decode, variant 300)
+    void* flags;    // decode_pipe_flag_bytes() bytes of aggregate / prefix words (default decode)
+    unsigned epoch; // word tag of this call, in [1, kEpochLimit)
+    u64_t* dbg;     // diagnostics only (tools/fused_timeline.py): per-tile timestamps, else null
+    unsigned pipe_parsers;  // set by launch_decode_pipe: parser workgroups of the launch
     unsigned* err;  // persistent device error word (kErr* bits), cleared by the host
     int variant;    // kernel tuning variant (tuning_variant("SYMHIP_DECODE_VARIANT"))
 };
@@ -63,11 +63,11 @@ constexpr unsigned kErrTimeout = 2u;
 constexpr unsigned kErrTooLarge = 4u;  // 64 consecutive records spanning >= 2 GiB
 
 size_t decode_workspace_bytes(int nvar, uint64_t n);
-// Look-back words of the single-pass decode: tagged with the call's epoch, so they need zeroing
-// only when allocated and when the epoch wraps.
-size_t decode_fused_flag_bytes(int nvar, uint64_t n);
+// Aggregate / prefix words of the default decode (decode_pipe.hip): tagged with the call's epoch, so
+// they need zeroing only when allocated and when the epoch wraps.
+size_t decode_pipe_flag_bytes(int nvar, uint64_t n);
 constexpr unsigned kEpochLimit = 1u << 20;
-hipError_t launch_decode_fused(const DecodeParams& p, void* flags, unsigned epoch, hipStream_t stream);
+hipError_t launch_decode_pipe(const DecodeParams& p, void* flags, unsigned epoch, hipStream_t stream);
 
 // Kernel variant selected by an environment variable (0 = default); lets tools/kbench.py
 // compare variants inside one process.

@@ -1,4 +1,6 @@
-// decode.hip -- batched Symphony UnmarshalSymphony for flat schemas on gfx950.
+// decode.hip -- batched Symphony UnmarshalSymphony for flat schemas on gfx950: the three-kernel
+// path (decode variant 300).  The default decode is decode_pipe.hip; this file also holds the
+// decode dispatch (launch_decode).
 //
 // Restates, for n records at once, the generated per-record unmarshaller into a fresh
 // struct: benchmark/kv-store-symphony/symphony/kv.syn.go:680-745 (SetRequest; Get/Resp
@@ -21,9 +23,8 @@
 //     Chunks are enumerated record-major (a record's key chunks, then its value chunks), so
 //     the lines a record spans are fetched together; each wave keeps kRB steps (64 chunks
 //     each) of loads in flight in a rolling register pipeline.
-// Measured on MI355X (profiles/): a single-pass decoupled look-back kept the same traffic --
-// the parse's header lines are evicted from L2 before the copy reaches them either way -- but
-// stalled every tile on the look-back round trips; here no wave ever waits on another.
+// No wave ever waits on another; the price is a second read of every record's header sectors
+// (the parse pass) before any byte moves, which the pipelined default overlaps with the copy.
 #include "codec.hpp"
 #include "device_util.hpp"
 
@@ -68,15 +69,15 @@ constexpr int kParseRecs = 2;
 template <int NF>
 constexpr int parse_win() { return NF > 0 ? 48 : 32; }  // table + first length prefix fit
 
-template <int NF, int NV, int kWin = 0, int kR = kParseRecs>
-__global__ __launch_bounds__(kThreads) void decode_parse_kernel(DecodeParams p, DecodeWs w) {
-    constexpr int kW = kWin ? kWin : parse_win<NF>();
-    constexpr int R = kR;
+template <int NF, int NV>
+__global__ __launch_bounds__(kThreads) void decode_parse_kernel(DecodeParams p, DecodeWs w, u64 tb, u64 te) {
+    constexpr int kW = parse_win<NF>();
+    constexpr int R = kParseRecs;
     __shared__ uint8_t win_all[kWaves][R][kWaveRecs * kW];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const u64 ntiles = num_tiles(p.n);
-    const u64 tile0 = ((u64)blockIdx.x * kWaves + wave) * R;
-    if (tile0 >= ntiles) return;
+    const u64 tile0 = tb + ((u64)blockIdx.x * kWaves + wave) * R;
+    if (tile0 >= te) return;
 
     // Loads are unconditional (exec-masked loads would make the compiler drain every load before
     // the next dependent use); lanes with nothing to read use `safe`, the workspace's first
@@ -88,7 +89,7 @@ __global__ __launch_bounds__(kThreads) void decode_parse_kernel(DecodeParams p, 
 #pragma unroll
     for (int h = 0; h < R; ++h) {
         const u64 r = (tile0 + h) * kWaveRecs + lane;
-        live[h] = r < p.n;
+        live[h] = r < p.n && tile0 + h < te;
         const u64 rc = live[h] ? r : p.n;  // branch-free loads: rec_off has n+1 entries
         start[h] = p.rec_off[rc];
         endv[h] = p.rec_off[live[h] ? rc + 1 : rc];
@@ -200,7 +201,7 @@ __global__ __launch_bounds__(kThreads) void decode_parse_kernel(DecodeParams p, 
             }
         }
         // tile aggregates (field lengths are < 2^32: split 32-bit DPP scans)
-        if (tile0 + h < ntiles) {
+        if (tile0 + h < te) {
 #pragma unroll
             for (int f = 0; f < NV; ++f) {
                 const u64 inc = wave_incl_scan_u32w_dpp((u32)flen[f]);
@@ -219,7 +220,7 @@ __global__ __launch_bounds__(kThreads) void decode_parse_kernel(DecodeParams p, 
 // parse kernel).  Wave w owns 1024 consecutive tiles of a block, lane-interleaved (element
 // k*64 + lane), so every load and store instruction is one coalesced 512-byte access; rows are
 // scanned with DPP and carried across k, waves combine through LDS.
-__global__ __launch_bounds__(kScanThreads) void decode_scan_kernel(DecodeParams p, DecodeWs w) {
+__global__ __launch_bounds__(kScanThreads) void decode_scan_kernel(DecodeParams p, DecodeWs w, u64 tb, u64 te) {
     constexpr int kRows = 16;
     constexpr int kWavesScan = kScanThreads / 64;
     constexpr u64 kBlock = (u64)kScanThreads * kRows;
@@ -230,16 +231,16 @@ __global__ __launch_bounds__(kScanThreads) void decode_scan_kernel(DecodeParams 
     const u64* agg = w.agg + (size_t)f * ntiles;
     u64* pre = w.pre + (size_t)f * ntiles;
     u64 carry = 0;  // total of all earlier blocks (uniform)
-    for (u64 base = 0; base < ntiles; base += kBlock) {
+    for (u64 base = tb; base < te; base += kBlock) {
         const u64 e0 = base + (u64)wave * (64 * kRows) + lane;
         u32 v[kRows];
 #pragma unroll
         for (int k = 0; k < kRows; ++k)  // unconditional (clamped) loads: all rows in flight at once
-            v[k] = (u32)agg[min(e0 + 64 * k, ntiles - 1)];
+            v[k] = (u32)agg[min(e0 + 64 * k, te - 1)];
         u64 run = 0, ex[kRows];
 #pragma unroll
         for (int k = 0; k < kRows; ++k) {
-            if (e0 + 64 * k >= ntiles) v[k] = 0;
+            if (e0 + 64 * k >= te) v[k] = 0;
             const u64 inc = wave_incl_scan_u32w_dpp(v[k]);
             ex[k] = run + inc - v[k];
             run += (u64)__builtin_amdgcn_readlane((u32)inc, 63) | ((u64)__builtin_amdgcn_readlane((u32)(inc >> 32), 63) << 32);
@@ -255,11 +256,11 @@ __global__ __launch_bounds__(kScanThreads) void decode_scan_kernel(DecodeParams 
         }
 #pragma unroll
         for (int k = 0; k < kRows; ++k)
-            if (e0 + 64 * k < ntiles) pre[e0 + 64 * k] = wpre + ex[k];
+            if (e0 + 64 * k < te) pre[e0 + 64 * k] = wpre + ex[k];
         carry += tot;
         __syncthreads();  // s_wsum is rewritten by the next block
     }
-    if (threadIdx.x == 0) p.offs[f][p.n] = carry;
+    if (threadIdx.x == 0 && te == ntiles) p.offs[f][p.n] = carry;
 }
 
 // ------------------------------------------------------------------ 3. copy
@@ -279,13 +280,13 @@ __device__ __forceinline__ T pick(const T (&a)[NV], bool second) {
 }
 
 template <int NV, int KRB = kRB>
-__global__ __launch_bounds__(kThreads) void decode_copy_kernel(DecodeParams p, DecodeWs w) {
+__global__ __launch_bounds__(kThreads) void decode_copy_kernel(DecodeParams p, DecodeWs w, u64 tb, u64 te) {
     static_assert(NV == 1 || NV == 2, "decode handles one or two string columns");
     __shared__ CopyWaveLds<NV> lds_all[kWaves];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const u64 tile = (u64)blockIdx.x * kWaves + wave;
+    const u64 tile = tb + (u64)blockIdx.x * kWaves + wave;
     const u64 ntiles = num_tiles(p.n);
-    if (tile >= ntiles) return;
+    if (tile >= te) return;
     CopyWaveLds<NV>& S = lds_all[wave];
     const u64 r0 = tile * kWaveRecs;
     const int cnt = (int)min((u64)kWaveRecs, p.n - r0);
@@ -412,44 +413,21 @@ __global__ __launch_bounds__(kThreads) void decode_copy_kernel(DecodeParams p, D
 
 // ------------------------------------------------------------------ launch
 template <int NF, int NV>
-static hipError_t launch_prefix_layout(const DecodeParams& p, const DecodeWs& w, hipStream_t stream) {
-    const u64 ntiles = num_tiles(p.n);
-    const dim3 pgrid((unsigned)((ntiles + kWaves * kParseRecs - 1) / (kWaves * kParseRecs)));
-    hipLaunchKernelGGL((decode_parse_kernel<NF, NV>), pgrid, dim3(kThreads), 0, stream, p, w);
-    hipLaunchKernelGGL(decode_scan_kernel, dim3(NV), dim3(kScanThreads), 0, stream, p, w);
-    return hipGetLastError();
-}
-static hipError_t launch_prefix(const DecodeParams& p, const DecodeWs& w, hipStream_t stream) {
-    if (p.lay.nfixed == 0 && p.lay.nvar == 1) return launch_prefix_layout<0, 1>(p, w, stream);
-    if (p.lay.nfixed == 0 && p.lay.nvar == 2) return launch_prefix_layout<0, 2>(p, w, stream);
-    if (p.lay.nfixed == 2 && p.lay.nvar == 2) return launch_prefix_layout<2, 2>(p, w, stream);
-    return hipErrorInvalidValue;
-}
-
-template <int NF, int NV>
 static hipError_t launch_layout(const DecodeParams& p, const DecodeWs& w, hipStream_t stream) {
     const u64 ntiles = num_tiles(p.n);
-    const dim3 grid((unsigned)((ntiles + kWaves - 1) / kWaves));
-    const dim3 pgrid((unsigned)((ntiles + kWaves * kParseRecs - 1) / (kWaves * kParseRecs)));
-    const int pv = p.variant % 100 >= 20 && p.variant % 100 < 30 ? p.variant % 100 : 0;
-    auto pg = [&](int r) { return dim3((unsigned)((ntiles + kWaves * r - 1) / (kWaves * r))); };
-    if (pv == 20) hipLaunchKernelGGL((decode_parse_kernel<NF, NV, 96, 1>), pg(1), dim3(kThreads), 0, stream, p, w);
-    else if (pv == 21) hipLaunchKernelGGL((decode_parse_kernel<NF, NV, 64, 2>), pg(2), dim3(kThreads), 0, stream, p, w);
-    else if (pv == 22) hipLaunchKernelGGL((decode_parse_kernel<NF, NV, 0, 4>), pg(4), dim3(kThreads), 0, stream, p, w);
-    else if (pv == 23) hipLaunchKernelGGL((decode_parse_kernel<NF, NV, 0, 1>), pg(1), dim3(kThreads), 0, stream, p, w);
-    else if (pv == 24) hipLaunchKernelGGL((decode_parse_kernel<NF, NV, 96, 2>), pg(2), dim3(kThreads), 0, stream, p, w);
-    else hipLaunchKernelGGL((decode_parse_kernel<NF, NV>), pgrid, dim3(kThreads), 0, stream, p, w);
-    hipLaunchKernelGGL(decode_scan_kernel, dim3(NV), dim3(kScanThreads), 0, stream, p, w);
-    if (p.variant == 301) return hipGetLastError();  // timing only: parse + scan
-    if (p.variant == 306)
-        hipLaunchKernelGGL((decode_copy_kernel<NV, 6>), grid, dim3(kThreads), 0, stream, p, w);
-    else if (p.variant == 308)
-        hipLaunchKernelGGL((decode_copy_kernel<NV, 8>), grid, dim3(kThreads), 0, stream, p, w);
-    else
-        hipLaunchKernelGGL((decode_copy_kernel<NV>), grid, dim3(kThreads), 0, stream, p, w);
+    constexpr u64 kGroup = kWaves * kParseRecs;  // tiles per parse workgroup
+    const unsigned pg = (unsigned)((ntiles + kGroup - 1) / kGroup);
+    const unsigned cg = (unsigned)((ntiles + kWaves - 1) / kWaves);
+    hipLaunchKernelGGL((decode_parse_kernel<NF, NV>), dim3(pg), dim3(kThreads), 0, stream, p, w, (u64)0, ntiles);
+    hipLaunchKernelGGL(decode_scan_kernel, dim3(NV), dim3(kScanThreads), 0, stream, p, w, (u64)0, ntiles);
+    if (p.variant != 301)  // 301: timing of parse + scan alone
+        hipLaunchKernelGGL((decode_copy_kernel<NV>), dim3(cg), dim3(kThreads), 0, stream, p, w, (u64)0, ntiles);
     return hipGetLastError();
 }
 
+// Decode dispatch: the single-launch pipeline (decode_pipe.hip) by default; variants 300/301 run
+// the three-kernel path above (parse -> scan -> copy), kept as a second, independently tested
+// implementation of the same contract.
 hipError_t launch_decode(const DecodeParams& p, hipStream_t stream) {
     if (p.n == 0) {
         for (int f = 0; f < p.lay.nvar; ++f) {
@@ -458,16 +436,8 @@ hipError_t launch_decode(const DecodeParams& p, hipStream_t stream) {
         }
         return hipSuccess;
     }
+    if (p.variant != 300 && p.variant != 301) return launch_decode_pipe(p, p.flags, p.epoch, stream);
     const DecodeWs w = ws_layout(p.ws, p.lay.nvar, p.n);
-    if (p.variant == 700 || p.variant == 710 || p.variant == 800 || p.variant == 810) {
-        // parse + scan kernels for the tile prefixes, then the LDS-staged stage/parse/copy kernel
-        DecodeParams q = p;
-        q.tile_pre = w.pre;
-        q.variant = (p.variant % 100 == 10 ? 417 : 407) + (p.variant >= 800 ? 100 : 0);
-        hipError_t e = launch_prefix(p, w, stream);
-        return e != hipSuccess ? e : launch_decode_fused(q, p.flags, p.epoch, stream);
-    }
-    if (p.variant >= 400) return launch_decode_fused(p, p.flags, p.epoch, stream);  // experimental single-pass
     if (p.lay.nfixed == 0 && p.lay.nvar == 1) return launch_layout<0, 1>(p, w, stream);
     if (p.lay.nfixed == 0 && p.lay.nvar == 2) return launch_layout<0, 2>(p, w, stream);
     if (p.lay.nfixed == 2 && p.lay.nvar == 2) return launch_layout<2, 2>(p, w, stream);

@@ -1,0 +1,565 @@
+// decode_pipe.hip -- batched Symphony UnmarshalSymphony on gfx950: the default decode.
+//
+// Restates, for n records at once, the generated per-record unmarshaller into a fresh struct:
+// benchmark/kv-store-symphony/symphony/kv.syn.go:680-745 (SetRequest; Get/Resp analogous),
+// examples/echo_symphony/symphony/echo.syn.go:186-263 (int32 fields), from the generator's rules
+// cmd/symphony-gen-arpc/protoc-gen-symphony/main.go:622-694, :734-793.
+//
+// A string field's output position is the sum of all earlier lengths in its column, so decode is a
+// scan.  Here it is ONE launch in which every stream byte is staged through LDS once, with three
+// roles by workgroup index (lowest first, so producers are resident before their consumers):
+//   [0, P)      parsers: a wave reads the headers of 64-record tiles (two 16-byte loads per record
+//               into registers, global loads past that window), runs Go's checks for the field
+//               lengths only, and publishes the tile's per-column aggregate word.  They never wait.
+//   P           scanner: walks the tiles in order, 1024 per step, and publishes every tile's
+//               exclusive prefix word up to the first tile whose aggregate is not yet published.
+//   P + 1 + t   copier of tile t:
+//                 1. stage: the tile's byte span -> LDS with aligned, coalesced 16-byte loads (up to
+//                    kStage bytes; a longer span's tail is read from HBM at copy time);
+//                 2. parse (wave 0, lane = record) from LDS: status byte, int32 fields, per-field
+//                    (position, length), the tile scan (DPP); publishes its own aggregate too;
+//                 3. waits for its prefix word (normally published long before), writes offsets;
+//                 4. copy (all lanes): each field as a run of 16-byte chunks (the last one moved back
+//                    to end at the field end): one byte-unaligned LDS read, one 16-byte store.
+// Prefix words are 8-byte {epoch, status, value} words written and polled with agent-scope relaxed
+// atomics -- the word is its own flag (MI355X_MICROARCH.md visibility, form "R2") -- tagged with the
+// call's epoch so they never need clearing between calls.
+//
+// Why this shape (measured on MI355X): a separate parse pass costs ~65 us of
+// scattered header reads before any byte moves; an in-kernel decoupled look-back between copiers
+// stalls on cross-XCD round trips (~2 us each) once ~1500 tiles are in flight; parsers that run
+// ahead make the chain a single streaming scanner the copiers rarely wait on.
+#include "../../include/symphony_hip.h"
+#include "codec.hpp"
+#include "device_util.hpp"
+
+namespace symhip {
+
+namespace pipe {
+
+constexpr int kRecs = 64;       // records per tile
+constexpr int kThreads = 256;   // 4 waves
+constexpr int kStage = 22528;   // staged bytes per tile: a whole 64-record tile of 350-B records
+constexpr int kStageLoads = (kStage / 16 + kThreads - 1) / kThreads;
+constexpr int kU = 2;           // copy chunks per lane per step
+
+// Word: [63:44] epoch, [43:42] status (1 = aggregate, 2 = exclusive prefix), [41:0] value.
+constexpr int kEpochShift = 44;
+constexpr u64 kStAgg = 1ull << 42;
+constexpr u64 kStPre = 2ull << 42;
+constexpr u64 kValMask = (1ull << 42) - 1;
+constexpr unsigned kSpinLimit = 1u << 21;  // bounded waits: a stuck call reports kErrTimeout and drains
+
+__host__ __device__ inline u64 num_tiles(u64 n) { return (n + kRecs - 1) / kRecs; }
+
+template <int NV>
+struct alignas(16) Lds {
+    uint8_t stage[kStage + 16];
+    u64 src[NV][kRecs];      // field payload position (stream offset)
+    int dst[NV][kRecs + 1];  // field start in the tile's column range; [cnt..] = aggregate
+    int cs[kRecs + 1];       // record's first copy chunk (record-major chunk sequence)
+    int nch0[kRecs];         // chunks of the record's first string field
+    i64 pre[NV];             // tile prefix per column
+    i64 lim[NV];             // bytes of the tile's column range that fit the output capacity
+    int total;               // chunks in the tile (-1: tile skipped, error reported)
+    u64 red[4];              // scanner: per-wave partial sums
+    int first[4];            // scanner: per-wave first unpublished tile
+};
+
+__device__ __forceinline__ bool tagged(u64 w, u32 epoch) { return (u32)(w >> kEpochShift) == epoch; }
+__device__ __forceinline__ u64 make_word(u32 epoch, u64 st, u64 v) {
+    return ((u64)epoch << kEpochShift) | st | (v & kValMask);
+}
+__device__ __forceinline__ void store_word(u64* w, u64 v) {
+    __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ u64 load_word(u64* w) { return __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+// Workgroup barrier that orders LDS only: outstanding global stores keep flying (__syncthreads()
+// would wait for them).  Global loads whose data is used were waited on at their use.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// u32 at byte q (q <= 4*NW-4) of a register window w[0..NW): bit-select the dword pair (a dynamic
+// register index would go to scratch) and align.
+template <int NW>
+__device__ __forceinline__ u32 win_u32(const u32 (&w)[NW], u32 q) {
+    const u32 d = q >> 2;
+    u32 lo = w[0], hi = w[1];
+#pragma unroll
+    for (int k = 1; k < NW; ++k) {
+        lo = d == (u32)k ? w[k] : lo;
+        hi = d == (u32)k ? (k < NW - 1 ? w[k + 1] : 0u) : hi;
+    }
+    return alignbyte(hi, lo, q & 3);
+}
+
+// ---------------------------------------------------------------- parser role
+// Step k covers tiles [k*4PR, (k+1)*4PR): wave (b, w) takes R consecutive tiles, lane = record; every
+// load of the R records a lane handles is issued before any is used.  Field lengths follow the same
+// Go checks as the copier's parse (kv.syn.go:681-745), so both publish identical aggregates.
+template <int NF, int NV, int R = 2, int WB = 32>
+__device__ void parser(const DecodeParams& p, u64* aw, u64 ntiles, u32 epoch, u32 P) {
+    constexpr int NW = WB / 4;  // window dwords
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const u64 n = p.n;
+    const uintptr_t in = (uintptr_t)p.in;
+    for (u64 t0 = ((u64)blockIdx.x * 4 + wave) * R; t0 < ntiles; t0 += (u64)P * 4 * R) {
+        bool live[R], win[R];
+        u64 start[R], L[R];
+        u32 w[R][NW];
+#pragma unroll
+        for (int h = 0; h < R; ++h) {
+            const u64 r = (t0 + h) * kRecs + lane;
+            live[h] = t0 + h < ntiles && r < n;
+            const u64 rc = live[h] ? r : n;
+            start[h] = p.rec_off[rc];
+            L[h] = p.rec_off[live[h] ? rc + 1 : rc] - start[h];
+        }
+#pragma unroll
+        for (int h = 0; h < R; ++h) {
+            win[h] = live[h] && L[h] >= (u64)WB;
+            const uintptr_t wa = win[h] ? in + start[h] : (uintptr_t)aw;  // readable filler (>= 256 B)
+#pragma unroll
+            for (int k = 0; k < WB / 16; ++k) {
+                const u32x4 a = ld16u(wa + 16 * k);
+                w[h][4 * k] = a.x;
+                w[h][4 * k + 1] = a.y;
+                w[h][4 * k + 2] = a.z;
+                w[h][4 * k + 3] = a.w;
+            }
+        }
+#pragma unroll
+        for (int h = 0; h < R; ++h) {
+            const uintptr_t A = in + start[h];
+            const bool wh = win[h];
+            const u64 Lh = L[h];
+            auto rd8 = [&](u64 q) -> u32 {
+                constexpr u64 M = WB - 4;
+                return wh && q < (u64)WB ? (win_u32<NW>(w[h], (u32)min(q, M)) >> (8 * (q > M ? q - M : 0))) & 0xffu
+                                         : ld_u8(A + q);
+            };
+            auto rd32 = [&](u64 q) -> u32 {
+                return wh && q + 4 <= (u64)WB ? win_u32<NW>(w[h], (u32)q) : *(gc_u32*)(A + q);  // unaligned OK
+            };
+            u64 flen[NV];
+#pragma unroll
+            for (int f = 0; f < NV; ++f) flen[f] = 0;
+            if (live[h] && Lh >= 13 && rd8(0) == 0x01) {
+                const u64 off2p = rd32(1);
+                if (off2p < Lh && rd8(off2p) == 0x01) {
+                    const u64 pts = off2p + 1;
+                    const u64 vt = pts + 4 * (u64)NF;  // var table: only if every int32 field fits
+                    if (Lh >= vt) {
+#pragma unroll
+                        for (int f = 0; f < NV; ++f) {
+                            const u64 te = vt + 4 * (u64)f;
+                            if (Lh >= te + 4) {
+                                u64 q = rd32(te);
+                                if (q > 0) q += off2p;
+                                if (q > 0 && Lh >= q + 4) {
+                                    const u64 nb = rd32(q);
+                                    if (Lh >= q + 4 + nb) flen[f] = nb;
+                                }
+                            }
+                        }
+                    }
+                }
+            }
+            if (t0 + h < ntiles) {
+#pragma unroll
+                for (int f = 0; f < NV; ++f) {
+                    const u64 inc = wave_incl_scan_u32w_dpp((u32)flen[f]);
+                    const u64 agg = (u64)__builtin_amdgcn_readlane((u32)inc, 63) |
+                                    ((u64)__builtin_amdgcn_readlane((u32)(inc >> 32), 63) << 32);
+                    if (lane == f) store_word(&aw[(size_t)f * ntiles + t0 + h], make_word(epoch, kStAgg, agg));
+                }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- scanner role
+// Each step loads the aggregate words of the next 1024 tiles, finds the first tile whose word is not
+// yet published (the frontier), and publishes the exclusive prefix of every tile before it.  A
+// tile's prefix so depends only on earlier tiles, whoever published their aggregates.
+template <int NV, typename LdsT>
+__device__ void scanner(u64* aw, u64* pw, u64 ntiles, u32 epoch, unsigned* err, LdsT& S) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr int kPer = 4;  // tiles per thread per step
+    constexpr u64 kStep = (u64)kThreads * kPer;
+    u64 carry[NV];
+#pragma unroll
+    for (int f = 0; f < NV; ++f) carry[f] = 0;
+    unsigned idle = 0;
+    for (u64 base = 0; base < ntiles;) {
+        const u64 t0 = base + (u64)tid * kPer;
+        u64 v[NV][kPer];
+#pragma unroll
+        for (int f = 0; f < NV; ++f)
+#pragma unroll
+            for (int k = 0; k < kPer; ++k)
+                v[f][k] = t0 + k < ntiles ? load_word(&aw[(size_t)f * ntiles + t0 + k]) : make_word(epoch, kStAgg, 0);
+        u32 miss = (u32)kStep;  // this thread's first unpublished tile (relative to base)
+#pragma unroll
+        for (int k = kPer - 1; k >= 0; --k) {
+            bool ok = true;
+#pragma unroll
+            for (int f = 0; f < NV; ++f) ok = ok && tagged(v[f][k], epoch);
+            if (!ok) miss = (u32)(tid * kPer + k);
+        }
+#pragma unroll
+        for (int d = 32; d > 0; d >>= 1) miss = min(miss, (u32)__shfl_xor((int)miss, d, 64));
+        if (lane == 0) S.first[wave] = (int)miss;
+        lds_barrier();
+        u32 m = (u32)min(min(S.first[0], S.first[1]), min(S.first[2], S.first[3]));
+        lds_barrier();  // S.first is rewritten by the next step
+        m = (u32)min((u64)m, ntiles - base);
+        if (m == 0) {  // the frontier has not moved: wait a little (bounded)
+            if (++idle >= kSpinLimit) {
+                if (tid == 0) atomicOr(err, kErrTimeout);
+                return;
+            }
+            __builtin_amdgcn_s_sleep(2);
+            continue;
+        }
+        idle = 0;
+#pragma unroll
+        for (int f = 0; f < NV; ++f) {
+            u64 x[kPer], sum = 0;
+#pragma unroll
+            for (int k = 0; k < kPer; ++k) {
+                x[k] = (u32)(tid * kPer + k) < m ? v[f][k] & kValMask : 0;
+                sum += x[k];
+            }
+            const u64 inc = wave_incl_scan_u64(sum, lane);
+            if (lane == 63) S.red[wave] = inc;
+            lds_barrier();
+            u64 wpre = 0, tot = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const u64 t = S.red[q];
+                if (q < wave) wpre += t;
+                tot += t;
+            }
+            lds_barrier();  // S.red is rewritten for the next column / step
+            u64 run = carry[f] + wpre + inc - sum;
+#pragma unroll
+            for (int k = 0; k < kPer; ++k) {
+                if ((u32)(tid * kPer + k) < m) store_word(&pw[(size_t)f * ntiles + t0 + k], make_word(epoch, kStPre, run));
+                run += x[k];
+            }
+            carry[f] += tot;
+        }
+        base += m;
+    }
+}
+
+// ---------------------------------------------------------------- the kernel
+// MODE 0: the pipeline.  MODE 1: copiers only, every prefix taken as 0 (timing of the data movement
+// alone; wrong output -- tools/kbench.py variant 402).  DIAG: per-tile phase timestamps into p.dbg
+// (8 u64 per tile, s_memrealtime at 100 MHz; tools/fused_timeline.py).
+template <int NF, int NV, int MODE = 0, int DIAG = 0>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))) void decode_pipe_kernel(
+    DecodeParams p, u64* flags, u32 epoch) {
+    static_assert(NV == 1 || NV == 2, "decode handles one or two string columns");
+    __shared__ Lds<NV> S;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const u64 n = p.n, ntiles = num_tiles(n);
+    const uintptr_t in = (uintptr_t)p.in;
+    // readable limit of the stream: the 16-byte boundary past its last byte (ABI memory rule)
+    const uintptr_t in_end16 = (in + p.rec_off[n] + 15) & ~(uintptr_t)15;
+    const uintptr_t in_last = in_end16 - 16;
+    const uintptr_t safe = (uintptr_t)flags;  // readable filler address for lanes with nothing to load
+    u64* aw = flags;                          // aggregate words [NV][ntiles]
+    u64* pw = flags + (size_t)NV * ntiles;    // prefix words [NV][ntiles]
+
+    const u32 P = p.pipe_parsers;
+    if (MODE == 0 && blockIdx.x < P) {
+        parser<NF, NV>(p, aw, ntiles, epoch, P);
+        return;
+    }
+    if (MODE == 0 && blockIdx.x == P) {
+        scanner<NV>(aw, pw, ntiles, epoch, p.err, S);
+        return;
+    }
+    const u64 tile = MODE == 0 ? blockIdx.x - P - 1 : blockIdx.x;
+    if (tile >= ntiles) return;
+    auto stamp = [&](int slot) {
+        if constexpr (DIAG)
+            if (tid == 0) p.dbg[tile * 8 + slot] = __builtin_amdgcn_s_memrealtime();
+    };
+    stamp(0);
+    const u64 r0 = tile * kRecs;
+    const int cnt = (int)min((u64)kRecs, n - r0);
+    const u64 s0 = p.rec_off[r0], s1 = p.rec_off[r0 + cnt];
+    const uintptr_t base = (in + s0) & ~(uintptr_t)15;
+    const uintptr_t stop = min((in + s1 + 15) & ~(uintptr_t)15, in_end16);
+    const int nst = (int)min((u64)kStage, (u64)(stop > base ? stop - base : 0));  // multiple of 16
+
+    // ---- 1. stage (and wave 0's record offsets) ----
+    u64 start = 0, endv = 0;
+    if (wave == 0) {
+        start = p.rec_off[r0 + min(lane, cnt)];
+        endv = p.rec_off[r0 + min(lane + 1, cnt)];
+    }
+    {
+        u32x4 sv[kStageLoads];
+#pragma unroll
+        for (int k = 0; k < kStageLoads; ++k) {  // unconditional loads: all in flight together
+            const int c = tid + kThreads * k;
+            sv[k] = ld16u(16 * c < nst ? base + 16 * (uintptr_t)c : safe);
+        }
+#pragma unroll
+        for (int k = 0; k < kStageLoads; ++k) {
+            const int c = tid + kThreads * k;
+            if (16 * c < nst) *(u32x4*)&S.stage[16 * c] = sv[k];
+        }
+    }
+    lds_barrier();
+    stamp(1);
+
+    // ---- 2. parse + 3. prefix (wave 0) ----
+    if (wave == 0) {
+        const bool live = lane < cnt;
+        const u64 L = endv - start;
+        const uintptr_t A = in + start;
+        auto rd8 = [&](u64 q) -> u32 {
+            const u64 a = (u64)(A - base) + q;
+            return a < (u64)nst ? (u32)S.stage[a] : ld_u8(A + q);
+        };
+        auto rd32 = [&](u64 q) -> u32 {
+            const u64 a = (u64)(A - base) + q;
+            return a + 4 <= (u64)nst ? *(const u32*)&S.stage[a] : *(gc_u32*)(A + q);  // unaligned OK
+        };
+        u32 st = 0;
+        int32_t fx[NF > 0 ? NF : 1] = {};
+        u64 flen[NV], fpos[NV];
+#pragma unroll
+        for (int f = 0; f < NV; ++f) flen[f] = fpos[f] = 0;
+        if (live) {
+            if (L < 13) {
+                st = SYM_STATUS_TOO_SHORT;  // "invalid data: too short" (kv.syn.go:681-683)
+            } else if (rd8(0) != 0x01) {
+                st = SYM_STATUS_BAD_VERSION;  // "invalid data: wrong public version" (:686-688)
+            } else {
+                const u64 off2p = rd32(1);
+                if (off2p >= L || rd8(off2p) != 0x01) {
+                    st = SYM_STATUS_NO_PRIVATE;  // "missing private segment" (:696-698)
+                } else {
+                    const u64 pts = off2p + 1;
+                    u64 toff = 0;
+#pragma unroll
+                    for (int f = 0; f < NF; ++f, toff += 4) {  // echo.syn.go:223-231
+                        if (st == 0) {
+                            if (L < pts + toff + 4) st = SYM_STATUS_FIELD_TOO_SHORT;
+                            else fx[f] = (int32_t)rd32(pts + toff);
+                        }
+                    }
+                    if (st == 0) {
+#pragma unroll
+                        for (int f = 0; f < NV; ++f, toff += 4) {  // kv.syn.go:717-742
+                            if (L >= pts + toff + 4) {
+                                u64 q = rd32(pts + toff);
+                                if (q > 0) q += off2p;
+                                if (q > 0 && L >= q + 4) {
+                                    const u64 nb = rd32(q);
+                                    if (L >= q + 4 + nb) {
+                                        flen[f] = nb;
+                                        fpos[f] = q + 4;
+                                    }
+                                }
+                            }
+                        }
+                    }
+                }
+            }
+            p.status[r0 + lane] = (uint8_t)st;
+#pragma unroll
+            for (int f = 0; f < NF; ++f) p.fixed[f][r0 + lane] = fx[f];
+        }
+        // tile scan of the field lengths (each < 2^32)
+        u64 agg[NV], excl[NV];
+        u32 nch[NV];
+        bool too_large = false;
+#pragma unroll
+        for (int f = 0; f < NV; ++f) {
+            const u64 inc = wave_incl_scan_u32w_dpp((u32)flen[f]);
+            agg[f] = (u64)__builtin_amdgcn_readlane((u32)inc, 63) |
+                     ((u64)__builtin_amdgcn_readlane((u32)(inc >> 32), 63) << 32);
+            excl[f] = inc - flen[f];
+            too_large |= agg[f] >= ((u64)1 << 31);  // positions inside a tile's range are 32-bit
+            nch[f] = (u32)((flen[f] + 15) >> 4);
+            S.src[f][lane] = start + fpos[f];
+            S.dst[f][lane] = (int)excl[f];  // lanes >= cnt hold the aggregate
+        }
+        stamp(2);
+        i64 pre[NV];
+        if constexpr (MODE == 0) {
+            u64 wv = 0;
+            if (lane < NV) {
+                // this tile's aggregate (a parser may have published the same value), then its prefix
+                store_word(&aw[(size_t)lane * ntiles + tile], make_word(epoch, kStAgg, lane == 0 ? agg[0] : agg[NV - 1]));
+                u64* a = &pw[(size_t)lane * ntiles + tile];
+                wv = load_word(a);
+                for (unsigned spins = 0; !tagged(wv, epoch);) {
+                    if (++spins >= kSpinLimit) {
+                        atomicOr(p.err, kErrTimeout);
+                        wv = make_word(epoch, kStPre, 0);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                    wv = load_word(a);
+                }
+            }
+            pre[0] = (i64)((u64)__shfl((long long)wv, 0, 64) & kValMask);
+            if constexpr (NV == 2) pre[1] = (i64)((u64)__shfl((long long)wv, 1, 64) & kValMask);
+        } else {  // timing only: spread the tiles over the columns in proportion to their stream offset
+            const double frac = (double)(s0 - p.rec_off[0]) / (double)(p.rec_off[n] - p.rec_off[0] + 1);
+#pragma unroll
+            for (int f = 0; f < NV; ++f) pre[f] = (i64)(frac * (double)p.cap[f]);
+        }
+        stamp(3);
+#pragma unroll
+        for (int f = 0; f < NV; ++f) {
+            if (live) p.offs[f][r0 + lane] = (u64)pre[f] + excl[f];
+            if (lane == 0 && r0 + cnt == n) p.offs[f][n] = (u64)pre[f] + agg[f];
+        }
+        const u32 nrec = nch[0] + (NV == 2 ? nch[NV - 1] : 0u);
+        const u32 cinc = wave_incl_scan_u32_dpp(nrec);
+        S.cs[lane] = (int)(cinc - nrec);
+        S.nch0[lane] = (int)nch[0];
+        if (lane == 0) {
+            const int T = (int)__builtin_amdgcn_readlane(cinc, 63);
+            S.cs[kRecs] = T;
+#pragma unroll
+            for (int f = 0; f < NV; ++f) {
+                S.dst[f][kRecs] = (int)agg[f];
+                S.pre[f] = pre[f];
+                const i64 cap = (i64)p.cap[f];
+                if (MODE == 0 && agg[f] > 0 && pre[f] + (i64)agg[f] > cap) atomicOr(p.err, kErrCapacity);
+                S.lim[f] = max((i64)0, min((i64)agg[f], cap - pre[f]));
+            }
+            S.total = too_large ? -1 : T;
+        }
+        if (__ballot(too_large) && lane == 0) atomicOr(p.err, kErrTooLarge);
+    }
+    lds_barrier();
+
+    // ---- 4. copy (all lanes) ----
+    const int T = __builtin_amdgcn_readfirstlane(S.total);
+    // per-column values as named scalars: a two-element array indexed by a lane value goes to scratch
+    const i64 pre0 = uniform_i64(S.pre[0]), pre1 = uniform_i64(S.pre[NV - 1]);
+    const i64 lim0 = uniform_i64(S.lim[0]), lim1 = uniform_i64(S.lim[NV - 1]);
+    const uintptr_t stage_end = base + (uintptr_t)nst;
+    for (int c0 = 0; c0 < T; c0 += kThreads * kU) {  // uniform loop
+        u32x4 v[kU];
+        int P_[kU], code[kU];
+        uintptr_t X[kU];
+        bool glob[kU];
+        bool anyg = false;
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int c = c0 + kThreads * u + tid;
+            const bool has = c < T;
+            const int k = has ? lds_search_64(S.cs, cnt, c) : 0;
+            int q = c - S.cs[k];
+            const int n0 = S.nch0[k];
+            const bool second = NV == 2 && q >= n0;
+            if (second) q -= n0;
+            const int f = second ? 1 : 0;
+            const int dk = S.dst[f][k], L = S.dst[f][k + 1] - dk;
+            const int off = L >= 16 ? min(16 * q, L - 16) : 0;
+            X[u] = in + S.src[f][k] + (uintptr_t)off;
+            glob[u] = has && X[u] + 16 > stage_end;
+            anyg |= glob[u];
+            P_[u] = has ? dk + off : -1;
+            code[u] = min(L, 16) | (second ? 1 << 10 : 0);
+            v[u] = has && !glob[u] ? lds16u(S.stage, (int)(X[u] - base)) : u32x4{0, 0, 0, 0};
+        }
+        if (__ballot(anyg)) {  // past the staged span: HBM loads, all issued before any use
+            u32x4 g[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const uintptr_t Xc = X[u] < in_last ? X[u] : in_last;
+                g[u] = ld16u(glob[u] ? Xc : safe);
+                code[u] |= glob[u] ? (int)((X[u] - Xc) << 5) : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const u32 sh = ((u32)code[u] >> 5) & 31u;
+                if (sh) {  // a short field read from the stream's last block: shift down
+                    u32 t[4];
+                    funnel16(g[u], u32x4{0, 0, 0, 0}, sh, t);
+                    g[u] = u32x4{t[0], t[1], t[2], t[3]};
+                }
+                if (glob[u]) v[u] = g[u];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const bool second = (code[u] >> 10) & 1;
+            const int nb = code[u] & 31;
+            const i64 hi = min((i64)(P_[u] + nb), second ? lim1 : lim0);
+            uint8_t* colb = second ? p.bytes[NV - 1] + pre1 : p.bytes[0] + pre0;
+            const bool full = P_[u] >= 0 && (i64)P_[u] + 16 <= hi;
+            if (full) *(g_u4*)(colb + P_[u]) = v[u];
+            const bool part = P_[u] >= 0 && !full && (i64)P_[u] < hi;
+            if (__ballot(part)) {
+                const u32 rr[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+                if (part) store_chunk(colb, P_[u], 0, hi, rr);
+            }
+        }
+    }
+    stamp(4);
+    if constexpr (DIAG)
+        if (tid == 0) p.dbg[tile * 8 + 5] = blockIdx.x;
+}
+
+template <int NF, int NV, int MODE, int DIAG>
+hipError_t launch(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stream) {
+    if (DIAG && !p.dbg) return hipErrorInvalidValue;  // timestamps need SYMHIP_DEBUG_PTR
+    static int cus[16] = {0};
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    int& ncu = cus[dev & 15];
+    if (ncu == 0 && (e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
+    const u64 nt = num_tiles(p.n);
+    u64 P = MODE == 0 ? (u64)ncu : 0;  // one parser workgroup per CU
+    if (P > (nt + 3) / 4) P = (nt + 3) / 4;
+    DecodeParams q = p;
+    q.pipe_parsers = (unsigned)P;
+    const u64 grid = MODE == 0 ? P + 1 + nt : nt;
+    hipLaunchKernelGGL((decode_pipe_kernel<NF, NV, MODE, DIAG>), dim3((unsigned)grid), dim3(kThreads), 0, stream, q,
+                       flags, epoch);
+    return hipGetLastError();
+}
+
+template <int MODE, int DIAG>
+hipError_t launch_layout(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stream) {
+    if (p.lay.nfixed == 0 && p.lay.nvar == 1) return launch<0, 1, MODE, DIAG>(p, flags, epoch, stream);
+    if (p.lay.nfixed == 0 && p.lay.nvar == 2) return launch<0, 2, MODE, DIAG>(p, flags, epoch, stream);
+    if (p.lay.nfixed == 2 && p.lay.nvar == 2) return launch<2, 2, MODE, DIAG>(p, flags, epoch, stream);
+    return hipErrorInvalidValue;
+}
+
+}  // namespace pipe
+
+size_t decode_pipe_flag_bytes(int nvar, uint64_t n) {
+    // aggregate + prefix word per column and tile; >= 256 bytes: the kernels' filler load address
+    return ((size_t)nvar * 2 * pipe::num_tiles(n) * sizeof(u64) + 256 + 255) & ~(size_t)255;
+}
+
+// variants: 0 the pipeline; 402 data movement only (timing, wrong output); 410 / 412 the same with
+// per-tile timestamps (SYMHIP_DEBUG_PTR)
+hipError_t launch_decode_pipe(const DecodeParams& p, void* flags, unsigned epoch, hipStream_t stream) {
+    u64* fl = (u64*)flags;
+    switch (p.variant) {
+        case 402: return pipe::launch_layout<1, 0>(p, fl, epoch, stream);
+        case 410: return pipe::launch_layout<0, 1>(p, fl, epoch, stream);
+        case 412: return pipe::launch_layout<1, 1>(p, fl, epoch, stream);
+        default: return pipe::launch_layout<0, 0>(p, fl, epoch, stream);
+    }
+}
+
+}  // namespace symhip

@@ -12,7 +12,8 @@ one: step s encodes set s%4 and decodes the stream encoded two steps earlier.
 Prints ONE JSON line on rank 0.  `value` = algorithmic GB/s over all ranks (SURVEY.md
 section 8d: 694 B encode + 695 B decode per 64/256 record), timed with a barrier +
 device sync on both sides, max over ranks.  `roofline` reports the dominant single kernel
-(encode, or decode's copy kernel) from HIP events on the stream the kernels run on; `cpu_baseline` times the C oracle (a restatement of the Go codec,
+(encode_kernel, or the one-launch decode_pipe_kernel) from HIP events on the stream the kernels
+run on; `cpu_baseline` times the C oracle (a restatement of the Go codec,
 single thread) on a bounded sample on this host.
 """
 from __future__ import annotations
@@ -37,20 +38,11 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 NSETS = 4
 
 
-DECODE_COPY_STEPS = 4  # decode.hip kRB: the default decode_copy_kernel<NV, kRB> instantiation
-
-
 def alg_bytes(n: int, nvar: int, var_total: int, stream_total: int) -> tuple[int, int]:
     """Algorithmic bytes of one encode and one decode call."""
     enc = var_total + 8 * nvar * n + stream_total + 8 * n
     dec = stream_total + 8 * n + var_total + 8 * nvar * n + n
     return enc, dec
-
-
-def copy_alg_bytes(n: int, nvar: int, var_total: int) -> int:
-    """Algorithmic bytes of decode's copy kernel: payload read and written, record offsets in,
-    column offsets out (the parse kernel's share -- headers, status, int32 fields -- excluded)."""
-    return 2 * var_total + 8 * n + 8 * nvar * n
 
 
 def dist_setup():
@@ -251,27 +243,34 @@ def main():
     dec_ms = float(np.mean([a.elapsed_time(b_) for a, b_ in ev["dec"]]))
     enc_b, dec_b = alg_bytes(n, s.nvar, var_total, total)
     value = world * (enc_b + dec_b) * args.steps / elapsed / 1e9
-    # decode = parse + scan + copy kernels; time parse + scan alone (decode variant 301, outside
-    # the timed region, same buffers and stream) so the copy kernel's share is a live number too
-    ps_ev = []
-    os.environ["SYMHIP_DECODE_VARIANT"] = "301"
-    for i in range(max(5, args.steps // 2)):
-        d = (i + 2) % NSETS
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        codec.decode(s, enc[d][0], enc[d][1], outputs=dec[d])
-        e1.record()
-        ps_ev.append((e0, e1))
-    del os.environ["SYMHIP_DECODE_VARIANT"]
-    torch.cuda.synchronize()
-    ps_ms = float(np.mean([a.elapsed_time(b_) for a, b_ in ps_ev]))
-    copy_ms = max(dec_ms - ps_ms, 1e-6)
-    copy_b = copy_alg_bytes(n, s.nvar, var_total)
-    # roofline: the dominant single kernel by time
-    if enc_ms >= copy_ms:
+    # Reference points for the decode, outside the timed region on the same buffers and stream:
+    # the three-kernel decode (variant 300) and the pipeline's data movement alone (variant 402:
+    # copiers only, prefixes taken as 0 -- wrong output, the bound the in-kernel scan costs against).
+    def time_variant(v: str, reps: int) -> float:
+        evs = []
+        os.environ["SYMHIP_DECODE_VARIANT"] = v
+        try:
+            for i in range(reps):
+                d = (i + 2) % NSETS
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                codec.decode(s, enc[d][0], enc[d][1], outputs=dec[d])
+                e1.record()
+                evs.append((e0, e1))
+        finally:
+            del os.environ["SYMHIP_DECODE_VARIANT"]
+        torch.cuda.synchronize()
+        return float(np.mean([a.elapsed_time(b_) for a, b_ in evs]))
+
+    reps = max(5, args.steps // 2)
+    three_ms = time_variant("300", reps)
+    move_ms = time_variant("402", reps)
+    codec.check()
+    # roofline: the dominant single kernel by time (the default decode is one launch)
+    if enc_ms >= dec_ms:
         kname, dom_ms, dom_bytes = f"encode_kernel<{s.nfixed}, {s.nvar}, 0>", enc_ms, enc_b
     else:
-        kname, dom_ms, dom_bytes = f"decode_copy_kernel<{s.nvar}, {DECODE_COPY_STEPS}>", copy_ms, copy_b
+        kname, dom_ms, dom_bytes = f"decode_pipe_kernel<{s.nfixed}, {s.nvar}, 0, 0>", dec_ms, dec_b
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     traffic = load_traffic(kname)
 
@@ -302,8 +301,12 @@ def main():
                                "gbps": round(enc_b / enc_ms / 1e6, 1)},
                     "decode": {"avg_ms": round(dec_ms, 4), "alg_bytes": dec_b,
                                "gbps": round(dec_b / dec_ms / 1e6, 1),
-                               "parse_scan_ms": round(ps_ms, 4), "copy_ms": round(copy_ms, 4),
-                               "copy_alg_bytes": copy_b, "copy_gbps": round(copy_b / copy_ms / 1e6, 1)}},
+                               "kernel": f"decode_pipe_kernel<{s.nfixed}, {s.nvar}, 0, 0>",
+                               "three_kernel_ms": round(three_ms, 4),
+                               "three_kernel_gbps": round(dec_b / three_ms / 1e6, 1),
+                               "movement_only_ms": round(move_ms, 4),
+                               "movement_only_note": "variant 402: copiers without the scan (wrong output); "
+                                                     "the data-movement bound of the pipeline"}},
         "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic},
     }

@@ -23,6 +23,17 @@ def dev():
     return torch.device("cuda", 0)
 
 
+@pytest.fixture(autouse=True, params=["pipe", "three_kernel"])
+def decode_impl(request, monkeypatch):
+    """Every test runs against both decode implementations behind the same C ABI: the default
+    single-launch pipeline (decode_pipe.hip) and the three-kernel path (decode.hip, variant 300)."""
+    if request.param == "three_kernel":
+        monkeypatch.setenv("SYMHIP_DECODE_VARIANT", "300")
+    else:
+        monkeypatch.delenv("SYMHIP_DECODE_VARIANT", raising=False)
+    return request.param
+
+
 @pytest.fixture(scope="module")
 def codec(dev):
     from arpc_amd.codec import Codec

@@ -14,7 +14,7 @@ from collections import defaultdict
 
 
 def short(name: str) -> str:
-    m = re.search(r"symhip::(\w+<[^>]*>)", name)
+    m = re.search(r"symhip::(?:\w+::)*(\w+<[^>]*>)", name)
     return m.group(1) if m else name[:60]
 
 
