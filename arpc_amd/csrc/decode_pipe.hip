@@ -48,7 +48,10 @@ constexpr int kEpochShift = 44;
 constexpr u64 kStAgg = 1ull << 42;
 constexpr u64 kStPre = 2ull << 42;
 constexpr u64 kValMask = (1ull << 42) - 1;
-constexpr unsigned kSpinLimit = 1u << 21;  // bounded waits: a stuck call reports kErrTimeout and drains
+// Bounded waits, in wall time (s_memrealtime runs at 100 MHz): a wait that outlives this reports
+// kErrTimeout (SYM_ERR_DEVICE from sym_ctx_check) and gives up, so the grid always drains.
+constexpr u64 kWaitTicks = 25000000;  // 250 ms
+__device__ __forceinline__ u64 now_ticks() { return __builtin_amdgcn_s_memrealtime(); }
 
 __host__ __device__ inline u64 num_tiles(u64 n) { return (n + kRecs - 1) / kRecs; }
 
@@ -190,7 +193,7 @@ __device__ void scanner(u64* aw, u64* pw, u64 ntiles, u32 epoch, unsigned* err, 
     u64 carry[NV];
 #pragma unroll
     for (int f = 0; f < NV; ++f) carry[f] = 0;
-    unsigned idle = 0;
+    u64 idle_since = 0;  // 0: the frontier moved on the last step
     for (u64 base = 0; base < ntiles;) {
         const u64 t0 = base + (u64)tid * kPer;
         u64 v[NV][kPer];
@@ -215,14 +218,16 @@ __device__ void scanner(u64* aw, u64* pw, u64 ntiles, u32 epoch, unsigned* err, 
         lds_barrier();  // S.first is rewritten by the next step
         m = (u32)min((u64)m, ntiles - base);
         if (m == 0) {  // the frontier has not moved: wait a little (bounded)
-            if (++idle >= kSpinLimit) {
+            const u64 t = uniform_i64((i64)now_ticks());
+            if (idle_since == 0) idle_since = t;
+            if (t - idle_since > kWaitTicks) {
                 if (tid == 0) atomicOr(err, kErrTimeout);
                 return;
             }
             __builtin_amdgcn_s_sleep(2);
             continue;
         }
-        idle = 0;
+        idle_since = 0;
 #pragma unroll
         for (int f = 0; f < NV; ++f) {
             u64 x[kPer], sum = 0;
@@ -401,8 +406,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
                 store_word(&aw[(size_t)lane * ntiles + tile], make_word(epoch, kStAgg, lane == 0 ? agg[0] : agg[NV - 1]));
                 u64* a = &pw[(size_t)lane * ntiles + tile];
                 wv = load_word(a);
-                for (unsigned spins = 0; !tagged(wv, epoch);) {
-                    if (++spins >= kSpinLimit) {
+                for (const u64 t0 = now_ticks(); !tagged(wv, epoch);) {
+                    if (now_ticks() - t0 > kWaitTicks) {
                         atomicOr(p.err, kErrTimeout);
                         wv = make_word(epoch, kStPre, 0);
                         break;
