@@ -51,7 +51,24 @@ SIGNATURES = {
                                _vp]),
     "sym_encode_host": (_int, [_ctx, _int, _u64, _vp, _vp, _vp, _u32, _u32, _u8p, _u64p]),
     "sym_decode_host": (_int, [_ctx, _int, _u64, _u8p, _u64p, _vp, _vp, _vp, _vp, _u8p]),
+    "sym_fragment_plan": (_int, [_ctx, _u8p, _u64p, _u64, _u32, _u64p, _u64p, _u8p, _vp]),
+    "sym_fragment_write": (_int, [_ctx, _u8p, _u64p, _u64, _u32, ctypes.c_uint8, _u64p, _vp, _u64p, _u64p, _u8p,
+                                  _u8p, _u64p, _vp]),
 }
+
+SYM_MAX_UDP_PAYLOAD = 1400
+SYM_DATA_PACKET_HEADER = 31
+SYM_PACKET_REQUEST = 1
+SYM_PACKET_RESPONSE = 2
+SYM_FRAG_OK = 0
+SYM_FRAG_TOO_SHORT = 1
+SYM_FRAG_BAD_OFFSET = 2
+
+
+class Endpoints(ctypes.Structure):
+    """struct sym_endpoints (include/symphony_hip.h)."""
+    _fields_ = [("dst_ip", ctypes.c_uint8 * 4), ("dst_port", ctypes.c_uint16),
+                ("src_ip", ctypes.c_uint8 * 4), ("src_port", ctypes.c_uint16)]
 
 _lib = None
 

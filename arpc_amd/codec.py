@@ -144,6 +144,49 @@ class Codec:
         return outputs
 
 
+@dataclass
+class Datagrams:
+    wire: torch.Tensor     # uint8 [total bytes]: every serialized DataPacket back to back
+    dg_off: torch.Tensor   # int64 [datagrams+1]: datagram j is wire[dg_off[j]:dg_off[j+1]]
+    first: torch.Tensor    # int64 [n+1]: record i's first datagram
+    wire_off: torch.Tensor  # int64 [n+1]: record i's first wire byte
+    status: torch.Tensor   # uint8 [n]: SYM_FRAG_*
+
+
+def _fragment(codec: "Codec", data: torch.Tensor, rec_off: torch.Tensor, rpc_id: torch.Tensor,
+              packet_type: int = _native.SYM_PACKET_REQUEST, dst=((127, 0, 0, 1), 9000), src=((127, 0, 0, 1), 9001),
+              max_udp_payload: int = _native.SYM_MAX_UDP_PAYLOAD, stream=None) -> Datagrams:
+    """aRPC's send side (FragmentPackets + DataPacket framing, pkg/transport/transport.go:146-201) for n
+    marshalled records; one sync between the plan and the write (the output size depends on the data)."""
+    _check_col(data, torch.uint8, "data", codec.device)
+    _check_col(rec_off, torch.int64, "rec_off", codec.device)
+    _check_col(rpc_id, torch.int64, "rpc_id", codec.device)
+    n = rec_off.numel() - 1
+    if rpc_id.numel() < n:
+        raise ValueError(f"rpc_id has {rpc_id.numel()} < {n} entries")
+    dev, sh = codec.device, _stream_handle(codec.device, stream)
+    first = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    wire_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    status = torch.empty(max(1, n), dtype=torch.uint8, device=dev)
+    _native.check(codec._lib.sym_fragment_plan(codec._ctx, _dptr(data) if data.numel() else 1, _dptr(rec_off), n,
+                                              max_udp_payload, _dptr(first), _dptr(wire_off), _dptr(status), sh),
+                  "sym_fragment_plan")
+    s = stream if stream is not None else torch.cuda.current_stream(dev)
+    s.synchronize()
+    total_dg, total = int(first[n].item()), int(wire_off[n].item())
+    wire = torch.empty(max(1, total), dtype=torch.uint8, device=dev)
+    dg_off = torch.empty(total_dg + 1, dtype=torch.int64, device=dev)
+    ep = _native.Endpoints((ctypes.c_uint8 * 4)(*dst[0]), dst[1], (ctypes.c_uint8 * 4)(*src[0]), src[1])
+    _native.check(codec._lib.sym_fragment_write(codec._ctx, _dptr(data) if data.numel() else 1, _dptr(rec_off), n,
+                                               max_udp_payload, packet_type, _dptr(rpc_id), ctypes.byref(ep),
+                                               _dptr(first), _dptr(wire_off), _dptr(status), _dptr(wire),
+                                               _dptr(dg_off), sh), "sym_fragment_write")
+    return Datagrams(wire[:total] if total else wire[:0], dg_off, first, wire_off, status[:n])
+
+
+Codec.fragment = _fragment
+
+
 def to_device(batch, device) -> tuple[list, list]:
     """datagen.Batch (numpy) -> (fixed int32 tensors, [(uint8 tensor, int64 offsets tensor)]) on device."""
     fixed = [torch.from_numpy(c).to(device) for c in batch.fixed]

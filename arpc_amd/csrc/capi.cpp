@@ -31,6 +31,9 @@ struct sym_ctx {
     void* pool = nullptr;
     size_t pool_bytes = 0;
     hipStream_t stream = nullptr;
+    // packetization plan: per-record counts / bytes (scan inputs) and the rocPRIM scan storage
+    void* frag = nullptr;
+    size_t frag_bytes = 0;
 };
 
 namespace {
@@ -92,6 +95,7 @@ int ensure_flags(sym_ctx* ctx, uint64_t n) {
     const size_t need = symhip::decode_pipe_flag_bytes(symhip::kMaxVar, n);
     if (need <= ctx->flag_bytes) return SYM_OK;
     if (ctx->flags) (void)hipFree(ctx->flags);
+    if (ctx->frag) (void)hipFree(ctx->frag);
     ctx->flags = nullptr;
     ctx->flag_bytes = 0;
     hipError_t e = hipMalloc(&ctx->flags, need);
@@ -166,6 +170,7 @@ int sym_ctx_destroy(sym_ctx* ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->ws) (void)hipFree(ctx->ws);
     if (ctx->flags) (void)hipFree(ctx->flags);
+    if (ctx->frag) (void)hipFree(ctx->frag);
     if (ctx->err) (void)hipFree(ctx->err);
     if (ctx->pool) (void)hipFree(ctx->pool);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -497,6 +502,76 @@ int sym_decode_host(sym_ctx* ctx, int schema, uint64_t n, const uint8_t* h_in, c
     if (e == hipSuccess) e = hipMemcpyAsync(h_status, base + o_status, n, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     return e == hipSuccess ? SYM_OK : hip_fail(e, "sym_decode_host D2H");
+}
+
+// ---- packetization ----
+
+int sym_fragment_plan(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_off, uint64_t n,
+                      uint32_t max_udp_payload, uint64_t* d_first, uint64_t* d_wire_off, uint8_t* d_status,
+                      void* stream) {
+    if (!ctx) return fail(SYM_ERR_INVALID, "sym_fragment_plan: ctx is NULL");
+    if (max_udp_payload <= SYM_DATA_PACKET_HEADER)  // FragmentPackets: "MTU must be positive"
+        return fail(SYM_ERR_INVALID, "sym_fragment_plan: max_udp_payload %u leaves no payload", max_udp_payload);
+    if (!d_rec_off || !d_first || !d_wire_off || (n && (!d_in || !d_status)))
+        return fail(SYM_ERR_INVALID, "sym_fragment_plan: NULL argument");
+    DeviceGuard g(ctx->device);
+    if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
+    const size_t cols = align256((n + 1) * sizeof(uint64_t));
+    const size_t temp = symhip::frag_scan_temp_bytes(n);
+    const size_t need = 2 * cols + temp;
+    if (need > ctx->frag_bytes) {
+        if (ctx->frag) (void)hipFree(ctx->frag);
+        ctx->frag = nullptr;
+        ctx->frag_bytes = 0;
+        hipError_t e = hipMalloc(&ctx->frag, need);
+        if (e != hipSuccess) return fail(SYM_ERR_NOMEM, "packetization workspace of %zu bytes: %s", need, hipGetErrorString(e));
+        ctx->frag_bytes = need;
+    }
+    uint64_t* cnt = (uint64_t*)ctx->frag;
+    uint64_t* bytes = (uint64_t*)((char*)ctx->frag + cols);
+    void* tmp = (char*)ctx->frag + 2 * cols;
+    hipError_t e = symhip::launch_frag_plan(d_in, d_rec_off, n, max_udp_payload - SYM_DATA_PACKET_HEADER, cnt, bytes,
+                                            d_first, d_wire_off, d_status, tmp, temp, (hipStream_t)stream);
+    return e == hipSuccess ? SYM_OK : hip_fail(e, "fragment plan launch");
+}
+
+int sym_fragment_write(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_off, uint64_t n,
+                       uint32_t max_udp_payload, uint8_t packet_type, const uint64_t* d_rpc_id,
+                       const sym_endpoints* endpoints, const uint64_t* d_first, const uint64_t* d_wire_off,
+                       const uint8_t* d_status, uint8_t* d_wire, uint64_t* d_dg_off, void* stream) {
+    if (!ctx) return fail(SYM_ERR_INVALID, "sym_fragment_write: ctx is NULL");
+    if (max_udp_payload <= SYM_DATA_PACKET_HEADER)
+        return fail(SYM_ERR_INVALID, "sym_fragment_write: max_udp_payload %u leaves no payload", max_udp_payload);
+    if (!endpoints || !d_dg_off || (n && (!d_in || !d_rec_off || !d_rpc_id || !d_first || !d_wire_off || !d_status ||
+                                          !d_wire)))
+        return fail(SYM_ERR_INVALID, "sym_fragment_write: NULL argument");
+    DeviceGuard g(ctx->device);
+    if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
+    if (n == 0) {
+        hipError_t e = hipMemsetAsync(d_dg_off, 0, sizeof(uint64_t), (hipStream_t)stream);
+        return e == hipSuccess ? SYM_OK : hip_fail(e, "hipMemsetAsync");
+    }
+    symhip::FragWriteArgs a{};
+    a.in = d_in;
+    a.rec_off = d_rec_off;
+    a.n = n;
+    a.M = max_udp_payload - SYM_DATA_PACKET_HEADER;
+    a.type = packet_type;
+    a.rpc_id = d_rpc_id;
+    for (int i = 0; i < 4; ++i) {
+        a.dst_ip[i] = endpoints->dst_ip[i];
+        a.src_ip[i] = endpoints->src_ip[i];
+    }
+    a.dst_port = endpoints->dst_port;
+    a.src_port = endpoints->src_port;
+    a.first = d_first;
+    a.out_off = d_wire_off;
+    a.status = d_status;
+    a.out = d_wire;
+    a.dg_off = d_dg_off;
+    a.err = ctx->err;
+    hipError_t e = symhip::launch_frag_write(a, (hipStream_t)stream);
+    return e == hipSuccess ? SYM_OK : hip_fail(e, "fragment write launch");
 }
 
 }  // extern "C"

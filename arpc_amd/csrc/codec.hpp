@@ -73,6 +73,29 @@ hipError_t launch_decode_pipe(const DecodeParams& p, void* flags, unsigned epoch
 // compare variants inside one process.
 int tuning_variant(const char* env_name);
 
+// ---- packetization (packetize.hip)
+struct FragWriteArgs {
+    const uint8_t* in;
+    const uint64_t* rec_off;
+    uint64_t n;
+    uint64_t M;  // payload bytes per datagram: max UDP payload - 31
+    uint8_t type;
+    const uint64_t* rpc_id;
+    uint8_t dst_ip[4], src_ip[4];
+    uint16_t dst_port, src_port;
+    const uint64_t* first;
+    const uint64_t* out_off;
+    const uint8_t* status;
+    uint8_t* out;
+    uint64_t* dg_off;
+    unsigned* err;
+};
+size_t frag_scan_temp_bytes(uint64_t n);
+hipError_t launch_frag_plan(const uint8_t* in, const uint64_t* rec_off, uint64_t n, uint64_t M, uint64_t* cnt,
+                            uint64_t* bytes, uint64_t* first, uint64_t* out_off, uint8_t* status, void* temp,
+                            size_t temp_bytes, hipStream_t stream);
+hipError_t launch_frag_write(const FragWriteArgs& a, hipStream_t stream);
+
 hipError_t launch_encode(const EncodeParams& p, hipStream_t stream);
 hipError_t launch_decode(const DecodeParams& p, hipStream_t stream);
 

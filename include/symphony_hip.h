@@ -153,6 +153,43 @@ int sym_decode_host(sym_ctx* ctx, int schema, uint64_t n, const uint8_t* h_in, c
                     int32_t* const* h_fixed, uint8_t* const* h_bytes, const uint64_t* caps, uint64_t* const* h_offs,
                     uint8_t* h_status);
 
+/* ---- packetization: aRPC's send side over a batch of marshalled records ----------
+ * What UDPTransport.Send does to one message (pkg/transport/transport.go:146-201), for n records:
+ * FragmentPackets(data, max_udp_payload - 31) (pkg/transport/symphony_fragmentation.go:23-125), then
+ * one serialized DataPacket per fragment (pkg/packet/builtin_packets.go:59-114): a 31-byte
+ * little-endian header {type, rpc_id, TotalPackets = uint16(#fragments), SeqNumber = uint16(index),
+ * MoreFragments = 0, FragmentIndex = 0, dst ip/port, src ip/port, payload length} and the fragment.
+ * The wire output is every datagram back to back, record after record, datagram j at
+ * wire[dg_off[j] .. dg_off[j+1]): the byte strings Send passes to WriteToUDP, in order.
+ * Two calls, because the output size depends on the data:
+ *   sym_fragment_plan   first[n+1]: datagrams before record i ([n] = total datagrams);
+ *                       wire_off[n+1]: wire bytes before record i ([n] = total bytes);
+ *                       status[n]: SYM_FRAG_* (a failed record emits nothing, as Send returns
+ *                       the error before sending).
+ *   sym_fragment_write  the datagrams, and dg_off[first[n] + 1]. */
+#define SYM_MAX_UDP_PAYLOAD 1400 /* MaxUDPPayloadSize, pkg/packet/codec.go:10 */
+#define SYM_DATA_PACKET_HEADER 31
+#define SYM_PACKET_REQUEST 1  /* PacketTypeRequest, builtin_packets.go:15 */
+#define SYM_PACKET_RESPONSE 2 /* PacketTypeResponse, builtin_packets.go:16 */
+#define SYM_FRAG_OK 0
+#define SYM_FRAG_TOO_SHORT 1  /* "data too short for offset header" (symphony_fragmentation.go:33-35) */
+#define SYM_FRAG_BAD_OFFSET 2 /* "invalid offset" (symphony_fragmentation.go:37-39) */
+
+typedef struct sym_endpoints {
+    uint8_t dst_ip[4]; /* IPv4 bytes as in the packet (e.g. 127,0,0,1) */
+    uint16_t dst_port;
+    uint8_t src_ip[4];
+    uint16_t src_port;
+} sym_endpoints;
+
+int sym_fragment_plan(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_off, uint64_t n,
+                      uint32_t max_udp_payload, uint64_t* d_first, uint64_t* d_wire_off, uint8_t* d_status,
+                      void* stream);
+int sym_fragment_write(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_off, uint64_t n,
+                       uint32_t max_udp_payload, uint8_t packet_type, const uint64_t* d_rpc_id,
+                       const sym_endpoints* endpoints, const uint64_t* d_first, const uint64_t* d_wire_off,
+                       const uint8_t* d_status, uint8_t* d_wire, uint64_t* d_dg_off, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

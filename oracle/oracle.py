@@ -121,3 +121,49 @@ def decode_batch(nfixed: int, nvar: int, data: np.ndarray, rec_off: np.ndarray):
     lib().sym_oracle_decode_batch(nfixed, nvar, n, _ptr(data) if data.size else 0, _ptr(rec_off),
                                   _ptr_array(fixed), _ptr_array(cols), _ptr_array(offs), _ptr(status))
     return ([f[:n] for f in fixed], [(cols[i][:int(offs[i][-1])], offs[i]) for i in range(nvar)], status[:n])
+
+
+# ---------------------------------------------------------------- packetization (fragment_oracle.c)
+FRAG_OK = 0
+FRAG_TOO_SHORT = 1   # "data too short for offset header" (pkg/transport/symphony_fragmentation.go:33-35)
+FRAG_BAD_OFFSET = 2  # "invalid offset" (:37-39)
+
+
+def _frag_lib():
+    L = lib()
+    if not getattr(L, "_frag_ready", False):
+        u64, vp = ctypes.c_uint64, ctypes.c_void_p
+        L.sym_oracle_fragment_plan.restype = None
+        L.sym_oracle_fragment_plan.argtypes = [u64, vp, vp, ctypes.c_uint32, vp, vp, vp]
+        L.sym_oracle_fragment_write.restype = None
+        L.sym_oracle_fragment_write.argtypes = [u64, vp, vp, ctypes.c_uint32, ctypes.c_uint8, vp, vp,
+                                                ctypes.c_uint16, vp, ctypes.c_uint16, vp, vp, vp]
+        L._frag_ready = True
+    return L
+
+
+def fragment_batch(data: np.ndarray, rec_off: np.ndarray, rpc_id: np.ndarray, packet_type: int = 1,
+                   dst=(b"\x7f\x00\x00\x01", 9000), src=(b"\x7f\x00\x00\x01", 9001), max_udp_payload: int = 1400):
+    """FragmentPackets + DataPacket serialization of every record, as aRPC's Send loop.
+
+    Returns (wire u8 array, dg_off u64 [total_dg+1], first u64 [n+1], out_off u64 [n+1], status u8 [n])."""
+    L = _frag_lib()
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    rec_off = np.ascontiguousarray(rec_off, dtype=np.uint64)
+    rpc_id = np.ascontiguousarray(rpc_id, dtype=np.uint64)
+    n = len(rec_off) - 1
+    first = np.zeros(n + 1, np.uint64)
+    out_off = np.zeros(n + 1, np.uint64)
+    status = np.zeros(max(1, n), np.uint8)
+    dp = _ptr(data) if data.size else 0
+    L.sym_oracle_fragment_plan(n, dp, _ptr(rec_off), max_udp_payload, _ptr(first), _ptr(out_off), _ptr(status))
+    total_dg, total = int(first[n]), int(out_off[n])
+    out = np.zeros(max(1, total), np.uint8)
+    dg_off = np.zeros(total_dg + 1, np.uint64)
+    longest = int(np.max(np.diff(rec_off))) if n else 0
+    scratch = np.zeros(longest // max(1, max_udp_payload - 31) + 4, np.uint64)
+    dip = np.frombuffer(bytes(dst[0]), np.uint8).copy()
+    sip = np.frombuffer(bytes(src[0]), np.uint8).copy()
+    L.sym_oracle_fragment_write(n, dp, _ptr(rec_off), max_udp_payload, packet_type, _ptr(rpc_id) if n else 0,
+                                _ptr(dip), dst[1], _ptr(sip), src[1], _ptr(out), _ptr(dg_off), _ptr(scratch))
+    return out[:total], dg_off, first, out_off, status[:n]
