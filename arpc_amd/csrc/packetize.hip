@@ -217,6 +217,11 @@ __global__ __launch_bounds__(kWaves * 64) void frag_write_kernel(WriteParams p) 
     const i64 mis = (i64)((uintptr_t)p.out & 15);
     const int firstc = (int)((((i64)T0 + mis) & ~(i64)15) - mis - (i64)T0);  // in (-16, 0]
     uint8_t* const out_t = p.out + T0;
+    // A 16-byte payload window reads up to 31 bytes before its fragment and 15 after: inside the
+    // stream unless the tile sits within 32 bytes of the stream's ends (batch edges).
+    const u64 s_lo = p.rec_off[0], s_hi = p.rec_off[p.n];
+    const bool tile_safe = p.rec_off[r0] >= s_lo + 32 && p.rec_off[r0 + cnt] + 16 <= s_hi;
+    const uintptr_t dummy = (uintptr_t)p.in & ~(uintptr_t)15;  // any readable block; its bytes are masked off
     // header window at datagram byte b in [-16, 31) of record k's template, with seq / len patched
     auto header_window = [&](int k, int b, u64 seq, u64 flen) -> u32x4 {
         u32x4 v = lds16u(S.tmpl, k * kSlot + 16 + b);
@@ -240,10 +245,14 @@ __global__ __launch_bounds__(kWaves * 64) void frag_write_kernel(WriteParams p) 
         if (b < kHdr) r = header_window(k, b, d, fl);
         {  // payload bytes of this datagram inside the chunk: chunk offsets [kHdr - b, kHdr + fl - b)
             const int lo = max(kHdr - b, 0);
-            const i64 hi = min((i64)kHdr + (i64)fl - b, (i64)16);
-            if ((i64)lo < hi) {
+            const int hi = (int)min((i64)kHdr + (i64)fl - b, (i64)16);
+            const uintptr_t X0 = (uintptr_t)(S.addr[k] + fs) + (uintptr_t)(i64)(b - kHdr);  // chunk byte t <- X0 + t
+            if (tile_safe) {  // one byte-unaligned load, unconditional (no wait until the store)
+                const u32x4 w = ld16u(lo < hi ? X0 : dummy);
+                r |= w & range_mask(masks, lo, hi);
+            } else if (lo < hi) {  // batch-edge tiles: only the aligned blocks holding payload bytes
                 u32 t[4] = {r.x, r.y, r.z, r.w};
-                or_window_global((uintptr_t)(S.addr[k] + fs) + (uintptr_t)(i64)(b - kHdr), lo, (int)hi, t);
+                or_window_global(X0, lo, hi, t);
                 r = u32x4{t[0], t[1], t[2], t[3]};
             }
         }

@@ -116,6 +116,61 @@ def load_traffic(kernel: str):
         return None
 
 
+def packetize_leg(codec: Codec, data: torch.Tensor, rec_off: torch.Tensor, dev, reps: int) -> dict:
+    """SURVEY.md 8f N2 beside the headline: the send side of aRPC's transport (FragmentPackets +
+    DataPacket framing) over the encoded batch, device-resident, timed with HIP events.
+    Algorithmic bytes: stream + record offsets + rpc ids in; wire bytes + datagram offsets + per-record
+    first datagram, wire offset and status out."""
+    import ctypes
+    from arpc_amd import _native
+    n = rec_off.numel() - 1
+    rpc = torch.arange(n, dtype=torch.int64, device=dev)
+    first = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    wire_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    status = torch.empty(n, dtype=torch.uint8, device=dev)
+    L, ctx = codec._lib, codec._ctx
+    sh = torch.cuda.current_stream(dev).cuda_stream
+    mtu = _native.SYM_MAX_UDP_PAYLOAD
+
+    def plan():
+        _native.check(L.sym_fragment_plan(ctx, data.data_ptr(), rec_off.data_ptr(), n, mtu, first.data_ptr(),
+                                          wire_off.data_ptr(), status.data_ptr(), sh), "sym_fragment_plan")
+    plan()
+    torch.cuda.synchronize()
+    ndg, total = int(first[n].item()), int(wire_off[n].item())
+    wire = torch.empty(total, dtype=torch.uint8, device=dev)
+    dg_off = torch.empty(ndg + 1, dtype=torch.int64, device=dev)
+    ep = _native.Endpoints((ctypes.c_uint8 * 4)(127, 0, 0, 1), 9000, (ctypes.c_uint8 * 4)(127, 0, 0, 1), 9001)
+
+    def write():
+        _native.check(L.sym_fragment_write(ctx, data.data_ptr(), rec_off.data_ptr(), n, mtu, _native.SYM_PACKET_REQUEST,
+                                           rpc.data_ptr(), ctypes.byref(ep), first.data_ptr(), wire_off.data_ptr(),
+                                           status.data_ptr(), wire.data_ptr(), dg_off.data_ptr(), sh),
+                      "sym_fragment_write")
+    write()
+    torch.cuda.synchronize()
+    ev = []
+    for _ in range(reps):
+        e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+        e0.record()
+        plan()
+        e1.record()
+        write()
+        e2.record()
+        ev.append((e0, e1, e2))
+    torch.cuda.synchronize()
+    codec.check()
+    plan_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in ev]))
+    write_ms = float(np.mean([b.elapsed_time(c) for _, b, c in ev]))
+    stream_b = int(rec_off[n].item() - rec_off[0].item())
+    alg = stream_b + 16 * n + total + 8 * (ndg + 1) + 17 * n
+    return {"records": n, "datagrams": ndg, "wire_bytes": total, "plan_ms": round(plan_ms, 4),
+            "write_ms": round(write_ms, 4), "alg_bytes": alg,
+            "gbps_algorithmic": round(alg / ((plan_ms + write_ms) * 1e-3) / 1e9, 1),
+            "note": "FragmentPackets(MaxUDPPayloadSize-31) + 31-byte DataPacket headers (pkg/transport/"
+                    "transport.go:146-201), device-resident, outside the timed region"}
+
+
 def host_inclusive(codec: Codec, kw: dict, dev, steps: int) -> dict:
     """Pinned host -> H2D -> encode -> D2H, then H2D -> decode -> D2H (serial, one stream)."""
     b = datagen.make_batch(**kw)
@@ -172,6 +227,7 @@ def main():
     ap.add_argument("--records", type=int, default=0, help="records per GPU (default: the config's 2^20)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--host-steps", type=int, default=5, help="host-inclusive steps (0 = skip)")
+    ap.add_argument("--packetize-reps", type=int, default=5, help="packetization leg repetitions (0 = skip)")
     args = ap.parse_args()
 
     world, rank, local = dist_setup()
@@ -312,6 +368,8 @@ def main():
     }
     if world == 1 and args.host_steps > 0:
         line["host_inclusive"] = host_inclusive(codec, kw, dev, args.host_steps)
+    if world == 1 and args.packetize_reps > 0:
+        line["packetize"] = packetize_leg(codec, enc[0][0], enc[0][1], dev, args.packetize_reps)
     if world == 1 and args.cpu_seconds > 0:
         line["cpu_baseline"] = cpu_baseline(kw, args.cpu_seconds)
     print(json.dumps(line), flush=True)
