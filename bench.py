@@ -46,13 +46,21 @@ def alg_bytes(n: int, nvar: int, var_total: int, stream_total: int) -> tuple[int
 
 
 def dist_setup():
+    """One process per GPU (torch.distributed.run env).  RCCL ("nccl") carries only the barrier and
+    the max-over-ranks of the elapsed time: the shards exchange no data.  SYMHIP_BENCH_ONE_GPU=1
+    (rehearsal on a 1-GPU box) puts every rank on device 0 and uses gloo for that control traffic."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("SYMHIP_BENCH_ONE_GPU") == "1":
+        local = 0
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        if os.environ.get("SYMHIP_BENCH_ONE_GPU") == "1":
+            dist.init_process_group(backend="gloo")
+        else:
+            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
     return world, rank, local
 
 
@@ -66,7 +74,8 @@ def max_over_ranks(x: float, world: int, dev) -> float:
     if world == 1:
         return x
     import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    on_gpu = dist.get_backend() == "nccl"
+    t = torch.tensor([x], dtype=torch.float64, device=dev if on_gpu else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
