@@ -62,6 +62,9 @@ def main():
     ready = np.maximum(t[1:, 2], t[:-1, 3])
     print("look-back lag after predecessor's inclusive", q(t[1:, 3] - ready))
     print("predecessor inclusive minus my aggregate   ", q(t[:-1, 3] - t[1:, 2]))
+    first = t[:min(1400, ntiles)]
+    print("first 1400 tiles: aggregate ready", q(first[:, 2]), "\n                  prefix known   ", q(first[:, 3]),
+          "\n                  staged         ", q(first[:, 1]))
     order = np.argsort(t[:, 0])
     gaps = []
     for w in set(blk.tolist()):
