@@ -54,6 +54,10 @@ SIGNATURES = {
     "sym_fragment_plan": (_int, [_ctx, _u8p, _u64p, _u64, _u32, _u64p, _u64p, _u8p, _vp]),
     "sym_fragment_write": (_int, [_ctx, _u8p, _u64p, _u64, _u32, ctypes.c_uint8, _u64p, _vp, _u64p, _u64p, _u8p,
                                   _u8p, _u64p, _vp]),
+    "sym_raw_get_fixed": (_int, [_ctx, _u8p, _u64p, _u64, _int, _u32, _u32, _vp, _u8p, _vp]),
+    "sym_raw_get_bytes": (_int, [_ctx, _u8p, _u64p, _u64, _int, _u32, _u8p, _u64, _u64p, _u8p, _vp]),
+    "sym_firewall_filter": (_int, [_ctx, _u8p, _u64p, _u64, _u32, ctypes.c_int32, _vp, _u8p, _u8p, _u64, _u64p,
+                                   _u64p, _u64p, _vp]),
 }
 
 SYM_MAX_UDP_PAYLOAD = 1400
@@ -63,6 +67,15 @@ SYM_PACKET_RESPONSE = 2
 SYM_FRAG_OK = 0
 SYM_FRAG_TOO_SHORT = 1
 SYM_FRAG_BAD_OFFSET = 2
+SYM_SEGMENT_PUBLIC = 0
+SYM_SEGMENT_PRIVATE = 1
+SYM_PUBLIC_TABLE_START = 13
+SYM_PRIVATE_TABLE_START = 1
+SYM_RAW_OK = 0
+SYM_RAW_INVALID_BUFFER = 1
+SYM_RAW_PUBLIC_ONLY = 2
+SYM_VERDICT_PASS = 1
+SYM_VERDICT_DROP = 2
 
 
 class Endpoints(ctypes.Structure):

@@ -187,6 +187,83 @@ def _fragment(codec: "Codec", data: torch.Tensor, rec_off: torch.Tensor, rpc_id:
 Codec.fragment = _fragment
 
 
+_FIXED_DTYPE = {1: torch.uint8, 4: torch.int32, 8: torch.int64}
+
+
+def _raw_get_fixed(codec: "Codec", data: torch.Tensor, rec_off: torch.Tensor, table_off: int, width: int = 4,
+                   segment: int = _native.SYM_SEGMENT_PUBLIC, stream=None):
+    """One fixed-width Raw getter over n buffers (main.go:1260-1294).  Returns (values, status):
+    uint8 / int32 / int64 [n] for width 1 / 4 / 8 (reinterpret for uint32, float, double), and uint8
+    [n] SYM_RAW_* (private fields: the complete-buffer assertion Go panics on)."""
+    _check_col(data, torch.uint8, "data", codec.device)
+    _check_col(rec_off, torch.int64, "rec_off", codec.device)
+    if width not in _FIXED_DTYPE:
+        raise ValueError(f"width {width}: fixed fields are 1, 4 or 8 bytes")
+    n = rec_off.numel() - 1
+    out = torch.empty(max(1, n), dtype=_FIXED_DTYPE[width], device=codec.device)
+    status = torch.empty(max(1, n), dtype=torch.uint8, device=codec.device)
+    _native.check(codec._lib.sym_raw_get_fixed(codec._ctx, _dptr(data) if data.numel() else 1, _dptr(rec_off), n,
+                                              segment, table_off, width, _dptr(out), _dptr(status),
+                                              _stream_handle(codec.device, stream)), "sym_raw_get_fixed")
+    return out[:n], status[:n]
+
+
+def _raw_get_bytes(codec: "Codec", data: torch.Tensor, rec_off: torch.Tensor, table_off: int,
+                   segment: int = _native.SYM_SEGMENT_PUBLIC, cap: int | None = None, stream=None):
+    """One string / bytes Raw getter over n buffers (main.go:1517-1565).  Returns (values uint8,
+    offsets int64 [n+1], status uint8 [n]).  `cap` bounds the value bytes (default: the input's
+    size, which always suffices; no host sync).  The values tensor has `cap` bytes: its first
+    offsets[n] are the values."""
+    _check_col(data, torch.uint8, "data", codec.device)
+    _check_col(rec_off, torch.int64, "rec_off", codec.device)
+    n = rec_off.numel() - 1
+    if cap is None:
+        cap = data.numel()
+    out = torch.empty(max(1, cap), dtype=torch.uint8, device=codec.device)
+    offs = torch.empty(n + 1, dtype=torch.int64, device=codec.device)
+    status = torch.empty(max(1, n), dtype=torch.uint8, device=codec.device)
+    _native.check(codec._lib.sym_raw_get_bytes(codec._ctx, _dptr(data) if data.numel() else 1, _dptr(rec_off), n,
+                                              segment, table_off, _dptr(out), cap, _dptr(offs), _dptr(status),
+                                              _stream_handle(codec.device, stream)), "sym_raw_get_bytes")
+    return out, offs, status[:n]
+
+
+@dataclass
+class Filtered:
+    score: torch.Tensor       # int32 [n]: GetScore of every buffer
+    verdict: torch.Tensor     # uint8 [n]: SYM_VERDICT_PASS / SYM_VERDICT_DROP
+    kept: torch.Tensor        # uint8 [>= kept bytes]: the passing buffers back to back
+    kept_off: torch.Tensor    # int64 [n+1]: the first nkept+1 entries are the kept buffers' offsets
+    kept_index: torch.Tensor  # int64 [n]: the first nkept entries are their input positions
+    nkept: torch.Tensor       # int64 [1] (device)
+
+
+def _firewall(codec: "Codec", data: torch.Tensor, rec_off: torch.Tensor, block_threshold: int,
+              score_table_off: int = _native.SYM_PUBLIC_TABLE_START, stream=None) -> Filtered:
+    """FirewallElement.ProcessRequest (cmd/proxy/element/firewall.go:39-52) over n buffered requests,
+    device-resident and without a host sync."""
+    _check_col(data, torch.uint8, "data", codec.device)
+    _check_col(rec_off, torch.int64, "rec_off", codec.device)
+    n = rec_off.numel() - 1
+    dev = codec.device
+    score = torch.empty(max(1, n), dtype=torch.int32, device=dev)
+    verdict = torch.empty(max(1, n), dtype=torch.uint8, device=dev)
+    kept = torch.empty(max(1, data.numel()), dtype=torch.uint8, device=dev)
+    kept_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    kept_index = torch.empty(max(1, n), dtype=torch.int64, device=dev)
+    nkept = torch.empty(1, dtype=torch.int64, device=dev)
+    _native.check(codec._lib.sym_firewall_filter(codec._ctx, _dptr(data) if data.numel() else 1, _dptr(rec_off), n,
+                                                score_table_off, block_threshold, _dptr(score), _dptr(verdict),
+                                                _dptr(kept), data.numel(), _dptr(kept_off), _dptr(kept_index),
+                                                _dptr(nkept), _stream_handle(dev, stream)), "sym_firewall_filter")
+    return Filtered(score[:n], verdict[:n], kept, kept_off, kept_index[:n], nkept)
+
+
+Codec.raw_get_fixed = _raw_get_fixed
+Codec.raw_get_bytes = _raw_get_bytes
+Codec.firewall = _firewall
+
+
 def to_device(batch, device) -> tuple[list, list]:
     """datagen.Batch (numpy) -> (fixed int32 tensors, [(uint8 tensor, int64 offsets tensor)]) on device."""
     fixed = [torch.from_numpy(c).to(device) for c in batch.fixed]

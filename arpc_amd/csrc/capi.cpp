@@ -31,7 +31,8 @@ struct sym_ctx {
     void* pool = nullptr;
     size_t pool_bytes = 0;
     hipStream_t stream = nullptr;
-    // packetization plan: per-record counts / bytes (scan inputs) and the rocPRIM scan storage
+    // scan workspace of the packetizer and the field getters: per-record scan inputs / outputs
+    // and the rocPRIM scan storage (stream-ordered, so calls on one stream share it)
     void* frag = nullptr;
     size_t frag_bytes = 0;
 };
@@ -95,7 +96,6 @@ int ensure_flags(sym_ctx* ctx, uint64_t n) {
     const size_t need = symhip::decode_pipe_flag_bytes(symhip::kMaxVar, n);
     if (need <= ctx->flag_bytes) return SYM_OK;
     if (ctx->flags) (void)hipFree(ctx->flags);
-    if (ctx->frag) (void)hipFree(ctx->frag);
     ctx->flags = nullptr;
     ctx->flag_bytes = 0;
     hipError_t e = hipMalloc(&ctx->flags, need);
@@ -129,6 +129,17 @@ int ensure_pool(sym_ctx* ctx, size_t need) {
 }
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+int ensure_scratch(sym_ctx* ctx, size_t need, const char* what) {
+    if (need <= ctx->frag_bytes) return SYM_OK;
+    if (ctx->frag) (void)hipFree(ctx->frag);
+    ctx->frag = nullptr;
+    ctx->frag_bytes = 0;
+    hipError_t e = hipMalloc(&ctx->frag, need);
+    if (e != hipSuccess) return fail(SYM_ERR_NOMEM, "%s workspace of %zu bytes: %s", what, need, hipGetErrorString(e));
+    ctx->frag_bytes = need;
+    return SYM_OK;
+}
 
 }  // namespace
 
@@ -198,7 +209,7 @@ int sym_ctx_check(sym_ctx* ctx, void* stream) {
     if (bits & symhip::kErrTimeout) return fail(SYM_ERR_DEVICE, "decode look-back timed out (device error bits 0x%x)", bits);
     if (bits & symhip::kErrTooLarge)
         return fail(SYM_ERR_INVALID, "64 consecutive records span >= 2 GiB; split the batch (device error bits 0x%x)", bits);
-    return fail(SYM_ERR_CAPACITY, "decode output column capacity exceeded (device error bits 0x%x)", bits);
+    return fail(SYM_ERR_CAPACITY, "output capacity exceeded (decode column, Raw getter values or firewall kept bytes; device error bits 0x%x)", bits);
 }
 
 int sym_schema_info(int schema, int* nfixed, int* nvar) {
@@ -518,15 +529,8 @@ int sym_fragment_plan(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_o
     if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
     const size_t cols = align256((n + 1) * sizeof(uint64_t));
     const size_t temp = symhip::frag_scan_temp_bytes(n);
-    const size_t need = 2 * cols + temp;
-    if (need > ctx->frag_bytes) {
-        if (ctx->frag) (void)hipFree(ctx->frag);
-        ctx->frag = nullptr;
-        ctx->frag_bytes = 0;
-        hipError_t e = hipMalloc(&ctx->frag, need);
-        if (e != hipSuccess) return fail(SYM_ERR_NOMEM, "packetization workspace of %zu bytes: %s", need, hipGetErrorString(e));
-        ctx->frag_bytes = need;
-    }
+    const int rc = ensure_scratch(ctx, 2 * cols + temp, "packetization");
+    if (rc != SYM_OK) return rc;
     uint64_t* cnt = (uint64_t*)ctx->frag;
     uint64_t* bytes = (uint64_t*)((char*)ctx->frag + cols);
     void* tmp = (char*)ctx->frag + 2 * cols;
@@ -572,6 +576,60 @@ int sym_fragment_write(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_
     a.err = ctx->err;
     hipError_t e = symhip::launch_frag_write(a, (hipStream_t)stream);
     return e == hipSuccess ? SYM_OK : hip_fail(e, "fragment write launch");
+}
+
+int sym_raw_get_fixed(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_off, uint64_t n, int segment,
+                      uint32_t table_off, uint32_t width, void* d_out, uint8_t* d_status, void* stream) {
+    if (!ctx) return fail(SYM_ERR_INVALID, "sym_raw_get_fixed: ctx is NULL");
+    if (segment != SYM_SEGMENT_PUBLIC && segment != SYM_SEGMENT_PRIVATE)
+        return fail(SYM_ERR_INVALID, "sym_raw_get_fixed: segment %d", segment);
+    if (width != 1 && width != 4 && width != 8)
+        return fail(SYM_ERR_INVALID, "sym_raw_get_fixed: width %u (fixed fields are 1, 4 or 8 bytes)", width);
+    if (n && (!d_in || !d_rec_off || !d_out)) return fail(SYM_ERR_INVALID, "sym_raw_get_fixed: NULL argument");
+    DeviceGuard g(ctx->device);
+    if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
+    hipError_t e = symhip::launch_raw_fixed(d_in, d_rec_off, n, segment, table_off, width, d_out, d_status,
+                                            (hipStream_t)stream);
+    return e == hipSuccess ? SYM_OK : hip_fail(e, "raw fixed getter launch");
+}
+
+int sym_raw_get_bytes(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_off, uint64_t n, int segment,
+                      uint32_t table_off, uint8_t* d_out, uint64_t out_cap, uint64_t* d_out_off, uint8_t* d_status,
+                      void* stream) {
+    if (!ctx) return fail(SYM_ERR_INVALID, "sym_raw_get_bytes: ctx is NULL");
+    if (segment != SYM_SEGMENT_PUBLIC && segment != SYM_SEGMENT_PRIVATE)
+        return fail(SYM_ERR_INVALID, "sym_raw_get_bytes: segment %d", segment);
+    if (!d_out_off || (n && (!d_in || !d_rec_off || (out_cap && !d_out))))
+        return fail(SYM_ERR_INVALID, "sym_raw_get_bytes: NULL argument");
+    DeviceGuard g(ctx->device);
+    if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
+    const int rc = ensure_scratch(ctx, symhip::raw_bytes_ws_bytes(n), "raw getter");
+    if (rc != SYM_OK) return rc;
+    hipError_t e = symhip::launch_raw_bytes(d_in, d_rec_off, n, segment, table_off, d_out, out_cap, d_out_off,
+                                            d_status, ctx->frag, ctx->err, (hipStream_t)stream);
+    return e == hipSuccess ? SYM_OK : hip_fail(e, "raw bytes getter launch");
+}
+
+int sym_firewall_filter(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_off, uint64_t n,
+                        uint32_t score_table_off, int32_t block_threshold, int32_t* d_score, uint8_t* d_verdict,
+                        uint8_t* d_kept, uint64_t kept_cap, uint64_t* d_kept_off, uint64_t* d_kept_index,
+                        uint64_t* d_nkept, void* stream) {
+    if (!ctx) return fail(SYM_ERR_INVALID, "sym_firewall_filter: ctx is NULL");
+    if (!d_kept_off || !d_nkept || (n && (!d_in || !d_rec_off || !d_verdict || (kept_cap && !d_kept))))
+        return fail(SYM_ERR_INVALID, "sym_firewall_filter: NULL argument");
+    DeviceGuard g(ctx->device);
+    if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
+    if (n == 0) {
+        hipError_t e = hipMemsetAsync(d_kept_off, 0, sizeof(uint64_t), (hipStream_t)stream);
+        if (e == hipSuccess) e = hipMemsetAsync(d_nkept, 0, sizeof(uint64_t), (hipStream_t)stream);
+        return e == hipSuccess ? SYM_OK : hip_fail(e, "hipMemsetAsync");
+    }
+    const int rc = ensure_scratch(ctx, symhip::firewall_ws_bytes(n), "firewall");
+    if (rc != SYM_OK) return rc;
+    hipError_t e = symhip::launch_firewall(d_in, d_rec_off, n, score_table_off, block_threshold, d_score, d_verdict,
+                                           d_kept, kept_cap, d_kept_off, d_kept_index, d_nkept, ctx->frag, ctx->err,
+                                           (hipStream_t)stream);
+    return e == hipSuccess ? SYM_OK : hip_fail(e, "firewall launch");
 }
 
 }  // extern "C"

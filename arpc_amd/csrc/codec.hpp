@@ -96,6 +96,19 @@ hipError_t launch_frag_plan(const uint8_t* in, const uint64_t* rec_off, uint64_t
                             size_t temp_bytes, hipStream_t stream);
 hipError_t launch_frag_write(const FragWriteArgs& a, hipStream_t stream);
 
+// ---- batched Raw getters and the firewall element (raw_fields.hip)
+hipError_t launch_raw_fixed(const uint8_t* in, const uint64_t* rec_off, uint64_t n, int priv, uint32_t table_off,
+                            uint32_t width, void* out, uint8_t* status, hipStream_t stream);
+size_t raw_bytes_ws_bytes(uint64_t n);
+hipError_t launch_raw_bytes(const uint8_t* in, const uint64_t* rec_off, uint64_t n, int priv, uint32_t table_off,
+                            uint8_t* out, uint64_t cap, uint64_t* out_off, uint8_t* status, void* ws, unsigned* err,
+                            hipStream_t stream);
+size_t firewall_ws_bytes(uint64_t n);
+hipError_t launch_firewall(const uint8_t* in, const uint64_t* rec_off, uint64_t n, uint32_t score_table_off,
+                           int32_t threshold, int32_t* score, uint8_t* verdict, uint8_t* kept, uint64_t cap,
+                           uint64_t* kept_off, uint64_t* kept_index, uint64_t* nkept, void* ws, unsigned* err,
+                           hipStream_t stream);
+
 hipError_t launch_encode(const EncodeParams& p, hipStream_t stream);
 hipError_t launch_decode(const DecodeParams& p, hipStream_t stream);
 

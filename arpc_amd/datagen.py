@@ -111,3 +111,82 @@ CORPORA = {
     "set_response_256": dict(schema="kv_set_response", n=3000, lens=(256,), seed=6),
     "echo_small": dict(schema="echo_request", n=2048, lens=(("uniform", 0, 32), ("uniform", 0, 200)), seed=13),
 }
+
+
+# ------------------------------------------------------------ element-schema records
+# kv-store-symphony-element's {Get,Set}Request: public Score (int32, table 13) and Username (string,
+# table 17), private Key [and Value].  Built here, vectorized, as synthetic INPUT for the field
+# getters and the firewall (bench.py and tests); layout of kv.syn.go:1041-1124 (SetRequest) and
+# :128-202 (GetRequest).  tests/test_raw_fields.py checks it against the C oracle's restatement.
+ELEMENT_FW = dict(n=1 << 20, lens=(16, 64, 256), seed=0x5EED0005)  # Username 16, Key 64, Value 256
+
+
+@dataclass
+class ElementBatch:
+    score: np.ndarray   # int32 [n]
+    strings: list       # (bytes, offs[n+1]) for Username, Key[, Value]
+    data: np.ndarray    # uint8 stream
+    rec_off: np.ndarray  # uint64 [n+1]
+
+
+def _put_u32(out: np.ndarray, pos: np.ndarray, v: np.ndarray) -> None:
+    v = v.astype(np.uint64)
+    for b in range(4):
+        out[pos + b] = ((v >> np.uint64(8 * b)) & np.uint64(0xFF)).astype(np.uint8)
+
+
+def _scatter(out: np.ndarray, dst: np.ndarray, col: tuple) -> None:
+    b, o = col
+    lens = np.diff(o).astype(np.int64)
+    n = len(lens)
+    uniform = n > 0 and b.size > 0 and bool((lens == lens[0]).all()) and (n == 1 or bool((np.diff(dst) == dst[1] - dst[0]).all()))
+    if uniform:  # equal lengths at equal strides: one strided 2-D copy
+        L, step = int(lens[0]), int(dst[1] - dst[0]) if n > 1 else 0
+        if n == 1 or step >= L:
+            view = np.lib.stride_tricks.as_strided(out[int(dst[0]):], shape=(n, L), strides=(step, 1))
+            view[...] = b[int(o[0]):int(o[-1])].reshape(n, L)
+            return
+    if b.size:
+        out[np.arange(int(o[-1] - o[0]), dtype=np.int64) + np.repeat(dst.astype(np.int64) - (o[:-1] - o[0]).astype(np.int64), lens)] = b[int(o[0]):int(o[-1])]
+
+
+def element_records(score: np.ndarray, strings: list) -> tuple[np.ndarray, np.ndarray]:
+    """Marshal element-schema records: strings = [Username, Key] or [Username, Key, Value] columns."""
+    n, npriv = len(score), len(strings) - 1
+    ln = [np.diff(o).astype(np.uint64) for _, o in strings]
+    pub = np.uint64(25) + ln[0]                            # publicSegmentSize
+    size = pub + np.uint64(1 + 4 * npriv) + sum(np.uint64(4) + x for x in ln[1:])
+    rec_off = np.zeros(n + 1, np.uint64)
+    np.cumsum(size, out=rec_off[1:])
+    out = np.zeros(int(rec_off[-1]), np.uint8)
+    s = rec_off[:-1].astype(np.int64)
+    out[s] = 1
+    _put_u32(out, s + 1, pub)
+    _put_u32(out, s + 13, score.view(np.uint32))
+    _put_u32(out, s + 17, np.full(n, 21, np.uint64))
+    _put_u32(out, s + 21, ln[0])
+    _scatter(out, s + 25, strings[0])
+    ps = s + pub.astype(np.int64)
+    out[ps] = 1
+    pay = np.int64(1 + 4 * npriv)                          # payload start, relative to the private segment
+    rel = np.full(n, pay, np.int64)
+    for k in range(npriv):
+        _put_u32(out, ps + 1 + 4 * k, rel.astype(np.uint64))
+        _put_u32(out, ps + rel, ln[k + 1])
+        _scatter(out, ps + rel + 4, strings[k + 1])
+        rel = rel + 4 + ln[k + 1].astype(np.int64)
+    return out, rec_off
+
+
+def make_element_batch(n: int, lens: tuple, seed: int, score_range=(0, 100)) -> ElementBatch:
+    """Scores uniform in [lo, hi) (firewall thresholds inside that range drop a known fraction)."""
+    lo, hi = score_range
+    score = (lo + (splitmix64(seed + 0x1000, n) % np.uint64(hi - lo)).astype(np.int64)).astype(np.int32)
+    strings = []
+    for f, spec in enumerate(lens):
+        ln = lengths(spec, n, seed + 0x10000 * (f + 1))
+        offs = np.zeros(n + 1, dtype=np.uint64)
+        np.cumsum(ln, out=offs[1:])
+        strings.append((random_bytes(seed + 0x100000000 * (f + 1), int(offs[-1])), offs))
+    data, rec_off = element_records(score, strings)
+    return ElementBatch(score, strings, data, rec_off)

@@ -190,6 +190,58 @@ int sym_fragment_write(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_
                        const sym_endpoints* endpoints, const uint64_t* d_first, const uint64_t* d_wire_off,
                        const uint8_t* d_status, uint8_t* d_wire, uint64_t* d_dg_off, void* stream);
 
+/* ---- Batched Raw getters and the proxy firewall element -----------------
+ *
+ * Replaces, for n buffers at once, the generated zero-copy getters
+ *   func (m XxxRaw) GetField() T       cmd/symphony-gen-arpc/protoc-gen-symphony/main.go:984-1036
+ *     fixed-width                      main.go:1260-1294
+ *     string / bytes                   main.go:1517-1565
+ *   e.g. GetRequestRaw.GetScore / GetUsername
+ *                                      benchmark/kv-store-symphony-element/symphony/kv.syn.go:285-310
+ * and the proxy's firewall element
+ *   func (f *FirewallElement) ProcessRequest(ctx, packet) (*BufferedPacket, PacketVerdict, ctx, error)
+ *                                      cmd/proxy/element/firewall.go:39-52
+ * Buffers are a batch as elsewhere: d_in + d_rec_off[n+1] (buffer i = d_in[rec_off[i], rec_off[i+1]);
+ * offsets non-decreasing); a buffer may be a complete record or only its public segment.
+ *
+ * `segment` / `table_off` name the field as the generator does: SYM_SEGMENT_PUBLIC with the absolute
+ * table offset (public fields start at 13), or SYM_SEGMENT_PRIVATE with the offset relative to the
+ * private segment (private fields start at 1); each field advances the offset by its width (fixed) or
+ * 4 (string / bytes) -- main.go:986-989, 1243-1257.
+ *
+ *   sym_raw_get_fixed   width 1 (bool), 4 (int32/uint32/float/enum) or 8 (int64/uint64/double);
+ *                       d_out[n] of `width` bytes each, little-endian; a short buffer reads 0.
+ *   sym_raw_get_bytes   the values back to back in d_out (at most out_cap bytes, else
+ *                       SYM_ERR_CAPACITY from sym_ctx_check and nothing written) with
+ *                       d_out_off[n+1]; an unset, truncated or out-of-range value reads empty.
+ *   d_status[n] (nullable): SYM_RAW_OK, or for private fields the buffer assertion Go panics on
+ *                       (main.go:1003-1013) -- the value then reads as zero / empty.
+ *   sym_firewall_filter score = GetScore (public int32 at score_table_off, 13 for the element
+ *                       schemas); verdict SYM_VERDICT_DROP when score >= block_threshold, else
+ *                       SYM_VERDICT_PASS; the passing buffers, unchanged and in order, back to back
+ *                       in d_kept (kept_cap >= rec_off[n] - rec_off[0] always suffices) with
+ *                       d_kept_off[nkept+1] (room for n+1), d_kept_index[nkept] (nullable) and
+ *                       *d_nkept, all on the device. */
+#define SYM_SEGMENT_PUBLIC 0
+#define SYM_SEGMENT_PRIVATE 1
+#define SYM_PUBLIC_TABLE_START 13
+#define SYM_PRIVATE_TABLE_START 1
+#define SYM_RAW_OK 0
+#define SYM_RAW_INVALID_BUFFER 1 /* "private getter called on invalid buffer" (len < 5) */
+#define SYM_RAW_PUBLIC_ONLY 2    /* "private getter called on public-only buffer" */
+#define SYM_VERDICT_PASS 1       /* util.PacketVerdictPass, cmd/proxy/util/packet.go:57-58 */
+#define SYM_VERDICT_DROP 2       /* util.PacketVerdictDrop, cmd/proxy/util/packet.go:60-61 */
+
+int sym_raw_get_fixed(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_off, uint64_t n, int segment,
+                      uint32_t table_off, uint32_t width, void* d_out, uint8_t* d_status, void* stream);
+int sym_raw_get_bytes(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_off, uint64_t n, int segment,
+                      uint32_t table_off, uint8_t* d_out, uint64_t out_cap, uint64_t* d_out_off, uint8_t* d_status,
+                      void* stream);
+int sym_firewall_filter(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_off, uint64_t n,
+                        uint32_t score_table_off, int32_t block_threshold, int32_t* d_score, uint8_t* d_verdict,
+                        uint8_t* d_kept, uint64_t kept_cap, uint64_t* d_kept_off, uint64_t* d_kept_index,
+                        uint64_t* d_nkept, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -167,3 +167,84 @@ def fragment_batch(data: np.ndarray, rec_off: np.ndarray, rpc_id: np.ndarray, pa
     L.sym_oracle_fragment_write(n, dp, _ptr(rec_off), max_udp_payload, packet_type, _ptr(rpc_id) if n else 0,
                                 _ptr(dip), dst[1], _ptr(sip), src[1], _ptr(out), _ptr(dg_off), _ptr(scratch))
     return out[:total], dg_off, first, out_off, status[:n]
+
+
+# ---------------------------------------------------------------- Raw getters / firewall (raw_oracle.c)
+RAW_OK = 0
+RAW_INVALID_BUFFER = 1  # private getter panic: "called on invalid buffer" (main.go:1003-1006)
+RAW_PUBLIC_ONLY = 2     # private getter panic: "called on public-only buffer" (main.go:1007-1013)
+VERDICT_PASS = 1        # cmd/proxy/util/packet.go:57-58
+VERDICT_DROP = 2
+
+
+def _raw_lib():
+    L = lib()
+    if not getattr(L, "_raw_ready", False):
+        u64, u32, i32, vp = ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p
+        L.sym_oracle_raw_fixed.restype = None
+        L.sym_oracle_raw_fixed.argtypes = [u64, vp, vp, i32, u32, u32, vp, vp]
+        L.sym_oracle_raw_bytes.restype = None
+        L.sym_oracle_raw_bytes.argtypes = [u64, vp, vp, i32, u32, vp, vp, vp]
+        L.sym_oracle_firewall.restype = u64
+        L.sym_oracle_firewall.argtypes = [u64, vp, vp, u32, ctypes.c_int32, vp, vp, vp, vp, vp]
+        L.sym_oracle_marshal_element_batch.restype = u64
+        L.sym_oracle_marshal_element_batch.argtypes = [u64, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+        L.sym_oracle_element_size.restype = u64
+        L.sym_oracle_element_size.argtypes = [i32, u64, u64, u64]
+        L._raw_ready = True
+    return L
+
+
+def _batch_args(data, rec_off):
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    rec_off = np.ascontiguousarray(rec_off, dtype=np.uint64)
+    return data, rec_off, len(rec_off) - 1, (_ptr(data) if data.size else 0)
+
+
+def raw_fixed(data, rec_off, table_off: int, width: int = 4, private: bool = False):
+    """-> (values as uint8/uint32/uint64 [n], status u8 [n])."""
+    data, rec_off, n, dp = _batch_args(data, rec_off)
+    out = np.zeros(max(1, n), {1: np.uint8, 4: np.uint32, 8: np.uint64}[width])
+    st = np.zeros(max(1, n), np.uint8)
+    _raw_lib().sym_oracle_raw_fixed(n, dp, _ptr(rec_off), int(private), table_off, width, _ptr(out), _ptr(st))
+    return out[:n], st[:n]
+
+
+def raw_bytes(data, rec_off, table_off: int, private: bool = False):
+    """-> (values u8, offsets u64 [n+1], status u8 [n])."""
+    data, rec_off, n, dp = _batch_args(data, rec_off)
+    out = np.zeros(max(1, data.size), np.uint8)
+    offs = np.zeros(n + 1, np.uint64)
+    st = np.zeros(max(1, n), np.uint8)
+    _raw_lib().sym_oracle_raw_bytes(n, dp, _ptr(rec_off), int(private), table_off, _ptr(out), _ptr(offs), _ptr(st))
+    return out[:int(offs[n])], offs, st[:n]
+
+
+def firewall(data, rec_off, block_threshold: int, score_table_off: int = 13):
+    """-> (score i32 [n], verdict u8 [n], kept u8, kept_off u64 [nkept+1], kept_index u64 [nkept])."""
+    data, rec_off, n, dp = _batch_args(data, rec_off)
+    score = np.zeros(max(1, n), np.int32)
+    verdict = np.zeros(max(1, n), np.uint8)
+    kept = np.zeros(max(1, data.size), np.uint8)
+    kept_off = np.zeros(n + 1, np.uint64)
+    kept_index = np.zeros(max(1, n), np.uint64)
+    k = _raw_lib().sym_oracle_firewall(n, dp, _ptr(rec_off), score_table_off, block_threshold, _ptr(score),
+                                       _ptr(verdict), _ptr(kept), _ptr(kept_off), _ptr(kept_index))
+    return score[:n], verdict[:n], kept[:int(kept_off[k])], kept_off[:k + 1], kept_index[:k]
+
+
+def marshal_element_batch(score, strings):
+    """Element-schema {Get,Set}Request records; strings = [(bytes, offs)] for Username, Key[, Value]."""
+    L = _raw_lib()
+    score = np.ascontiguousarray(score, dtype=np.int32)
+    n, npriv = len(score), len(strings) - 1
+    cols = [(np.ascontiguousarray(b, np.uint8), np.ascontiguousarray(o, np.uint64)) for b, o in strings]
+    total = int(L.sym_oracle_element_size(npriv, 0, 0, 0)) * n + sum(int(o[-1] - o[0]) for _, o in cols)
+    out = np.zeros(max(1, total), np.uint8)
+    out_off = np.zeros(n + 1, np.uint64)
+    val = cols[2] if npriv == 2 else (np.zeros(1, np.uint8), np.zeros(n + 1, np.uint64))
+    got = L.sym_oracle_marshal_element_batch(n, npriv, _ptr(score), _ptr(cols[0][0]) or 0, _ptr(cols[0][1]),
+                                             _ptr(cols[1][0]), _ptr(cols[1][1]), _ptr(val[0]), _ptr(val[1]),
+                                             _ptr(out), _ptr(out_off))
+    assert got == total, (got, total)
+    return out[:total], out_off
