@@ -7,19 +7,18 @@
 //  * fixed-width fields: one thread per record, the field's bytes read straight from the record
 //    (at most two dword loads), one coalesced store of the column;
 //  * string / bytes fields: a thread per record resolves (source offset, length) with the getter's
-//    bounds checks, a device-wide exclusive scan (rocPRIM) places the values, and a gather kernel
-//    copies them out;
-//  * the firewall element: score + verdict per record, one scan over (kept bytes, kept count)
-//    pairs, and the same gather kernel compacts the passing records into a forwardable batch.
+//    bounds checks and its tile's byte total; one small kernel scans the tile totals; the gather
+//    kernel rescans its tile's lengths in registers (DPP / shuffles), writes the value offsets and
+//    copies the values;
+//  * the firewall element: score + verdict per record and per-tile (kept bytes, kept records)
+//    totals, the same tile scan, and the gather kernel compacts the passing records into a
+//    forwardable batch (offsets, input positions, bytes).
 //
 // The gather kernel is output-stationary like encode_kernel and the packetizer: a wave owns 64
 // consecutive segments whose outputs are contiguous, lane = aligned 16-byte output chunk, each
 // chunk assembled from byte-unaligned 16-byte loads of the (one or more) segments it covers and
-// written with one global_store_dwordx4.
-#include <cstring>  // rocprim/iterator/texture_cache_iterator.hpp uses memset
-
-#include <rocprim/device/device_scan.hpp>
-
+// written with one global_store_dwordx4.  Per-record scan inputs never round-trip through HBM
+// (only 16 bytes per 256-record tile do), which is what a device-wide library scan would cost.
 #include "../../include/symphony_hip.h"
 #include "codec.hpp"
 #include "device_util.hpp"
@@ -31,13 +30,8 @@ namespace raw {
 constexpr int kSegs = 64;  // segments per wave tile
 constexpr int kWaves = 4;
 
-struct Pair {  // firewall scan element: kept bytes, kept records
+struct Pair {  // tile total / prefix: bytes, records (kept records for the firewall)
     u64 bytes, count;
-};
-struct PairPlus {
-    __host__ __device__ Pair operator()(const Pair& a, const Pair& b) const {
-        return Pair{a.bytes + b.bytes, a.count + b.count};
-    }
 };
 
 // The private getters' complete-buffer assertion (main.go:1003-1013); sets off2p when it holds.
@@ -76,174 +70,282 @@ __global__ __launch_bounds__(256) void fixed_kernel(const uint8_t* in, const u64
     if (status) status[i] = st;
 }
 
+// Tile total of a per-record (bytes, count) over the 256 threads of a workgroup -> agg[tile].
+__device__ inline void tile_total(u64 b, u64 c, Pair* agg, u64* red_b, u64* red_c) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    b = wave_sum_u64(b);
+    c = wave_sum_u64(c);
+    if (lane == 0) {
+        red_b[wave] = b;
+        red_c[wave] = c;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0)
+        agg[blockIdx.x] = Pair{red_b[0] + red_b[1] + red_b[2] + red_b[3], red_c[0] + red_c[1] + red_c[2] + red_c[3]};
+}
+
 // ---- string / bytes getters: resolve each value's source and length (main.go:1527-1555)
 __global__ __launch_bounds__(256) void var_locate_kernel(const uint8_t* in, const u64* rec_off, u64 n, int priv,
-                                                         u32 toff, u64* seg_src, u64* seg_len, uint8_t* status) {
+                                                         u32 toff, u64* seg_src, u64* seg_len, uint8_t* status,
+                                                         Pair* agg) {
+    __shared__ u64 red_b[4], red_c[4];
     const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
-    if (i > n) return;
-    if (i == n) {  // n+1 scan inputs: the last exclusive prefix is the total
-        seg_len[n] = 0;
-        return;
-    }
-    const u64 s = rec_off[i], L = rec_off[i + 1] - s;
-    const uintptr_t m = (uintptr_t)(in + s);
-    uint8_t st = SYM_RAW_OK;
-    u64 base = toff, o = 0;
-    if (priv) {
-        st = private_check(m, L, o);
-        base = o + toff;
-    }
-    u64 src = s, len = 0;
-    if (st == SYM_RAW_OK && L >= base + 4) {
-        u64 po = ld_u32(m + base);
-        if (po != 0) {             // 0 = unset (:1537-1539)
-            if (priv) po += o;     // relative -> absolute (:1542-1544)
-            if (L >= po + 4) {
-                const u64 d = ld_u32(m + po);
-                if (L >= po + 4 + d) {
-                    src = s + po + 4;
-                    len = d;
+    u64 len = 0;
+    if (i < n) {
+        const u64 s = rec_off[i], L = rec_off[i + 1] - s;
+        const uintptr_t m = (uintptr_t)(in + s);
+        uint8_t st = SYM_RAW_OK;
+        u64 base = toff, o = 0;
+        if (priv) {
+            st = private_check(m, L, o);
+            base = o + toff;
+        }
+        u64 src = s;
+        if (st == SYM_RAW_OK && L >= base + 4) {
+            u64 po = ld_u32(m + base);
+            if (po != 0) {          // 0 = unset (:1537-1539)
+                if (priv) po += o;  // relative -> absolute (:1542-1544)
+                if (L >= po + 4) {
+                    const u64 d = ld_u32(m + po);
+                    if (L >= po + 4 + d) {
+                        src = s + po + 4;
+                        len = d;
+                    }
                 }
             }
         }
+        seg_src[i] = src;
+        seg_len[i] = len;
+        if (status) status[i] = st;
     }
-    seg_src[i] = src;
-    seg_len[i] = len;
-    if (status) status[i] = st;
+    tile_total(len, 0, agg, red_b, red_c);
 }
 
 // ---- firewall element: GetScore, shouldBlock, verdict (firewall.go:34-52)
 __global__ __launch_bounds__(256) void firewall_mark_kernel(const uint8_t* in, const u64* rec_off, u64 n, u32 toff,
                                                             int32_t threshold, int32_t* score, uint8_t* verdict,
-                                                            Pair* kept) {
+                                                            Pair* agg) {
+    __shared__ u64 red_b[4], red_c[4];
     const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
-    if (i > n) return;
-    if (i == n) {
-        kept[n] = Pair{0, 0};
-        return;
+    u64 kb = 0, kc = 0;
+    if (i < n) {
+        const u64 s = rec_off[i], L = rec_off[i + 1] - s;
+        const int32_t sc = L >= (u64)toff + 4 ? (int32_t)ld_u32((uintptr_t)(in + s) + toff) : 0;  // kv.syn.go:285-291
+        const bool drop = sc >= threshold;
+        if (score) score[i] = sc;
+        verdict[i] = drop ? SYM_VERDICT_DROP : SYM_VERDICT_PASS;
+        kb = drop ? 0 : L;
+        kc = drop ? 0 : 1;
     }
-    const u64 s = rec_off[i], L = rec_off[i + 1] - s;
-    const int32_t sc = L >= (u64)toff + 4 ? (int32_t)ld_u32((uintptr_t)(in + s) + toff) : 0;  // kv.syn.go:285-291
-    const bool drop = sc >= threshold;
-    if (score) score[i] = sc;
-    verdict[i] = drop ? SYM_VERDICT_DROP : SYM_VERDICT_PASS;
-    kept[i] = drop ? Pair{0, 0} : Pair{L, 1};
+    tile_total(kb, kc, agg, red_b, red_c);
 }
 
-// ---- gather: out[dst[i] .. dst[i+1]) = in[src[i] .. src[i] + dst[i+1] - dst[i])
+// ---- exclusive scan of the tile totals (one workgroup; pre[ntiles] = grand total).  Each thread
+// takes 4 consecutive tiles, so up to 4096 tiles (2^20 records) take one block-wide scan.
+__global__ __launch_bounds__(1024) void tile_scan_kernel(const Pair* agg, Pair* pre, u64 ntiles) {
+    constexpr int kPer = 4;
+    __shared__ u64 wb[16], wc[16];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    u64 carry_b = 0, carry_c = 0;
+    for (u64 base = 0; base < ntiles; base += 1024 * kPer) {  // uniform loop
+        const u64 t0 = base + (u64)threadIdx.x * kPer;
+        Pair v[kPer];
+        u64 sb = 0, sc = 0;
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            v[k] = t0 + k < ntiles ? agg[t0 + k] : Pair{0, 0};
+            sb += v[k].bytes;
+            sc += v[k].count;
+        }
+        const u64 ib = wave_incl_scan_u64(sb, lane), ic = wave_incl_scan_u64(sc, lane);
+        if (lane == 63) {
+            wb[wave] = ib;
+            wc[wave] = ic;
+        }
+        __syncthreads();
+        u64 pb = carry_b + ib - sb, pc = carry_c + ic - sc, tb = 0, tc = 0;
+        for (int q = 0; q < 16; ++q) {
+            if (q < wave) {
+                pb += wb[q];
+                pc += wc[q];
+            }
+            tb += wb[q];
+            tc += wc[q];
+        }
+        __syncthreads();  // wb / wc are rewritten by the next round
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            if (t0 + k < ntiles) pre[t0 + k] = Pair{pb, pc};
+            pb += v[k].bytes;
+            pc += v[k].count;
+        }
+        carry_b += tb;
+        carry_c += tc;
+    }
+    if (threadIdx.x == 0) pre[ntiles] = Pair{carry_b, carry_c};
+}
+
+// ---- gather: each workgroup owns a 256-record tile; out gets the segments back to back
 struct GatherArgs {
     const uint8_t* in;
-    const u64* rec_off;  // [0] and [n]: the readable input range (for the unconditional loads)
-    const u64* src;      // per segment: source byte offset in `in`
-    const u64* dst;      // n+1 output offsets, element stride `ds` u64s (1: offsets, 2: Pair.bytes)
-    int ds;
+    const u64* rec_off;
     u64 n;
+    const Pair* pre;    // tile prefixes (ntiles + 1)
+    // VAR: value sources and lengths; FW: records, kept when verdict == PASS
+    const u64* seg_src;
+    const u64* seg_len;
+    const uint8_t* verdict;
     uint8_t* out;
     u64 cap;
-    u64* kept_off;    // FW: compacted record offsets (nkept+1)
+    u64* out_off;     // VAR: value offsets (n+1); FW: kept record offsets (nkept+1)
     u64* kept_index;  // FW: input position of each kept record (nullable)
     u64* nkept;       // FW
     unsigned* err;
 };
 
 struct WaveLds {
-    u64 addr[kSegs];  // segment's source address
-    int o[kSegs + 1];  // segment's output start relative to the tile; [cnt] = span
+    u64 addr[kSegs];   // segment's source address
+    int o[kSegs + 1];  // segment's output start relative to the wave's; [cnt] = span
 };
+
+__device__ __forceinline__ u64 readlane_u64(u64 v, int l) {
+    return (u64)__builtin_amdgcn_readlane((u32)v, l) | ((u64)__builtin_amdgcn_readlane((u32)(v >> 32), l) << 32);
+}
 
 template <bool FW>
 __global__ __launch_bounds__(kWaves * 64) void gather_kernel(GatherArgs a) {
     __shared__ WaveLds lds_all[kWaves];
     __shared__ MaskTable masks;
-    mask_table_init(masks, threadIdx.x);
-    __syncthreads();  // the only workgroup barrier
+    __shared__ u64 wsum_b[kWaves], wsum_c[kWaves];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    WaveLds& S = lds_all[wave];
-    const u64 r0 = ((u64)blockIdx.x * kWaves + wave) * kSegs;
-    if (r0 >= a.n) return;  // wave-uniform
-    const int cnt = (int)min((u64)kSegs, a.n - r0);
-    const int ds = a.ds;
-    if (a.dst[a.n * ds] > a.cap) {  // output does not fit: nothing is written
-        if (lane == 0 && r0 == 0) atomicOr(a.err, kErrCapacity);
+    const u64 ntiles = (a.n + 255) / 256;
+    const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
+    mask_table_init(masks, threadIdx.x);
+
+    // ---- phase 1 (thread = record): length, keep flag, in-tile exclusive scan
+    u64 src = 0, len = 0, keep = 0;
+    if (i < a.n) {
+        if constexpr (FW) {
+            src = a.rec_off[i];
+            keep = a.verdict[i] == SYM_VERDICT_PASS;
+            len = keep ? a.rec_off[i + 1] - src : 0;
+        } else {
+            src = a.seg_src[i];
+            len = a.seg_len[i];
+        }
+    }
+    const u64 ib = wave_incl_scan_u64(len, lane);
+    const u32 ic = FW ? wave_incl_scan_u32_dpp((u32)keep) : 0u;
+    if (lane == 63) {
+        wsum_b[wave] = ib;
+        wsum_c[wave] = ic;
+    }
+    __syncthreads();  // the only workgroup barrier
+    const Pair total = a.pre[ntiles];
+    if (total.bytes > a.cap) {  // output does not fit: nothing is written (uniform)
+        if (i == 0) atomicOr(a.err, kErrCapacity);
         return;
     }
-    const u64 D0 = a.dst[r0 * ds], D1 = a.dst[(r0 + cnt) * ds];
-    if (D1 - D0 >= ((u64)1 << 31)) {  // tile positions are 32-bit
+    const Pair tp = a.pre[blockIdx.x];
+    u64 wb = tp.bytes, wc = tp.count;
+    for (int q = 0; q < wave; ++q) {
+        wb += wsum_b[q];
+        wc += wsum_c[q];
+    }
+    const u64 d = wb + ib - len;  // this segment's output start
+    if constexpr (FW) {
+        const u64 rank = wc + ic - keep;
+        if (keep) {
+            a.out_off[rank] = d;
+            if (a.kept_index) a.kept_index[rank] = i;
+        }
+        if (i == a.n - 1) {
+            a.out_off[rank + keep] = d + len;
+            *a.nkept = rank + keep;
+        }
+    } else {
+        if (i < a.n) a.out_off[i] = d;
+        if (i == a.n - 1) a.out_off[a.n] = d + len;
+    }
+
+    // ---- phase 2 (wave = 64 segments, lane = aligned 16-byte output chunk)
+    const u64 r0 = (u64)blockIdx.x * 256 + (u64)wave * kSegs;
+    if (r0 >= a.n) return;  // wave-uniform
+    const int cnt = (int)min((u64)kSegs, a.n - r0);
+    WaveLds& S = lds_all[wave];
+    const u64 D0 = readlane_u64(d, 0), D1 = readlane_u64(d + len, cnt - 1);
+    if (D1 - D0 >= ((u64)1 << 31)) {  // positions are 32-bit
         if (lane == 0) atomicOr(a.err, kErrTooLarge);
         return;
     }
     const u64 in_lo = a.rec_off[0], in_hi = a.rec_off[a.n];
-
-    // ---- phase 1 (lane = segment)
-    bool interior = true;
-    if (lane < cnt) {
-        const u64 i = r0 + lane;
-        const u64 d = a.dst[i * ds], len = a.dst[(i + 1) * ds] - d;
-        const u64 src = a.src[i];
-        S.addr[lane] = (u64)(uintptr_t)(a.in + src);
-        S.o[lane] = (int)(d - D0);
-        if (lane == cnt - 1) S.o[cnt] = (int)(D1 - D0);
-        // a 16-byte window reads up to 15 bytes either side of its segment
-        interior = len == 0 || (src >= in_lo + 16 && src + len + 16 <= in_hi);
-        if constexpr (FW) {
-            const u64 c0 = a.dst[i * 2 + 1], c1 = a.dst[(i + 1) * 2 + 1];
-            if (c1 > c0) {
-                a.kept_off[c0] = d;
-                if (a.kept_index) a.kept_index[c0] = i;
-            }
-            if (i == a.n - 1) {
-                a.kept_off[c1] = d + len;
-                *a.nkept = c1;
-            }
-        }
-    }
-    const bool safe = __all(interior);
-    wave_sync();
-
-    // ---- phase 2 (lane = aligned 16-byte output chunk)
+    // Only non-empty segments go to LDS (dropped records, unset values): a chunk then usually
+    // covers one or two of them, which the unrolled path below loads without a loop.
+    const bool live = lane < cnt && len > 0;
+    const u64 lm = __ballot(live);
+    const int slot = __builtin_amdgcn_mbcnt_hi((u32)(lm >> 32), __builtin_amdgcn_mbcnt_lo((u32)lm, 0u));
+    const int nl = __popcll(lm);
     const int span = (int)(D1 - D0);
+    if (live) {
+        S.addr[slot] = (u64)(uintptr_t)(a.in + src);
+        S.o[slot] = (int)(d - D0);
+    }
+    if (lane == 0) S.o[nl] = span;
+    // a 16-byte window reads up to 15 bytes either side of its segment
+    const bool safe = __all(!live || (src >= in_lo + 16 && src + len + 16 <= in_hi));
+    wave_sync();
+    if (nl == 0) return;
     const i64 mis = (i64)((uintptr_t)a.out & 15);
     const int firstc = (int)((((i64)D0 + mis) & ~(i64)15) - mis - (i64)D0);  // in (-16, 0]
     uint8_t* const out_t = a.out + D0;
-    for (int B = firstc; B < span; B += 16 * 64) {  // wave-uniform loop
+    if (safe) {
+        // kU chunks per lane per step: every load of the step is issued before its stores
+        constexpr int kU = 4;
+        for (int B = firstc; B < span; B += 16 * 64 * kU) {  // wave-uniform loop
+            u32x4 r[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const int P = B + 16 * 64 * u + 16 * lane;
+                r[u] = u32x4{0, 0, 0, 0};
+                if (P >= span) continue;
+                const int k0 = lds_search_64(S.o, nl, max(P, 0));
+                const int o0 = S.o[k0], o1 = S.o[k0 + 1];
+                const bool two = k0 + 1 < nl && o1 < P + 16;  // the next segment starts in this chunk
+                const int o2 = two ? S.o[k0 + 2] : o1;
+                const uintptr_t X0 = (uintptr_t)(S.addr[k0] + (u64)(i64)(P - o0));
+                const uintptr_t X1 = two ? (uintptr_t)(S.addr[k0 + 1] + (u64)(i64)(P - o1)) : X0;
+                r[u] = (ld16u(X0) & range_mask(masks, o0 - P, o1 - P)) |
+                       (ld16u(X1) & range_mask(masks, two ? o1 - P : 16, o2 - P));
+                for (int k = k0 + 2; two && k < nl && S.o[k] < P + 16; ++k)  // segments < 16 bytes
+                    r[u] |= ld16u((uintptr_t)(S.addr[k] + (u64)(i64)(P - S.o[k]))) &
+                            range_mask(masks, S.o[k] - P, S.o[k + 1] - P);
+            }
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const int P = B + 16 * 64 * u + 16 * lane;
+                if (P >= span) continue;
+                const u32 rr[4] = {r[u].x, r[u].y, r[u].z, r[u].w};
+                store_chunk(out_t, P, 0, span, rr);
+            }
+        }
+        return;
+    }
+    for (int B = firstc; B < span; B += 16 * 64) {  // batch-edge waves: aligned blocks only
         const int P = B + 16 * lane;
         if (P >= span) continue;
-        u32x4 r = {0, 0, 0, 0};
-        for (int k = lds_search_64(S.o, cnt, max(P, 0)); k < cnt; ++k) {
+        u32 t[4] = {0, 0, 0, 0};
+        for (int k = lds_search_64(S.o, nl, max(P, 0)); k < nl; ++k) {
             const int lo = S.o[k] - P;
             if (lo >= 16) break;
             const int hi = min(S.o[k + 1] - P, 16);
-            if (hi <= max(lo, 0)) continue;  // empty segment
-            const uintptr_t X0 = (uintptr_t)(S.addr[k] + (u64)(i64)(P - S.o[k]));  // chunk byte t <- X0 + t
-            if (safe) {
-                r |= ld16u(X0) & range_mask(masks, lo, hi);
-            } else {  // batch-edge tiles: only the aligned blocks holding wanted bytes
-                u32 t[4] = {r.x, r.y, r.z, r.w};
-                or_window_global(X0, max(lo, 0), hi, t);
-                r = u32x4{t[0], t[1], t[2], t[3]};
-            }
+            or_window_global((uintptr_t)(S.addr[k] + (u64)(i64)(P - S.o[k])), max(lo, 0), hi, t);
         }
-        const u32 rr[4] = {r.x, r.y, r.z, r.w};
-        store_chunk(out_t, P, 0, span, rr);
+        store_chunk(out_t, P, 0, span, t);
     }
 }
 
-template <typename T, typename Op>
-size_t scan_temp(u64 n, Op op) {
-    size_t bytes = 0;
-    (void)rocprim::exclusive_scan(nullptr, bytes, (const T*)nullptr, (T*)nullptr, T{}, (size_t)n + 1, op);
-    return (bytes + 255) & ~(size_t)255;
-}
-
 inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
-
-hipError_t launch_gather(const GatherArgs& a, bool fw, hipStream_t stream) {
-    const u64 tiles = (a.n + kSegs - 1) / kSegs;
-    const dim3 grid((unsigned)((tiles + kWaves - 1) / kWaves)), block(kWaves * 64);
-    if (fw) hipLaunchKernelGGL(gather_kernel<true>, grid, block, 0, stream, a);
-    else hipLaunchKernelGGL(gather_kernel<false>, grid, block, 0, stream, a);
-    return hipGetLastError();
-}
+inline u64 tiles_of(u64 n) { return (n + 255) / 256; }
 
 }  // namespace raw
 
@@ -260,70 +362,71 @@ hipError_t launch_raw_fixed(const uint8_t* in, const u64* rec_off, u64 n, int pr
     return hipGetLastError();
 }
 
-size_t raw_bytes_ws_bytes(u64 n) {
-    return 2 * raw::al256((n + 1) * sizeof(u64)) + raw::scan_temp<u64>(n, rocprim::plus<u64>());
+// workspace: [tile totals (ntiles) | tile prefixes (ntiles+1) | VAR: value sources (n) | lengths (n)]
+static size_t tile_ws(u64 n) { return 2 * raw::al256((raw::tiles_of(n) + 1) * sizeof(raw::Pair)); }
+
+size_t raw_bytes_ws_bytes(u64 n) { return tile_ws(n) + 2 * raw::al256(n * sizeof(u64)); }
+
+size_t firewall_ws_bytes(u64 n) { return tile_ws(n); }
+
+static hipError_t scan_and_gather(raw::GatherArgs& a, bool fw, raw::Pair* agg, raw::Pair* pre, hipStream_t stream) {
+    const u64 nt = raw::tiles_of(a.n);
+    hipLaunchKernelGGL(raw::tile_scan_kernel, dim3(1), dim3(1024), 0, stream, agg, pre, nt);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    a.pre = pre;
+    if (fw) hipLaunchKernelGGL(raw::gather_kernel<true>, dim3((unsigned)nt), dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL(raw::gather_kernel<false>, dim3((unsigned)nt), dim3(256), 0, stream, a);
+    return hipGetLastError();
 }
 
 hipError_t launch_raw_bytes(const uint8_t* in, const u64* rec_off, u64 n, int priv, u32 table_off, uint8_t* out,
                             u64 cap, u64* out_off, uint8_t* status, void* ws, unsigned* err, hipStream_t stream) {
-    const size_t col = raw::al256((n + 1) * sizeof(u64));
-    u64* seg_src = (u64*)ws;
-    u64* seg_len = (u64*)((char*)ws + col);
-    void* temp = (char*)ws + 2 * col;
-    size_t tb = raw::scan_temp<u64>(n, rocprim::plus<u64>());
-    hipLaunchKernelGGL(raw::var_locate_kernel, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, stream, in,
-                       rec_off, n, priv, table_off, seg_src, seg_len, status);
+    if (n == 0) return hipMemsetAsync(out_off, 0, sizeof(u64), stream);
+    const size_t pc = raw::al256((raw::tiles_of(n) + 1) * sizeof(raw::Pair));
+    raw::Pair* agg = (raw::Pair*)ws;
+    raw::Pair* pre = (raw::Pair*)((char*)ws + pc);
+    u64* seg_src = (u64*)((char*)ws + 2 * pc);
+    u64* seg_len = (u64*)((char*)ws + 2 * pc + raw::al256(n * sizeof(u64)));
+    hipLaunchKernelGGL(raw::var_locate_kernel, dim3((unsigned)raw::tiles_of(n)), dim3(256), 0, stream, in, rec_off, n,
+                       priv, table_off, seg_src, seg_len, status, agg);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    e = rocprim::exclusive_scan(temp, tb, (const u64*)seg_len, out_off, (u64)0, (size_t)n + 1, rocprim::plus<u64>(),
-                                stream);
-    if (e != hipSuccess || n == 0) return e;
     raw::GatherArgs a{};
     a.in = in;
     a.rec_off = rec_off;
-    a.src = seg_src;
-    a.dst = out_off;
-    a.ds = 1;
     a.n = n;
+    a.seg_src = seg_src;
+    a.seg_len = seg_len;
     a.out = out;
     a.cap = cap;
+    a.out_off = out_off;
     a.err = err;
-    return raw::launch_gather(a, false, stream);
-}
-
-size_t firewall_ws_bytes(u64 n) {
-    return 2 * raw::al256((n + 1) * sizeof(raw::Pair)) + raw::scan_temp<raw::Pair>(n, raw::PairPlus());
+    return scan_and_gather(a, false, agg, pre, stream);
 }
 
 hipError_t launch_firewall(const uint8_t* in, const u64* rec_off, u64 n, u32 score_table_off, int32_t threshold,
                            int32_t* score, uint8_t* verdict, uint8_t* kept, u64 cap, u64* kept_off, u64* kept_index,
                            u64* nkept, void* ws, unsigned* err, hipStream_t stream) {
-    const size_t col = raw::al256((n + 1) * sizeof(raw::Pair));
-    raw::Pair* mark = (raw::Pair*)ws;
-    raw::Pair* pre = (raw::Pair*)((char*)ws + col);
-    void* temp = (char*)ws + 2 * col;
-    size_t tb = raw::scan_temp<raw::Pair>(n, raw::PairPlus());
-    hipLaunchKernelGGL(raw::firewall_mark_kernel, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, stream, in,
-                       rec_off, n, score_table_off, threshold, score, verdict, mark);
+    const size_t pc = raw::al256((raw::tiles_of(n) + 1) * sizeof(raw::Pair));
+    raw::Pair* agg = (raw::Pair*)ws;
+    raw::Pair* pre = (raw::Pair*)((char*)ws + pc);
+    hipLaunchKernelGGL(raw::firewall_mark_kernel, dim3((unsigned)raw::tiles_of(n)), dim3(256), 0, stream, in, rec_off,
+                       n, score_table_off, threshold, score, verdict, agg);
     hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    e = rocprim::exclusive_scan(temp, tb, (const raw::Pair*)mark, pre, raw::Pair{0, 0}, (size_t)n + 1,
-                                raw::PairPlus(), stream);
     if (e != hipSuccess) return e;
     raw::GatherArgs a{};
     a.in = in;
     a.rec_off = rec_off;
-    a.src = rec_off;
-    a.dst = (const u64*)pre;
-    a.ds = 2;
     a.n = n;
+    a.verdict = verdict;
     a.out = kept;
     a.cap = cap;
-    a.kept_off = kept_off;
+    a.out_off = kept_off;
     a.kept_index = kept_index;
     a.nkept = nkept;
     a.err = err;
-    return raw::launch_gather(a, true, stream);
+    return scan_and_gather(a, true, agg, pre, stream);
 }
 
 }  // namespace symhip

@@ -180,6 +180,58 @@ def packetize_leg(codec: Codec, data: torch.Tensor, rec_off: torch.Tensor, dev, 
                     "transport.go:146-201), device-resident, outside the timed region"}
 
 
+def proxy_leg(codec: Codec, dev, reps: int) -> dict:
+    """SURVEY.md 8f N1 beside the headline: the proxy's firewall element (GetScore, shouldBlock, and
+    the passing requests compacted into a forwardable batch) and the Raw getters GetScore /
+    GetUsername, over 2^20 element-schema SetRequests (datagen.ELEMENT_FW: Username 16, Key 64,
+    Value 256 -> 378-byte records), device-resident, HIP events.  Threshold 50 on scores uniform in
+    [0, 100): half the requests pass.
+    Algorithmic bytes -- firewall: offsets 8(n+1) + score 4n read, kept bytes read and written,
+    score 4n + verdict n + kept offsets 8(k+1) + kept index 8k written; GetScore: offsets + 4n read,
+    4n value + n status written; GetUsername: offsets + table entry, length and value read, value +
+    offsets 8(n+1) + n status written."""
+    from arpc_amd import datagen
+    b = datagen.make_element_batch(**datagen.ELEMENT_FW)
+    n = len(b.score)
+    data = torch.from_numpy(b.data).to(dev)
+    off = torch.from_numpy(b.rec_off.view(np.int64)).to(dev)
+    fw = codec.firewall(data, off, 50)
+    codec.raw_get_fixed(data, off, 13, 4)
+    ub, uo, _ = codec.raw_get_bytes(data, off, 17)
+    torch.cuda.synchronize()
+    codec.check()
+    k = int(fw.nkept.item())
+    kept_b = int(fw.kept_off[k].item())
+    user_b = int(uo[n].item())
+
+    def timed(fn) -> float:
+        ev = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            ev.append((e0, e1))
+        torch.cuda.synchronize()
+        codec.check()
+        return float(np.median([a.elapsed_time(c) for a, c in ev]))
+
+    fw_ms = timed(lambda: codec.firewall(data, off, 50))
+    sc_ms = timed(lambda: codec.raw_get_fixed(data, off, 13, 4))
+    un_ms = timed(lambda: codec.raw_get_bytes(data, off, 17))
+    fw_alg = 8 * (n + 1) + 4 * n + 2 * kept_b + 4 * n + n + 8 * (k + 1) + 8 * k
+    sc_alg = 8 * (n + 1) + 4 * n + 4 * n + n
+    un_alg = 8 * (n + 1) + 8 * n + 2 * user_b + 8 * (n + 1) + n
+    gbps = lambda a, ms: round(a / (ms * 1e-3) / 1e9, 1)
+    return {"records": n, "record_bytes": int(b.rec_off[1]), "threshold": 50, "kept": k, "kept_bytes": kept_b,
+            "firewall_ms": round(fw_ms, 4), "firewall_alg_bytes": fw_alg, "firewall_gbps": gbps(fw_alg, fw_ms),
+            "firewall_mrps": round(n / (fw_ms * 1e-3) / 1e6, 1),
+            "get_score_ms": round(sc_ms, 4), "get_score_gbps": gbps(sc_alg, sc_ms),
+            "get_username_ms": round(un_ms, 4), "get_username_gbps": gbps(un_alg, un_ms),
+            "note": "FirewallElement.ProcessRequest (cmd/proxy/element/firewall.go:39-52) and GetRequestRaw "
+                    "getters (kv-store-symphony-element kv.syn.go:285-310) batched; outside the timed region"}
+
+
 def host_inclusive(codec: Codec, kw: dict, dev, steps: int) -> dict:
     """Pinned host -> H2D -> encode -> D2H, then H2D -> decode -> D2H (serial, one stream)."""
     b = datagen.make_batch(**kw)
@@ -237,6 +289,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--host-steps", type=int, default=5, help="host-inclusive steps (0 = skip)")
     ap.add_argument("--packetize-reps", type=int, default=5, help="packetization leg repetitions (0 = skip)")
+    ap.add_argument("--proxy-reps", type=int, default=10, help="firewall / Raw getter leg repetitions (0 = skip)")
     args = ap.parse_args()
 
     world, rank, local = dist_setup()
@@ -379,6 +432,8 @@ def main():
         line["host_inclusive"] = host_inclusive(codec, kw, dev, args.host_steps)
     if world == 1 and args.packetize_reps > 0:
         line["packetize"] = packetize_leg(codec, enc[0][0], enc[0][1], dev, args.packetize_reps)
+    if world == 1 and args.proxy_reps > 0:
+        line["proxy"] = proxy_leg(codec, dev, args.proxy_reps)
     if world == 1 and args.cpu_seconds > 0:
         line["cpu_baseline"] = cpu_baseline(kw, args.cpu_seconds)
     print(json.dumps(line), flush=True)
