@@ -58,6 +58,7 @@ SIGNATURES = {
     "sym_raw_get_bytes": (_int, [_ctx, _u8p, _u64p, _u64, _int, _u32, _u8p, _u64, _u64p, _u8p, _vp]),
     "sym_firewall_filter": (_int, [_ctx, _u8p, _u64p, _u64, _u32, ctypes.c_int32, _vp, _u8p, _u8p, _u64, _u64p,
                                    _u64p, _u64p, _vp]),
+    "sym_reassemble": (_int, [_ctx, _u8p, _u64p, _u64, _u8p, _u64, _u64p, _u64p, _u64p, _u64p, _u8p, _vp]),
 }
 
 SYM_MAX_UDP_PAYLOAD = 1400
@@ -76,6 +77,11 @@ SYM_RAW_INVALID_BUFFER = 1
 SYM_RAW_PUBLIC_ONLY = 2
 SYM_VERDICT_PASS = 1
 SYM_VERDICT_DROP = 2
+SYM_RX_CONSUMED = 0
+SYM_RX_PENDING = 1
+SYM_RX_NOT_DATA = 2
+SYM_RX_TOO_SHORT = 3
+SYM_RX_BAD_LENGTH = 4
 
 
 class Endpoints(ctypes.Structure):

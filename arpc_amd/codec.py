@@ -259,6 +259,39 @@ def _firewall(codec: "Codec", data: torch.Tensor, rec_off: torch.Tensor, block_t
     return Filtered(score[:n], verdict[:n], kept, kept_off, kept_index[:n], nkept)
 
 
+@dataclass
+class Messages:
+    data: torch.Tensor     # uint8 [>= message bytes]: completed messages back to back
+    offsets: torch.Tensor  # int64 [n+1]: the first nmsg+1 entries are the message offsets
+    rpc_id: torch.Tensor   # int64 [n]: the first nmsg entries are their RPCIDs
+    dgram: torch.Tensor    # int64 [n]: ... and the arrival index of each one's completing datagram
+    nmsg: torch.Tensor     # int64 [1] (device)
+    status: torch.Tensor   # uint8 [n]: SYM_RX_* per datagram
+
+
+def _reassemble(codec: "Codec", wire: torch.Tensor, dg_off: torch.Tensor, cap: int | None = None,
+                stream=None) -> Messages:
+    """UDPTransport.Receive + DataReassembler.ProcessFragment (pkg/transport/transport.go:253-317,
+    fragmentation.go:49-183) over n datagrams in arrival order, device-resident, no host sync.
+    `cap` bounds the message bytes (default: the wire size, which always suffices)."""
+    _check_col(wire, torch.uint8, "wire", codec.device)
+    _check_col(dg_off, torch.int64, "dg_off", codec.device)
+    n = dg_off.numel() - 1
+    dev = codec.device
+    cap = wire.numel() if cap is None else cap
+    data = torch.empty(max(1, cap), dtype=torch.uint8, device=dev)
+    offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    rpc = torch.empty(max(1, n), dtype=torch.int64, device=dev)
+    dg = torch.empty(max(1, n), dtype=torch.int64, device=dev)
+    nmsg = torch.empty(1, dtype=torch.int64, device=dev)
+    status = torch.empty(max(1, n), dtype=torch.uint8, device=dev)
+    _native.check(codec._lib.sym_reassemble(codec._ctx, _dptr(wire) if wire.numel() else 1, _dptr(dg_off), n,
+                                           _dptr(data), cap, _dptr(offs), _dptr(rpc), _dptr(dg), _dptr(nmsg),
+                                           _dptr(status), _stream_handle(dev, stream)), "sym_reassemble")
+    return Messages(data, offs, rpc[:n], dg[:n], nmsg, status[:n])
+
+
+Codec.reassemble = _reassemble
 Codec.raw_get_fixed = _raw_get_fixed
 Codec.raw_get_bytes = _raw_get_bytes
 Codec.firewall = _firewall

@@ -632,4 +632,27 @@ int sym_firewall_filter(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec
     return e == hipSuccess ? SYM_OK : hip_fail(e, "firewall launch");
 }
 
+int sym_reassemble(sym_ctx* ctx, const uint8_t* d_wire, const uint64_t* d_dg_off, uint64_t n, uint8_t* d_msg,
+                   uint64_t msg_cap, uint64_t* d_msg_off, uint64_t* d_msg_rpc, uint64_t* d_msg_dg, uint64_t* d_nmsg,
+                   uint8_t* d_status, void* stream) {
+    if (!ctx) return fail(SYM_ERR_INVALID, "sym_reassemble: ctx is NULL");
+    if (n >= ((uint64_t)1 << 31)) return fail(SYM_ERR_INVALID, "sym_reassemble: %llu datagrams (limit 2^31)",
+                                              (unsigned long long)n);
+    if (!d_msg_off || !d_nmsg ||
+        (n && (!d_wire || !d_dg_off || !d_msg_rpc || !d_msg_dg || !d_status || (msg_cap && !d_msg))))
+        return fail(SYM_ERR_INVALID, "sym_reassemble: NULL argument");
+    DeviceGuard g(ctx->device);
+    if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
+    if (n == 0) {
+        hipError_t e = hipMemsetAsync(d_msg_off, 0, sizeof(uint64_t), (hipStream_t)stream);
+        if (e == hipSuccess) e = hipMemsetAsync(d_nmsg, 0, sizeof(uint64_t), (hipStream_t)stream);
+        return e == hipSuccess ? SYM_OK : hip_fail(e, "hipMemsetAsync");
+    }
+    const int rc = ensure_scratch(ctx, symhip::reassemble_ws_bytes(n), "reassembly");
+    if (rc != SYM_OK) return rc;
+    hipError_t e = symhip::launch_reassemble(d_wire, d_dg_off, n, d_msg, msg_cap, d_msg_off, d_msg_rpc, d_msg_dg, d_nmsg,
+                                             d_status, ctx->frag, ctx->err, (hipStream_t)stream);
+    return e == hipSuccess ? SYM_OK : hip_fail(e, "reassembly launch");
+}
+
 }  // extern "C"

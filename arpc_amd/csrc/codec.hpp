@@ -96,6 +96,40 @@ hipError_t launch_frag_plan(const uint8_t* in, const uint64_t* rec_off, uint64_t
                             size_t temp_bytes, hipStream_t stream);
 hipError_t launch_frag_write(const FragWriteArgs& a, hipStream_t stream);
 
+// ---- segment gather (raw_fields.hip): out = the segments in[src[i], src[i] + len[i]) back to back
+namespace raw {
+struct Pair {  // tile total / prefix: bytes, records (kept records for the firewall)
+    uint64_t bytes, count;
+};
+struct GatherArgs {
+    const uint8_t* in;
+    const uint64_t* rec_off;  // FW: the records
+    uint64_t n;               // segments, or an upper bound of them when n_ptr is set
+    const uint64_t* n_ptr;    // nullable: the segment count, on the device
+    const uint64_t* lo_ptr;   // readable input range [*lo_ptr, *hi_ptr) (for unconditional loads)
+    const uint64_t* hi_ptr;
+    const Pair* pre;          // tile prefixes of the lengths (tiles_of(n) + 1)
+    // VAR: segment sources and lengths; FW: records, kept when verdict == PASS
+    const uint64_t* seg_src;
+    const uint64_t* seg_len;
+    const uint8_t* verdict;
+    uint8_t* out;
+    uint64_t cap;
+    uint64_t* out_off;     // VAR: segment offsets (n+1, nullable); FW: kept record offsets (nkept+1)
+    uint64_t* kept_index;  // FW: input position of each kept record (nullable)
+    uint64_t* nkept;       // FW
+    unsigned* err;
+};
+}  // namespace raw
+hipError_t launch_tile_scan(const raw::Pair* agg, raw::Pair* pre, uint64_t ntiles, hipStream_t stream);
+hipError_t launch_segment_gather(const raw::GatherArgs& a, hipStream_t stream);
+
+// ---- receive-side reassembly (reassemble.hip)
+size_t reassemble_ws_bytes(uint64_t n);
+hipError_t launch_reassemble(const uint8_t* wire, const uint64_t* dg_off, uint64_t n, uint8_t* msg, uint64_t msg_cap,
+                             uint64_t* msg_off, uint64_t* msg_rpc, uint64_t* msg_dg, uint64_t* nmsg, uint8_t* status,
+                             void* ws, unsigned* err, hipStream_t stream);
+
 // ---- batched Raw getters and the firewall element (raw_fields.hip)
 hipError_t launch_raw_fixed(const uint8_t* in, const uint64_t* rec_off, uint64_t n, int priv, uint32_t table_off,
                             uint32_t width, void* out, uint8_t* status, hipStream_t stream);

@@ -30,10 +30,6 @@ namespace raw {
 constexpr int kSegs = 64;  // segments per wave tile
 constexpr int kWaves = 4;
 
-struct Pair {  // tile total / prefix: bytes, records (kept records for the firewall)
-    u64 bytes, count;
-};
-
 // The private getters' complete-buffer assertion (main.go:1003-1013); sets off2p when it holds.
 __device__ inline uint8_t private_check(uintptr_t m, u64 L, u64& off2p) {
     if (L < 5) return SYM_RAW_INVALID_BUFFER;
@@ -186,23 +182,6 @@ __global__ __launch_bounds__(1024) void tile_scan_kernel(const Pair* agg, Pair* 
 }
 
 // ---- gather: each workgroup owns a 256-record tile; out gets the segments back to back
-struct GatherArgs {
-    const uint8_t* in;
-    const u64* rec_off;
-    u64 n;
-    const Pair* pre;    // tile prefixes (ntiles + 1)
-    // VAR: value sources and lengths; FW: records, kept when verdict == PASS
-    const u64* seg_src;
-    const u64* seg_len;
-    const uint8_t* verdict;
-    uint8_t* out;
-    u64 cap;
-    u64* out_off;     // VAR: value offsets (n+1); FW: kept record offsets (nkept+1)
-    u64* kept_index;  // FW: input position of each kept record (nullable)
-    u64* nkept;       // FW
-    unsigned* err;
-};
-
 struct WaveLds {
     u64 addr[kSegs];   // segment's source address
     int o[kSegs + 1];  // segment's output start relative to the wave's; [cnt] = span
@@ -218,13 +197,14 @@ __global__ __launch_bounds__(kWaves * 64) void gather_kernel(GatherArgs a) {
     __shared__ MaskTable masks;
     __shared__ u64 wsum_b[kWaves], wsum_c[kWaves];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const u64 ntiles = (a.n + 255) / 256;
+    const u64 ntiles = (a.n + 255) / 256;    // of the tile scan (a.n bounds the segment count)
+    const u64 n = a.n_ptr ? *a.n_ptr : a.n;  // segments
     const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
     mask_table_init(masks, threadIdx.x);
 
     // ---- phase 1 (thread = record): length, keep flag, in-tile exclusive scan
     u64 src = 0, len = 0, keep = 0;
-    if (i < a.n) {
+    if (i < n) {
         if constexpr (FW) {
             src = a.rec_off[i];
             keep = a.verdict[i] == SYM_VERDICT_PASS;
@@ -259,26 +239,26 @@ __global__ __launch_bounds__(kWaves * 64) void gather_kernel(GatherArgs a) {
             a.out_off[rank] = d;
             if (a.kept_index) a.kept_index[rank] = i;
         }
-        if (i == a.n - 1) {
+        if (i == n - 1) {
             a.out_off[rank + keep] = d + len;
             *a.nkept = rank + keep;
         }
     } else {
-        if (i < a.n) a.out_off[i] = d;
-        if (i == a.n - 1) a.out_off[a.n] = d + len;
+        if (a.out_off && i < n) a.out_off[i] = d;
+        if (a.out_off && i == n - 1) a.out_off[n] = d + len;
     }
 
     // ---- phase 2 (wave = 64 segments, lane = aligned 16-byte output chunk)
     const u64 r0 = (u64)blockIdx.x * 256 + (u64)wave * kSegs;
-    if (r0 >= a.n) return;  // wave-uniform
-    const int cnt = (int)min((u64)kSegs, a.n - r0);
+    if (r0 >= n) return;  // wave-uniform
+    const int cnt = (int)min((u64)kSegs, n - r0);
     WaveLds& S = lds_all[wave];
     const u64 D0 = readlane_u64(d, 0), D1 = readlane_u64(d + len, cnt - 1);
     if (D1 - D0 >= ((u64)1 << 31)) {  // positions are 32-bit
         if (lane == 0) atomicOr(a.err, kErrTooLarge);
         return;
     }
-    const u64 in_lo = a.rec_off[0], in_hi = a.rec_off[a.n];
+    const u64 in_lo = *a.lo_ptr, in_hi = *a.hi_ptr;
     // Only non-empty segments go to LDS (dropped records, unset values): a chunk then usually
     // covers one or two of them, which the unrolled path below loads without a loop.
     const bool live = lane < cnt && len > 0;
@@ -369,6 +349,16 @@ size_t raw_bytes_ws_bytes(u64 n) { return tile_ws(n) + 2 * raw::al256(n * sizeof
 
 size_t firewall_ws_bytes(u64 n) { return tile_ws(n); }
 
+hipError_t launch_tile_scan(const raw::Pair* agg, raw::Pair* pre, u64 ntiles, hipStream_t stream) {
+    hipLaunchKernelGGL(raw::tile_scan_kernel, dim3(1), dim3(1024), 0, stream, agg, pre, ntiles);
+    return hipGetLastError();
+}
+
+hipError_t launch_segment_gather(const raw::GatherArgs& a, hipStream_t stream) {
+    hipLaunchKernelGGL(raw::gather_kernel<false>, dim3((unsigned)raw::tiles_of(a.n)), dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
+
 static hipError_t scan_and_gather(raw::GatherArgs& a, bool fw, raw::Pair* agg, raw::Pair* pre, hipStream_t stream) {
     const u64 nt = raw::tiles_of(a.n);
     hipLaunchKernelGGL(raw::tile_scan_kernel, dim3(1), dim3(1024), 0, stream, agg, pre, nt);
@@ -396,6 +386,8 @@ hipError_t launch_raw_bytes(const uint8_t* in, const u64* rec_off, u64 n, int pr
     a.in = in;
     a.rec_off = rec_off;
     a.n = n;
+    a.lo_ptr = rec_off;
+    a.hi_ptr = rec_off + n;
     a.seg_src = seg_src;
     a.seg_len = seg_len;
     a.out = out;
@@ -419,6 +411,8 @@ hipError_t launch_firewall(const uint8_t* in, const u64* rec_off, u64 n, u32 sco
     a.in = in;
     a.rec_off = rec_off;
     a.n = n;
+    a.lo_ptr = rec_off;
+    a.hi_ptr = rec_off + n;
     a.verdict = verdict;
     a.out = kept;
     a.cap = cap;

@@ -1,0 +1,422 @@
+// reassemble.hip -- batched receive-side reassembly of aRPC DataPackets on gfx950.
+//
+// Restates, for n datagrams received in a given order, what UDPTransport.Receive
+// (pkg/transport/transport.go:253-317) + DataPacketCodec.Deserialize (pkg/packet/builtin_packets.go:
+// 118-161) + DataReassembler.ProcessFragment (pkg/transport/fragmentation.go:49-183) return one call
+// at a time: every completed message, in completion order, with its RPCID and completing datagram,
+// plus each datagram's fate (consumed by a message, still pending, or dropped by the parser).
+//
+// The reassembler keeps one state per RPCID and its decisions for one RPCID depend only on that
+// RPCID's datagrams in arrival order, so the batch is regrouped rather than replayed:
+//  1. parse (thread per datagram): header checks, and the RPCID inserted into an open-addressing
+//     hash table whose slot index becomes a dense group key;
+//  2. a stable radix sort (rocPRIM) of (group key, arrival index) on only the key's ~log2(2n) bits:
+//     each group becomes a contiguous run in arrival order;
+//  3. group pass (thread per group): the ProcessFragment state machine over the group's run, with
+//     per-sequence state (fragment-index bitmap, last index, latest index-0 fragment) in a scratch
+//     slice owned by the group, O(1) work per datagram; it records, at each completing datagram,
+//     the message's (bytes, segments, 1);
+//  4. an exclusive scan of those triples in ARRIVAL order gives every message its index, byte
+//     offset and first segment -- completion order across RPCIDs is arrival order of the
+//     completing datagrams, as in the one-at-a-time loop;
+//  5. the group pass again, now writing message offsets / RPCIDs / completing datagrams and the
+//     message's payload segments (wire offset, length) in (seq, fragment index) order;
+//  6. the segment gather of raw_fields.hip copies the payloads into the message stream.
+#include <cstring>  // rocprim/iterator/texture_cache_iterator.hpp uses memset
+
+#include <rocprim/device/device_radix_sort.hpp>
+
+#include "../../include/symphony_hip.h"
+#include "codec.hpp"
+#include "device_util.hpp"
+
+namespace symhip {
+
+namespace rx {
+
+using raw::Pair;
+
+constexpr int kHdr = 31;        // DataPacket header (builtin_packets.go:68)
+constexpr u64 kEmpty = ~0ull;   // free hash slot; an RPCID equal to it gets the group key `special`
+
+struct SeqState {    // one sequence number of the group's current message
+    u32 bits[8];     // fragment indices received (0..255)
+    u32 latest0;     // arrival index of the latest fragment with index 0
+    u32 flags;       // 1 seen, 2 has its last fragment, 4 complete; lastFragmentIndex << 8
+};
+
+__device__ inline u64 mix64(u64 x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdull;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ull;
+    x ^= x >> 33;
+    return x;
+}
+
+// meta: seq | total << 16 | more << 32 | fragment index << 40
+__device__ inline u32 m_seq(u64 m) { return (u32)(m & 0xffff); }
+__device__ inline u32 m_total(u64 m) { return (u32)((m >> 16) & 0xffff); }
+__device__ inline bool m_more(u64 m) { return (m >> 32) & 1; }
+__device__ inline u32 m_fidx(u64 m) { return (u32)((m >> 40) & 0xff); }
+
+struct Args {
+    const uint8_t* wire;
+    const u64* dg_off;
+    u64 n;
+    u64* table;
+    u64 tmask;
+    u32 special, nodata;   // group keys: RPCID == kEmpty, not a DataPacket
+    u64* rpc;
+    u64* meta;
+    u32* plen;
+    u32* gid;
+    u32* idx;
+    const u32* gs;         // sorted group keys / arrival indices
+    const u32* is;
+    SeqState* state;
+    uint8_t* status;
+    Pair* cnt;             // per arrival (n+1): (message bytes, segments << 32 | messages)
+    const Pair* pre;       // its exclusive scan
+    u64* msg_off;
+    u64* msg_rpc;
+    u64* msg_dg;
+    u64* seg_src;
+    u64* seg_len;
+};
+
+// ---- 1. parse + group key (transport.go:266-283, builtin_packets.go:118-161)
+__global__ __launch_bounds__(256) void parse_kernel(Args a) {
+    const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
+    if (i > a.n) return;
+    a.cnt[i] = Pair{0, 0};
+    if (i == a.n) return;
+    const u64 s = a.dg_off[i], L = a.dg_off[i + 1] - s;
+    const uintptr_t p = (uintptr_t)(a.wire + s);
+    uint8_t st = SYM_RX_PENDING;
+    u32 g = a.nodata;
+    if (L < 1) {
+        st = SYM_RX_TOO_SHORT;                       // "data too short to read packet type"
+    } else if (const u32 t = ld_u8(p); t != 1 && t != 2) {
+        st = SYM_RX_NOT_DATA;                        // Error packet, or no codec for the type
+    } else if (L < kHdr) {
+        st = SYM_RX_TOO_SHORT;                       // "data too short for DataPacket header"
+    } else {
+        const u32 pl = ld_u32(p + 27);
+        if (L < (u64)kHdr + pl) {
+            st = SYM_RX_BAD_LENGTH;                  // "too short for declared payload length"
+        } else {
+            const u64 r = (u64)ld_u32(p + 1) | ((u64)ld_u32(p + 5) << 32);
+            a.rpc[i] = r;
+            a.meta[i] = (u64)(ld_u32(p + 11) & 0xffff) | ((u64)(ld_u32(p + 9) & 0xffff) << 16) |
+                        ((u64)(ld_u8(p + 13) != 0) << 32) | ((u64)ld_u8(p + 14) << 40);
+            a.plen[i] = pl;
+            if (r == kEmpty) {
+                g = a.special;
+            } else {  // open addressing; the table has >= 2n slots, so a free slot is always found
+                u64 h = mix64(r) & a.tmask;
+                for (;;) {
+                    const u64 prev = atomicCAS((unsigned long long*)&a.table[h], (unsigned long long)kEmpty,
+                                               (unsigned long long)r);
+                    if (prev == kEmpty || prev == r) break;
+                    h = (h + 1) & a.tmask;
+                }
+                g = (u32)h;
+            }
+        }
+    }
+    a.status[i] = st;
+    a.gid[i] = g;
+    a.idx[i] = (u32)i;
+}
+
+__device__ inline bool seq_complete(const SeqState& x) {
+    if (!(x.flags & 2)) return false;
+    const u32 li = x.flags >> 8;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+        const int hi = (int)li - 32 * w;  // highest wanted bit in this word
+        if (hi < 0) break;
+        const u32 need = hi >= 31 ? ~0u : (2u << hi) - 1u;
+        if ((x.bits[w] & need) != need) return false;
+    }
+    return true;
+}
+
+// ---- 3 / 5. the ProcessFragment state machine over one group's run (fragmentation.go:62-181)
+template <int PASS>
+__global__ __launch_bounds__(256) void group_kernel(Args a) {
+    const u64 q0 = (u64)blockIdx.x * 256 + threadIdx.x;
+    if (q0 >= a.n) return;
+    const u32 g = a.gs[q0];
+    if (g > a.special) return;                   // not a DataPacket (sorted last)
+    if (q0 > 0 && a.gs[q0 - 1] == g) return;     // not the first of its group
+    u64 e = q0 + 1;
+    while (e < a.n && a.gs[e] == g) ++e;
+    const u64 k = e - q0;                        // sequence numbers >= k can never complete
+    SeqState* S = a.state + q0;
+    for (u64 t = 0; t < k; ++t) S[t] = SeqState{};
+    u64 r = q0;  // first datagram of the current message
+    u32 distinct = 0, ncomplete = 0, maxseq = 0;
+    bool big = false;
+    for (u64 q = q0; q < e; ++q) {
+        const u32 j = a.is[q];
+        const u64 m = a.meta[j];
+        const u32 s = m_seq(m), T = m_total(m), fi = m_fidx(m);
+        if (s >= k) {
+            big = true;
+        } else {
+            SeqState x = S[s];
+            const bool was = seq_complete(x);
+            if (!(x.flags & 1)) {
+                x.flags |= 1;
+                ++distinct;
+            }
+            x.bits[fi >> 5] |= 1u << (fi & 31);
+            if (fi == 0) x.latest0 = j;            // a later fragment overwrites (map store, :79-83)
+            if (!m_more(m)) {                       // :87-93
+                const u32 li = max(x.flags >> 8, fi);
+                x.flags = (x.flags & 0xffu) | 2u | (li << 8);
+            }
+            const bool now = seq_complete(x);
+            ncomplete += (u32)now - (u32)was;
+            S[s] = x;
+        }
+        maxseq = max(maxseq, s);
+        // :99-133 -- distinct sequence numbers == TotalPackets of THIS packet and all complete
+        if (big || T == 0 || maxseq >= T || distinct != T || ncomplete != T) continue;
+        u64 bytes = 0, segs = 0, ob = 0, sb = 0;
+        if constexpr (PASS == 1) {
+            const Pair pp = a.pre[j];
+            const u64 mi = pp.count & 0xffffffffull;
+            sb = pp.count >> 32;
+            ob = pp.bytes;
+            a.msg_off[mi] = ob;
+            a.msg_rpc[mi] = a.rpc[j];
+            a.msg_dg[mi] = j;
+        }
+        for (u32 s2 = 0; s2 < T; ++s2) {           // :153-161, (seq, fragment index) order
+            const SeqState x = S[s2];
+            const u32 li = x.flags >> 8;
+            for (u32 f = 0; f <= li; ++f) {
+                u32 src = x.latest0;
+                if (f > 0)                          // rare: the latest arrival with (s2, f)
+                    for (u64 b = q + 1; b-- > r;) {
+                        const u64 mb = a.meta[a.is[b]];
+                        if (m_seq(mb) == s2 && m_fidx(mb) == f) {
+                            src = a.is[b];
+                            break;
+                        }
+                    }
+                if constexpr (PASS == 1) {
+                    a.seg_src[sb + segs] = a.dg_off[src] + kHdr;
+                    a.seg_len[sb + segs] = a.plen[src];
+                }
+                bytes += a.plen[src];
+                ++segs;
+            }
+        }
+        if constexpr (PASS == 0) a.cnt[j] = Pair{bytes, (segs << 32) | 1u};
+        for (u64 b = r; b <= q; ++b) {              // :175-178: the RPCID's state is deleted
+            const u32 jb = a.is[b];
+            if constexpr (PASS == 0) a.status[jb] = SYM_RX_CONSUMED;
+            const u32 sb2 = m_seq(a.meta[jb]);
+            if (sb2 < k) S[sb2] = SeqState{};
+        }
+        r = q + 1;
+        distinct = ncomplete = maxseq = 0;
+        big = false;
+    }
+}
+
+// ---- 4. exclusive scan of the per-arrival triples (256 per tile)
+__device__ inline void block_scan_pair(Pair v, Pair& excl, Pair& tile_total) {
+    __shared__ u64 wb[4], wc[4];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const u64 ib = wave_incl_scan_u64(v.bytes, lane), ic = wave_incl_scan_u64(v.count, lane);
+    if (lane == 63) {
+        wb[wave] = ib;
+        wc[wave] = ic;
+    }
+    __syncthreads();
+    u64 pb = 0, pc = 0;
+    for (int q = 0; q < wave; ++q) {
+        pb += wb[q];
+        pc += wc[q];
+    }
+    excl = Pair{pb + ib - v.bytes, pc + ic - v.count};
+    tile_total = Pair{wb[0] + wb[1] + wb[2] + wb[3], wc[0] + wc[1] + wc[2] + wc[3]};
+}
+
+__global__ __launch_bounds__(256) void pair_tile_total_kernel(const Pair* v, u64 m, Pair* agg) {
+    const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
+    Pair e, t;
+    block_scan_pair(i < m ? v[i] : Pair{0, 0}, e, t);
+    if (threadIdx.x == 0) agg[blockIdx.x] = t;
+}
+
+__global__ __launch_bounds__(256) void pair_scan_apply_kernel(const Pair* v, u64 m, const Pair* tpre, Pair* out) {
+    const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
+    Pair e, t;
+    block_scan_pair(i < m ? v[i] : Pair{0, 0}, e, t);
+    const Pair b = tpre[blockIdx.x];
+    if (i < m) out[i] = Pair{b.bytes + e.bytes, b.count + e.count};
+}
+
+// message count, closing offset and segment count from the grand total
+__global__ void finalize_kernel(const Pair* total, u64* msg_off, u64* nmsg, u64* nseg) {
+    const Pair t = *total;
+    const u64 nm = t.count & 0xffffffffull;
+    *nmsg = nm;
+    msg_off[nm] = t.bytes;
+    *nseg = t.count >> 32;
+}
+
+// ---- 6. tile totals of the segment lengths (segment count on the device)
+__global__ __launch_bounds__(256) void seg_tile_total_kernel(const u64* seg_len, const u64* nseg, Pair* agg) {
+    const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
+    Pair e, t;
+    block_scan_pair(Pair{i < *nseg ? seg_len[i] : 0, 0}, e, t);
+    if (threadIdx.x == 0) agg[blockIdx.x] = t;
+}
+
+inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+inline u64 tiles(u64 m) { return (m + 255) / 256; }
+inline u64 table_size(u64 n) {
+    u64 t = 1024;
+    while (t < 2 * n) t <<= 1;
+    return t;
+}
+inline unsigned log2u(u64 t) {
+    unsigned b = 0;
+    while (((u64)1 << b) < t) ++b;
+    return b;
+}
+
+struct Layout {
+    size_t table, rpc, meta, plen, gid, idx, gs, is, state, cnt, pre, agg, tpre, seg_src, seg_len, agg2, pre2, nseg,
+        temp, total;
+    size_t temp_bytes;
+};
+
+inline Layout layout(u64 n) {
+    Layout L{};
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+        const size_t at = o;
+        o += al256(bytes);
+        return at;
+    };
+    const u64 TS = table_size(n);
+    L.table = take(TS * 8);
+    L.rpc = take(n * 8);
+    L.meta = take(n * 8);
+    L.plen = take(n * 4);
+    L.gid = take(n * 4);
+    L.idx = take(n * 4);
+    L.gs = take(n * 4);
+    L.is = take(n * 4);
+    L.state = take(n * sizeof(SeqState));
+    L.cnt = take((n + 1) * sizeof(Pair));
+    L.pre = take((n + 1) * sizeof(Pair));
+    L.agg = take((tiles(n + 1) + 1) * sizeof(Pair));
+    L.tpre = take((tiles(n + 1) + 1) * sizeof(Pair));
+    L.seg_src = take(n * 8);
+    L.seg_len = take(n * 8);
+    L.agg2 = take((tiles(n) + 1) * sizeof(Pair));
+    L.pre2 = take((tiles(n) + 1) * sizeof(Pair));
+    L.nseg = take(8);
+    size_t tb = 0;
+    (void)rocprim::radix_sort_pairs(nullptr, tb, (const u32*)nullptr, (u32*)nullptr, (const u32*)nullptr,
+                                    (u32*)nullptr, (size_t)n, 0u, log2u(TS) + 1);
+    L.temp_bytes = al256(tb);
+    L.temp = take(L.temp_bytes);
+    L.total = o;
+    return L;
+}
+
+}  // namespace rx
+
+size_t reassemble_ws_bytes(u64 n) { return rx::layout(n).total; }
+
+hipError_t launch_reassemble(const uint8_t* wire, const u64* dg_off, u64 n, uint8_t* msg, u64 msg_cap, u64* msg_off,
+                             u64* msg_rpc, u64* msg_dg, u64* nmsg, uint8_t* status, void* ws, unsigned* err,
+                             hipStream_t stream) {
+    using rx::Pair;
+    const rx::Layout L = rx::layout(n);
+    char* w = (char*)ws;
+    const u64 TS = rx::table_size(n);
+    rx::Args a{};
+    a.wire = wire;
+    a.dg_off = dg_off;
+    a.n = n;
+    a.table = (u64*)(w + L.table);
+    a.tmask = TS - 1;
+    a.special = (u32)TS;
+    a.nodata = (u32)TS + 1;
+    a.rpc = (u64*)(w + L.rpc);
+    a.meta = (u64*)(w + L.meta);
+    a.plen = (u32*)(w + L.plen);
+    a.gid = (u32*)(w + L.gid);
+    a.idx = (u32*)(w + L.idx);
+    a.gs = (const u32*)(w + L.gs);
+    a.is = (const u32*)(w + L.is);
+    a.state = (rx::SeqState*)(w + L.state);
+    a.status = status;
+    a.cnt = (Pair*)(w + L.cnt);
+    a.pre = (const Pair*)(w + L.pre);
+    a.msg_off = msg_off;
+    a.msg_rpc = msg_rpc;
+    a.msg_dg = msg_dg;
+    a.seg_src = (u64*)(w + L.seg_src);
+    a.seg_len = (u64*)(w + L.seg_len);
+    const dim3 b256(256);
+    hipError_t e = hipMemsetAsync(a.table, 0xff, TS * 8, stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(rx::parse_kernel, dim3((unsigned)rx::tiles(n + 1)), b256, 0, stream, a);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    size_t tb = L.temp_bytes;
+    e = rocprim::radix_sort_pairs(w + L.temp, tb, (const u32*)a.gid, (u32*)(w + L.gs), (const u32*)a.idx,
+                                  (u32*)(w + L.is), (size_t)n, 0u, rx::log2u(TS) + 1, stream);
+    if (e != hipSuccess) return e;
+    const dim3 gq((unsigned)rx::tiles(n));
+    hipLaunchKernelGGL(rx::group_kernel<0>, gq, b256, 0, stream, a);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    const u64 nt = rx::tiles(n + 1);
+    Pair* agg = (Pair*)(w + L.agg);
+    Pair* tpre = (Pair*)(w + L.tpre);
+    hipLaunchKernelGGL(rx::pair_tile_total_kernel, dim3((unsigned)nt), b256, 0, stream, (const Pair*)a.cnt, n + 1, agg);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = launch_tile_scan(agg, tpre, nt, stream)) != hipSuccess) return e;
+    hipLaunchKernelGGL(rx::pair_scan_apply_kernel, dim3((unsigned)nt), b256, 0, stream, (const Pair*)a.cnt, n + 1,
+                       (const Pair*)tpre, (Pair*)(w + L.pre));
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    u64* nseg = (u64*)(w + L.nseg);
+    hipLaunchKernelGGL(rx::finalize_kernel, dim3(1), dim3(1), 0, stream, (const Pair*)(w + L.pre) + n, msg_off, nmsg,
+                       nseg);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(rx::group_kernel<1>, gq, b256, 0, stream, a);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    const u64 ns = rx::tiles(n);
+    Pair* agg2 = (Pair*)(w + L.agg2);
+    Pair* pre2 = (Pair*)(w + L.pre2);
+    hipLaunchKernelGGL(rx::seg_tile_total_kernel, dim3((unsigned)ns), b256, 0, stream, (const u64*)a.seg_len,
+                       (const u64*)nseg, agg2);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = launch_tile_scan(agg2, pre2, ns, stream)) != hipSuccess) return e;
+    raw::GatherArgs ga{};
+    ga.in = wire;
+    ga.n = n;
+    ga.n_ptr = nseg;
+    ga.lo_ptr = dg_off;
+    ga.hi_ptr = dg_off + n;
+    ga.pre = pre2;
+    ga.seg_src = a.seg_src;
+    ga.seg_len = a.seg_len;
+    ga.out = msg;
+    ga.cap = msg_cap;
+    ga.err = err;
+    return launch_segment_gather(ga, stream);
+}
+
+}  // namespace symhip

@@ -180,6 +180,42 @@ def packetize_leg(codec: Codec, data: torch.Tensor, rec_off: torch.Tensor, dev, 
                     "transport.go:146-201), device-resident, outside the timed region"}
 
 
+def reassembly_leg(codec: Codec, data: torch.Tensor, rec_off: torch.Tensor, dev, reps: int) -> dict:
+    """SURVEY.md 8f N3 beside the headline: the receive side of aRPC's transport (Receive parse +
+    DataReassembler.ProcessFragment) over the packetized batch, datagrams in send order,
+    device-resident, HIP events.  Algorithmic bytes: datagram offsets + every datagram read;
+    message bytes, message offsets / RPCIDs / completing datagrams and a status byte per datagram
+    written."""
+    n = rec_off.numel() - 1
+    rpc = torch.arange(n, dtype=torch.int64, device=dev)
+    dg = codec.fragment(data, rec_off, rpc)
+    torch.cuda.synchronize()
+    codec.check()
+    nd = dg.dg_off.numel() - 1
+    r = codec.reassemble(dg.wire, dg.dg_off)
+    torch.cuda.synchronize()
+    codec.check()
+    k = int(r.nmsg.item())
+    mbytes = int(r.offsets[k].item())
+    ok = k == n and bool(torch.equal(r.data[:mbytes], data[:mbytes]))  # one datagram per record, in order
+    ev = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        codec.reassemble(dg.wire, dg.dg_off)
+        e1.record()
+        ev.append((e0, e1))
+    torch.cuda.synchronize()
+    codec.check()
+    ms = float(np.median([a.elapsed_time(b) for a, b in ev]))
+    wire_b = int(dg.wire.numel())
+    alg = 8 * (nd + 1) + wire_b + mbytes + 8 * (k + 1) + 16 * k + nd
+    return {"datagrams": nd, "messages": k, "wire_bytes": wire_b, "message_bytes": mbytes, "round_trip_ok": ok,
+            "reassemble_ms": round(ms, 4), "alg_bytes": alg, "gbps_algorithmic": round(alg / (ms * 1e-3) / 1e9, 1),
+            "note": "UDPTransport.Receive + DataReassembler.ProcessFragment (pkg/transport/transport.go:253-317, "
+                    "fragmentation.go:49-183) batched; datagrams from sym_fragment_write, send order"}
+
+
 def proxy_leg(codec: Codec, dev, reps: int) -> dict:
     """SURVEY.md 8f N1 beside the headline: the proxy's firewall element (GetScore, shouldBlock, and
     the passing requests compacted into a forwardable batch) and the Raw getters GetScore /
@@ -290,6 +326,7 @@ def main():
     ap.add_argument("--host-steps", type=int, default=5, help="host-inclusive steps (0 = skip)")
     ap.add_argument("--packetize-reps", type=int, default=5, help="packetization leg repetitions (0 = skip)")
     ap.add_argument("--proxy-reps", type=int, default=10, help="firewall / Raw getter leg repetitions (0 = skip)")
+    ap.add_argument("--reassembly-reps", type=int, default=5, help="reassembly leg repetitions (0 = skip)")
     args = ap.parse_args()
 
     world, rank, local = dist_setup()
@@ -432,6 +469,8 @@ def main():
         line["host_inclusive"] = host_inclusive(codec, kw, dev, args.host_steps)
     if world == 1 and args.packetize_reps > 0:
         line["packetize"] = packetize_leg(codec, enc[0][0], enc[0][1], dev, args.packetize_reps)
+    if world == 1 and args.reassembly_reps > 0:
+        line["reassembly"] = reassembly_leg(codec, enc[0][0], enc[0][1], dev, args.reassembly_reps)
     if world == 1 and args.proxy_reps > 0:
         line["proxy"] = proxy_leg(codec, dev, args.proxy_reps)
     if world == 1 and args.cpu_seconds > 0:

@@ -242,6 +242,32 @@ int sym_firewall_filter(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec
                         uint8_t* d_kept, uint64_t kept_cap, uint64_t* d_kept_off, uint64_t* d_kept_index,
                         uint64_t* d_nkept, void* stream);
 
+/* ---- Receive-side reassembly of DataPackets -------------------------------
+ *
+ * Replaces, for n datagrams in arrival order, the per-datagram receive path
+ *   func (t *UDPTransport) Receive(bufferSize, role) ([]byte, *net.UDPAddr, uint64, PacketType, error)
+ *                                      pkg/transport/transport.go:253-317 (parse and route)
+ *   func (c *DataPacketCodec) Deserialize(data []byte) (any, error)
+ *                                      pkg/packet/builtin_packets.go:118-161
+ *   func (r *DataReassembler) ProcessFragment(pkt, addr, buffer) ([]byte, *net.UDPAddr, uint64, bool)
+ *                                      pkg/transport/fragmentation.go:49-183
+ * with the reassembler starting empty.  Input: d_wire + d_dg_off[n+1] (datagram j =
+ * wire[dg_off[j], dg_off[j+1])), e.g. the output of sym_fragment_write.  Output, in the order the
+ * one-at-a-time loop returns them: the completed messages back to back in d_msg (msg_cap bytes;
+ * the batch's payload bytes always suffice, else SYM_ERR_CAPACITY from sym_ctx_check),
+ * d_msg_off[nmsg+1], d_msg_rpc[nmsg] (RPCID) and d_msg_dg[nmsg] (arrival index of the completing
+ * datagram: its header carries the packet type and addresses Receive returns); *d_nmsg; all
+ * arrays sized for n messages (n+1 offsets).  d_status[n]: SYM_RX_*.  n < 2^31. */
+#define SYM_RX_CONSUMED 0   /* part of a returned message */
+#define SYM_RX_PENDING 1    /* still held by the reassembler after the batch */
+#define SYM_RX_NOT_DATA 2   /* not a Request / Response DataPacket: not reassembled */
+#define SYM_RX_TOO_SHORT 3  /* empty, or shorter than the 31-byte DataPacket header */
+#define SYM_RX_BAD_LENGTH 4 /* "data too short for declared payload length" */
+
+int sym_reassemble(sym_ctx* ctx, const uint8_t* d_wire, const uint64_t* d_dg_off, uint64_t n, uint8_t* d_msg,
+                   uint64_t msg_cap, uint64_t* d_msg_off, uint64_t* d_msg_rpc, uint64_t* d_msg_dg, uint64_t* d_nmsg,
+                   uint8_t* d_status, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

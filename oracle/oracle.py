@@ -36,7 +36,8 @@ def build() -> str:
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(_LIB_PATH):
+        srcs = [os.path.join(_HERE, f) for f in os.listdir(_HERE) if f.endswith(".c")]
+        if not os.path.exists(_LIB_PATH) or any(os.path.getmtime(s) > os.path.getmtime(_LIB_PATH) for s in srcs):
             build()
         L = ctypes.CDLL(_LIB_PATH)
         u64, i32, vp = ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p
@@ -248,3 +249,33 @@ def marshal_element_batch(score, strings):
                                              _ptr(out), _ptr(out_off))
     assert got == total, (got, total)
     return out[:total], out_off
+
+
+# ---------------------------------------------------------------- reassembly (reassembly_oracle.c)
+RX_CONSUMED = 0   # part of a returned message
+RX_PENDING = 1    # still held by the reassembler after the batch
+RX_NOT_DATA = 2   # not a Request / Response DataPacket
+RX_TOO_SHORT = 3  # empty or shorter than the 31-byte header
+RX_BAD_LENGTH = 4  # "data too short for declared payload length"
+
+
+def reassemble(wire, dg_off):
+    """DataReassembler over datagrams in arrival order ->
+    (msg u8, msg_off u64 [nmsg+1], msg_rpc u64 [nmsg], msg_dg u64 [nmsg], status u8 [n])."""
+    L = lib()
+    if not getattr(L, "_rx_ready", False):
+        u64, vp = ctypes.c_uint64, ctypes.c_void_p
+        L.sym_oracle_reassemble.restype = u64
+        L.sym_oracle_reassemble.argtypes = [u64, vp, vp, vp, vp, vp, vp, vp]
+        L._rx_ready = True
+    wire = np.ascontiguousarray(wire, dtype=np.uint8)
+    dg_off = np.ascontiguousarray(dg_off, dtype=np.uint64)
+    n = len(dg_off) - 1
+    msg = np.zeros(max(1, wire.size), np.uint8)
+    msg_off = np.zeros(n + 1, np.uint64)
+    rpc = np.zeros(max(1, n), np.uint64)
+    dg = np.zeros(max(1, n), np.uint64)
+    st = np.zeros(max(1, n), np.uint8)
+    k = L.sym_oracle_reassemble(n, _ptr(wire) if wire.size else 0, _ptr(dg_off), _ptr(msg), _ptr(msg_off), _ptr(rpc),
+                                _ptr(dg), _ptr(st))
+    return msg[:int(msg_off[k])], msg_off[:k + 1], rpc[:k], dg[:k], st[:n]

@@ -1,0 +1,227 @@
+"""Receive-side reassembly of DataPackets.
+
+CPU tests pin the oracle (oracle/reassembly_oracle.c) with hand-derived cases read off
+pkg/transport/fragmentation.go:49-183 (duplicates overwrite, the ARRIVING packet's TotalPackets
+decides, fragment indices, RPCID reuse after completion), the parse/routing rules of
+pkg/transport/transport.go:253-317 and pkg/packet/builtin_packets.go:118-161, and round trips through
+the packetizer oracle (the reference has no test of DataReassembler: SURVEY.md 4).
+GPU tests compare the HIP reassembler with the oracle bit-exactly on the same batches, on
+adversarial arrival orders, and on the packetized config-2/3 streams.
+"""
+import struct
+
+import numpy as np
+import pytest
+
+from arpc_amd import datagen
+from oracle import oracle
+
+
+def dgram(rpc, total, seq, payload=b"", more=False, fidx=0, ptype=1, extra=b"", plen=None):
+    """DataPacketCodec.Serialize (builtin_packets.go:59-114) plus optional trailing bytes."""
+    h = struct.pack("<BQHHBB4sH4sHI", ptype, rpc, total, seq, int(more), fidx, b"\x7f\0\0\1", 9000, b"\x7f\0\0\1",
+                    9001, len(payload) if plen is None else plen)
+    assert len(h) == 31
+    return h + payload + extra
+
+
+def batch(dgs):
+    off = np.zeros(len(dgs) + 1, np.uint64)
+    np.cumsum([len(d) for d in dgs], out=off[1:])
+    return np.frombuffer(b"".join(dgs), np.uint8).copy(), off
+
+
+def messages(dgs):
+    msg, off, rpc, dg, st = oracle.reassemble(*batch(dgs))
+    out = [(int(rpc[i]), int(dg[i]), msg[int(off[i]):int(off[i + 1])].tobytes()) for i in range(len(rpc))]
+    return out, list(st)
+
+
+C, P = oracle.RX_CONSUMED, oracle.RX_PENDING
+
+
+# ------------------------------------------------------------------ oracle pinning (CPU)
+def test_oracle_single_and_out_of_order():
+    got, st = messages([dgram(7, 1, 0, b"hello"), dgram(9, 3, 2, b"C"), dgram(9, 3, 0, b"A"), dgram(9, 3, 1, b"B")])
+    assert got == [(7, 0, b"hello"), (9, 3, b"ABC")] and st == [C, C, C, C]
+
+
+def test_oracle_duplicate_overwrites():
+    got, st = messages([dgram(5, 2, 0, b"old"), dgram(5, 2, 0, b"new"), dgram(5, 2, 1, b"!")])
+    assert got == [(5, 2, b"new!")] and st == [C, C, C]
+
+
+def test_oracle_interleaved_completion_order():
+    got, _ = messages([dgram(1, 2, 0, b"a0"), dgram(2, 2, 1, b"b1"), dgram(2, 2, 0, b"b0"), dgram(1, 2, 1, b"a1")])
+    assert got == [(2, 2, b"b0b1"), (1, 3, b"a0a1")]
+
+
+def test_oracle_incomplete_and_extra_sequences():
+    got, st = messages([dgram(3, 3, 0, b"x"), dgram(3, 3, 1, b"y"),               # 2 of 3: pending
+                        dgram(4, 2, 0, b"p"), dgram(4, 2, 5, b"q"), dgram(4, 2, 1, b"r"),  # seq 5 of 2: never
+                        dgram(6, 0, 0, b"z")])                                    # TotalPackets 0: never
+    assert got == [] and st == [P] * 6
+
+
+def test_oracle_arriving_total_decides():
+    got, _ = messages([dgram(8, 3, 0, b"A"), dgram(8, 2, 1, b"B")])
+    assert got == [(8, 1, b"AB")]
+
+
+def test_oracle_fragment_indices():
+    got, _ = messages([dgram(1, 1, 0, b"-second", fidx=1), dgram(1, 1, 0, b"first", more=True, fidx=0),
+                       dgram(2, 1, 0, b"a", more=True), dgram(2, 1, 0, b"b", fidx=2), dgram(2, 1, 0, b"c", fidx=1)])
+    assert got == [(1, 1, b"first-second"), (2, 4, b"acb")]  # index order 0, 1, 2
+    got, st = messages([dgram(3, 1, 0, b"a", more=True), dgram(3, 1, 0, b"c", fidx=2)])  # index 1 missing
+    assert got == [] and st == [P, P]
+
+
+def test_oracle_rpc_reuse_after_completion():
+    got, _ = messages([dgram(4, 1, 0, b"one"), dgram(4, 1, 0, b"two"), dgram(4, 2, 0, b"th"), dgram(4, 2, 1, b"ree")])
+    assert got == [(4, 0, b"one"), (4, 1, b"two"), (4, 3, b"three")]
+
+
+def test_oracle_parse_errors():
+    got, st = messages([b"", dgram(1, 1, 0, b"e", ptype=3), dgram(1, 1, 0, b"u", ptype=9), b"\x01" * 30,
+                        dgram(1, 1, 0, b"short", plen=100), dgram(1, 1, 0, b"ok", extra=b"trailing"),
+                        dgram(2, 1, 0, b"resp", ptype=2)])
+    assert st == [oracle.RX_TOO_SHORT, oracle.RX_NOT_DATA, oracle.RX_NOT_DATA, oracle.RX_TOO_SHORT,
+                  oracle.RX_BAD_LENGTH, C, C]
+    assert got == [(1, 5, b"ok"), (2, 6, b"resp")]
+
+
+def packetized(cfg, n, max_udp_payload=1400):
+    kw = dict(cfg, n=n)
+    b = datagen.make_batch(**kw)
+    stream, off = oracle.encode_batch(b.fixed, b.var, 1, 2)
+    rpc = (np.arange(n, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)) ^ np.uint64(0x1234)
+    wire, dg_off, *_ = oracle.fragment_batch(stream, off, rpc, max_udp_payload=max_udp_payload)
+    return stream, off, rpc, wire, dg_off
+
+
+def shuffled(wire, dg_off, perm):
+    dgs = [wire[int(dg_off[j]):int(dg_off[j + 1])].tobytes() for j in perm]
+    return batch(dgs)
+
+
+@pytest.mark.parametrize("mtu", [1400, 200])
+def test_oracle_round_trip_through_packetizer(mtu):
+    stream, off, rpc, wire, dg_off = packetized(datagen.CONFIG3, 300, mtu)
+    nd = len(dg_off) - 1
+    for perm in (np.arange(nd), np.random.default_rng(1).permutation(nd)):
+        msg, moff, mrpc, mdg, st = oracle.reassemble(*shuffled(wire, dg_off, perm))
+        assert (st == C).all() and len(mrpc) == 300
+        want = {int(rpc[i]): stream[int(off[i]):int(off[i + 1])].tobytes() for i in range(300)}
+        got = {int(mrpc[i]): msg[int(moff[i]):int(moff[i + 1])].tobytes() for i in range(300)}
+        assert got == want
+
+
+def adversarial(n_msgs, seed):
+    """Messages of 1-40 fragments (some with fragment indices), shuffled and interleaved; duplicates,
+    drops, RPCID collisions, wrong totals, corrupt headers."""
+    rng = np.random.default_rng(seed)
+    dgs = []
+    for m in range(n_msgs):
+        rpc = int(rng.integers(0, n_msgs // 3 + 2)) if rng.random() < 0.3 else int(rng.integers(0, 1 << 63))
+        if rng.random() < 0.02:
+            rpc = (1 << 64) - 1  # the hash table's empty key
+        T = int(rng.choice([1, 1, 2, 3, rng.integers(1, 41)]))
+        for s in range(T):
+            nf = 1 if rng.random() < 0.8 else int(rng.integers(1, 4))
+            for f in range(nf):
+                dgs.append(dgram(rpc, T, s, rng.integers(0, 256, int(rng.integers(0, 90)), dtype=np.uint8).tobytes(),
+                                 more=f < nf - 1, fidx=f))
+        if rng.random() < 0.1:
+            dgs.append(dgram(rpc, T, int(rng.integers(0, T + 3)), b"dup"))
+        if rng.random() < 0.05:
+            dgs.append(dgram(rpc, int(rng.integers(0, T + 2)), 0, b"tot"))
+    for _ in range(len(dgs) // 50):
+        dgs.insert(int(rng.integers(0, len(dgs) + 1)),
+                   rng.choice([b"", b"\x03" * 40, b"\x01" * 12, dgram(1, 1, 0, b"x", plen=77)]))
+    order = rng.permutation(len(dgs)) if seed % 2 else np.argsort(rng.random(len(dgs)) + np.arange(len(dgs)) / 20)
+    drop = rng.random(len(dgs)) < 0.03
+    return [dgs[i] for i in order if not drop[i]]
+
+
+def test_oracle_adversarial_is_mixed():
+    got, st = messages(adversarial(400, 3))
+    assert len(got) > 100 and {C, P, oracle.RX_NOT_DATA, oracle.RX_TOO_SHORT, oracle.RX_BAD_LENGTH} <= set(st)
+
+
+# ------------------------------------------------------------------ HIP reassembler (GPU)
+@pytest.fixture(scope="module")
+def gdev():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="module")
+def gcodec(gdev):
+    from arpc_amd.codec import Codec
+    c = Codec(gdev)
+    yield c
+    c.close()
+
+
+def _gpu_vs_oracle(codec, dev, wire, dg_off, misalign=0):
+    import torch
+    want = oracle.reassemble(wire, dg_off)
+    buf = torch.full((wire.size + misalign + 32,), 0xA5, dtype=torch.uint8, device=dev)
+    if wire.size:
+        buf[misalign:misalign + wire.size].copy_(torch.from_numpy(wire))
+    w = buf[misalign:misalign + wire.size]
+    o = torch.from_numpy(dg_off.view(np.int64).copy()).to(dev)
+    r = codec.reassemble(w, o)
+    codec.check()
+    k = int(r.nmsg.item())
+    assert k == len(want[2]), (k, len(want[2]))
+    np.testing.assert_array_equal(r.status.cpu().numpy(), want[4], err_msg="status")
+    np.testing.assert_array_equal(r.offsets[:k + 1].cpu().numpy().view(np.uint64), want[1], err_msg="msg_off")
+    np.testing.assert_array_equal(r.rpc_id[:k].cpu().numpy().view(np.uint64), want[2], err_msg="rpc")
+    np.testing.assert_array_equal(r.dgram[:k].cpu().numpy().view(np.uint64), want[3], err_msg="completing dgram")
+    np.testing.assert_array_equal(r.data[:int(want[1][-1])].cpu().numpy(), want[0], err_msg="message bytes")
+    return want
+
+
+@pytest.mark.gpu
+def test_reassembly_kats_gpu(gcodec, gdev):
+    dgs = [dgram(7, 1, 0, b"hello"), dgram(9, 3, 2, b"C"), dgram(9, 3, 0, b"A"), dgram(9, 3, 1, b"B"),
+           dgram(5, 2, 0, b"old"), dgram(5, 2, 0, b"new"), dgram(5, 2, 1, b"!"), dgram(8, 3, 0, b"A"),
+           dgram(8, 2, 1, b"B"), dgram(1, 1, 0, b"-second", fidx=1), dgram(1, 1, 0, b"first", more=True),
+           dgram(4, 1, 0, b"one"), dgram(4, 1, 0, b"two"), b"", dgram(1, 1, 0, b"e", ptype=3), b"\x01" * 30,
+           dgram(1, 1, 0, b"short", plen=100), dgram(1, 1, 0, b"ok", extra=b"trailing"),
+           dgram(3, 3, 0, b"x"), dgram(6, 0, 0, b"z"), dgram((1 << 64) - 1, 1, 0, b"max")]
+    _gpu_vs_oracle(gcodec, gdev, *batch(dgs), misalign=3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [1, 2, 3, 4])
+def test_reassembly_adversarial_gpu(gcodec, gdev, seed):
+    _gpu_vs_oracle(gcodec, gdev, *batch(adversarial(1500, seed)), misalign=seed)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [0, 1, 255, 256, 257])
+def test_reassembly_edge_counts_gpu(gcodec, gdev, n):
+    rng = np.random.default_rng(n)
+    _gpu_vs_oracle(gcodec, gdev, *batch([dgram(int(rng.integers(0, 40)), int(rng.integers(1, 3)), int(rng.integers(0, 2)),
+                                               b"p" * int(rng.integers(0, 50))) for _ in range(n)]))
+
+
+@pytest.mark.gpu
+def test_reassembly_large_message_gpu(gcodec, gdev):
+    rng = np.random.default_rng(5)
+    dgs = [dgram(77, 3000, s, bytes([s & 255]) * 13) for s in rng.permutation(3000)]
+    want = _gpu_vs_oracle(gcodec, gdev, *batch(dgs))
+    assert len(want[2]) == 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg,mtu", [("config2", 1400), ("config3", 1400), ("config3", 300)])
+def test_reassembly_round_trip_gpu(gcodec, gdev, cfg, mtu):
+    stream, off, rpc, wire, dg_off = packetized(datagen.CONFIG2 if cfg == "config2" else datagen.CONFIG3, 20000, mtu)
+    perm = np.random.default_rng(7).permutation(len(dg_off) - 1)
+    want = _gpu_vs_oracle(gcodec, gdev, *shuffled(wire, dg_off, perm))
+    assert len(want[2]) == 20000 and (want[4] == C).all()
