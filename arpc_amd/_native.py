@@ -59,6 +59,8 @@ SIGNATURES = {
     "sym_firewall_filter": (_int, [_ctx, _u8p, _u64p, _u64, _u32, ctypes.c_int32, _vp, _u8p, _u8p, _u64, _u64p,
                                    _u64p, _u64p, _vp]),
     "sym_reassemble": (_int, [_ctx, _u8p, _u64p, _u64, _u8p, _u64, _u64p, _u64p, _u64p, _u64p, _u8p, _vp]),
+    "sym_encrypt": (_int, [_ctx, _u8p, _u64p, _u64, ctypes.c_char_p, ctypes.c_char_p, _u8p, _u8p, _u64p, _u8p, _vp]),
+    "sym_decrypt": (_int, [_ctx, _u8p, _u64p, _u64, ctypes.c_char_p, ctypes.c_char_p, _u8p, _u64p, _u8p, _vp]),
 }
 
 SYM_MAX_UDP_PAYLOAD = 1400
@@ -82,6 +84,13 @@ SYM_RX_PENDING = 1
 SYM_RX_NOT_DATA = 2
 SYM_RX_TOO_SHORT = 3
 SYM_RX_BAD_LENGTH = 4
+SYM_CRYPT_OK = 0
+SYM_CRYPT_TOO_SHORT = 1
+SYM_CRYPT_BAD_OFFSET = 2
+SYM_CRYPT_AUTH_PUBLIC = 3
+SYM_CRYPT_AUTH_PRIVATE = 4
+SYM_CRYPT_BAD_VERSION = 5
+SYM_GCM_OVERHEAD = 28
 
 
 class Endpoints(ctypes.Structure):

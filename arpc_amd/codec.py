@@ -292,6 +292,61 @@ def _reassemble(codec: "Codec", wire: torch.Tensor, dg_off: torch.Tensor, cap: i
 
 
 Codec.reassemble = _reassemble
+
+
+@dataclass
+class Sealed:
+    data: torch.Tensor     # uint8 [>= offsets[n]]
+    offsets: torch.Tensor  # int64 [n+1]
+    status: torch.Tensor   # uint8 [n]: SYM_CRYPT_*
+
+
+def _check_key(k: bytes, what: str) -> bytes:
+    k = bytes(k)
+    if len(k) != 32:
+        raise ValueError(f"{what}: AES-256 keys are 32 bytes, got {len(k)}")
+    return k
+
+
+def _encrypt(codec: "Codec", data: torch.Tensor, rec_off: torch.Tensor, nonces: torch.Tensor, public_key: bytes,
+             private_key: bytes, stream=None) -> Sealed:
+    """EncryptSymphonyData (pkg/transport/encryption.go:82-171) over n records; nonces: uint8 [n, 24]
+    (public, then private), the random draw of encryption.go:115-121 made an input.  No host sync."""
+    _check_col(data, torch.uint8, "data", codec.device)
+    _check_col(rec_off, torch.int64, "rec_off", codec.device)
+    _check_col(nonces, torch.uint8, "nonces", codec.device)
+    n = rec_off.numel() - 1
+    if nonces.numel() < 24 * n:
+        raise ValueError(f"nonces: need 24 bytes per record ({24 * n}), got {nonces.numel()}")
+    out = torch.empty(max(1, data.numel() + 2 * _native.SYM_GCM_OVERHEAD * n), dtype=torch.uint8, device=codec.device)
+    off = torch.empty(n + 1, dtype=torch.int64, device=codec.device)
+    st = torch.empty(max(1, n), dtype=torch.uint8, device=codec.device)
+    _native.check(codec._lib.sym_encrypt(codec._ctx, _dptr(data) if data.numel() else 1, _dptr(rec_off), n,
+                                        _check_key(public_key, "public_key"), _check_key(private_key, "private_key"),
+                                        _dptr(nonces) if n else 1, _dptr(out), _dptr(off), _dptr(st),
+                                        _stream_handle(codec.device, stream)), "sym_encrypt")
+    return Sealed(out, off, st[:n])
+
+
+def _decrypt(codec: "Codec", data: torch.Tensor, rec_off: torch.Tensor, public_key: bytes, private_key: bytes,
+             stream=None) -> Sealed:
+    """DecryptSymphonyData (pkg/transport/encryption.go:183-256) over n records.  A record that fails
+    authentication keeps its size and is zero-filled; status says why.  No host sync."""
+    _check_col(data, torch.uint8, "data", codec.device)
+    _check_col(rec_off, torch.int64, "rec_off", codec.device)
+    n = rec_off.numel() - 1
+    out = torch.empty(max(1, data.numel()), dtype=torch.uint8, device=codec.device)
+    off = torch.empty(n + 1, dtype=torch.int64, device=codec.device)
+    st = torch.empty(max(1, n), dtype=torch.uint8, device=codec.device)
+    _native.check(codec._lib.sym_decrypt(codec._ctx, _dptr(data) if data.numel() else 1, _dptr(rec_off), n,
+                                        _check_key(public_key, "public_key"), _check_key(private_key, "private_key"),
+                                        _dptr(out), _dptr(off), _dptr(st), _stream_handle(codec.device, stream)),
+                  "sym_decrypt")
+    return Sealed(out, off, st[:n])
+
+
+Codec.encrypt = _encrypt
+Codec.decrypt = _decrypt
 Codec.raw_get_fixed = _raw_get_fixed
 Codec.raw_get_bytes = _raw_get_bytes
 Codec.firewall = _firewall

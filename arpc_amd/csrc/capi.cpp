@@ -35,6 +35,10 @@ struct sym_ctx {
     // and the rocPRIM scan storage (stream-ordered, so calls on one stream share it)
     void* frag = nullptr;
     size_t frag_bytes = 0;
+    // segment cipher: device key schedule + GHASH tables of the last key pair, and that pair
+    void* crypt_tables = nullptr;
+    uint8_t crypt_keys[64] = {0};
+    int num_cus = 0;
 };
 
 namespace {
@@ -182,6 +186,7 @@ int sym_ctx_destroy(sym_ctx* ctx) {
     if (ctx->ws) (void)hipFree(ctx->ws);
     if (ctx->flags) (void)hipFree(ctx->flags);
     if (ctx->frag) (void)hipFree(ctx->frag);
+    if (ctx->crypt_tables) (void)hipFree(ctx->crypt_tables);
     if (ctx->err) (void)hipFree(ctx->err);
     if (ctx->pool) (void)hipFree(ctx->pool);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -653,6 +658,58 @@ int sym_reassemble(sym_ctx* ctx, const uint8_t* d_wire, const uint64_t* d_dg_off
     hipError_t e = symhip::launch_reassemble(d_wire, d_dg_off, n, d_msg, msg_cap, d_msg_off, d_msg_rpc, d_msg_dg, d_nmsg,
                                              d_status, ctx->frag, ctx->err, (hipStream_t)stream);
     return e == hipSuccess ? SYM_OK : hip_fail(e, "reassembly launch");
+}
+
+static int crypt_call(bool enc, sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_off, uint64_t n,
+                      const uint8_t* pub_key, const uint8_t* priv_key, const uint8_t* d_nonces, uint8_t* d_out,
+                      uint64_t* d_out_off, uint8_t* d_status, void* stream) {
+    const char* what = enc ? "sym_encrypt" : "sym_decrypt";
+    if (!ctx) return fail(SYM_ERR_INVALID, "%s: ctx is NULL", what);
+    if (!pub_key || !priv_key) return fail(SYM_ERR_INVALID, "%s: publicKey and privateKey are required", what);
+    if (!d_out_off || (n && (!d_in || !d_rec_off || !d_out || !d_status || (enc && !d_nonces))))
+        return fail(SYM_ERR_INVALID, "%s: NULL argument", what);
+    DeviceGuard g(ctx->device);
+    if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
+    if (n == 0) {
+        hipError_t e = hipMemsetAsync(d_out_off, 0, sizeof(uint64_t), (hipStream_t)stream);
+        return e == hipSuccess ? SYM_OK : hip_fail(e, "hipMemsetAsync");
+    }
+    hipError_t e;
+    if (!ctx->num_cus && (e = hipDeviceGetAttribute(&ctx->num_cus, hipDeviceAttributeMultiprocessorCount,
+                                                    ctx->device)) != hipSuccess)
+        return hip_fail(e, "hipDeviceGetAttribute");
+    const bool same = ctx->crypt_tables && !memcmp(ctx->crypt_keys, pub_key, 32) && !memcmp(ctx->crypt_keys + 32, priv_key, 32);
+    if (!same) {  // key schedule + GHASH tables on the host, once per key pair
+        const size_t tb = symhip::crypt_tables_bytes();
+        if (!ctx->crypt_tables && (e = hipMalloc(&ctx->crypt_tables, tb)) != hipSuccess)
+            return fail(SYM_ERR_NOMEM, "%s: key tables: %s", what, hipGetErrorString(e));
+        void* h = malloc(tb);
+        if (!h) return fail(SYM_ERR_NOMEM, "%s: out of host memory", what);
+        symhip::crypt_build_tables(pub_key, priv_key, h);
+        // stream-ordered behind earlier calls that may still read the old tables
+        if ((e = hipStreamSynchronize((hipStream_t)stream)) == hipSuccess)
+            e = hipMemcpy(ctx->crypt_tables, h, tb, hipMemcpyHostToDevice);
+        free(h);
+        if (e != hipSuccess) return hip_fail(e, "uploading key tables");
+        memcpy(ctx->crypt_keys, pub_key, 32);
+        memcpy(ctx->crypt_keys + 32, priv_key, 32);
+    }
+    const int rc = ensure_scratch(ctx, symhip::crypt_ws_bytes(n), "segment cipher");
+    if (rc != SYM_OK) return rc;
+    e = symhip::launch_crypt(enc, d_in, d_rec_off, n, d_nonces, ctx->crypt_tables, d_out, d_out_off, d_status,
+                             ctx->frag, ctx->num_cus, (hipStream_t)stream);
+    return e == hipSuccess ? SYM_OK : hip_fail(e, what);
+}
+
+int sym_encrypt(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_off, uint64_t n, const uint8_t* pub_key,
+                const uint8_t* priv_key, const uint8_t* d_nonces, uint8_t* d_out, uint64_t* d_out_off,
+                uint8_t* d_status, void* stream) {
+    return crypt_call(true, ctx, d_in, d_rec_off, n, pub_key, priv_key, d_nonces, d_out, d_out_off, d_status, stream);
+}
+
+int sym_decrypt(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_off, uint64_t n, const uint8_t* pub_key,
+                const uint8_t* priv_key, uint8_t* d_out, uint64_t* d_out_off, uint8_t* d_status, void* stream) {
+    return crypt_call(false, ctx, d_in, d_rec_off, n, pub_key, priv_key, nullptr, d_out, d_out_off, d_status, stream);
 }
 
 }  // extern "C"

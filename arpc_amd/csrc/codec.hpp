@@ -124,6 +124,14 @@ struct GatherArgs {
 hipError_t launch_tile_scan(const raw::Pair* agg, raw::Pair* pre, uint64_t ntiles, hipStream_t stream);
 hipError_t launch_segment_gather(const raw::GatherArgs& a, hipStream_t stream);
 
+// ---- per-segment AES-256-GCM (crypto.hip)
+size_t crypt_tables_bytes();
+void crypt_build_tables(const uint8_t pub_key[32], const uint8_t priv_key[32], void* host_tables);
+size_t crypt_ws_bytes(uint64_t n);
+hipError_t launch_crypt(bool enc, const uint8_t* in, const uint64_t* rec_off, uint64_t n, const uint8_t* nonces,
+                        const void* d_tables, uint8_t* out, uint64_t* out_off, uint8_t* status, void* ws, int num_cus,
+                        hipStream_t stream);
+
 // ---- receive-side reassembly (reassemble.hip)
 size_t reassemble_ws_bytes(uint64_t n);
 hipError_t launch_reassemble(const uint8_t* wire, const uint64_t* dg_off, uint64_t n, uint8_t* msg, uint64_t msg_cap,

@@ -268,6 +268,39 @@ int sym_reassemble(sym_ctx* ctx, const uint8_t* d_wire, const uint64_t* d_dg_off
                    uint64_t msg_cap, uint64_t* d_msg_off, uint64_t* d_msg_rpc, uint64_t* d_msg_dg, uint64_t* d_nmsg,
                    uint8_t* d_status, void* stream);
 
+/* ---- Per-segment AES-256-GCM of Symphony records --------------------------
+ *
+ * Replaces, for n records at once,
+ *   func EncryptSymphonyData(data, publicKey, privateKey []byte) []byte
+ *   func DecryptSymphonyData(data, publicKey, privateKey []byte) []byte
+ *                                      pkg/transport/encryption.go:82-256 (segments sealed by
+ *                                      encryptSegmentWithNonce / opened by decryptSegment, :262-335)
+ * The public segment data[13:offsetToPrivate] is sealed under pub_key, the private segment
+ * data[offsetToPrivate:] (version byte included) under priv_key, each as nonce(12) || ciphertext ||
+ * tag(16) (AES-256-GCM, no additional data); offsetToPrivate is rewritten.  Keys are 32 bytes (host
+ * memory); their key schedule and GHASH tables are built on the host and cached in the ctx.
+ *   sym_encrypt  d_nonces: 24 bytes per record (public nonce, then private), device memory -- the
+ *                random nonces of encryption.go:115-121 made an input.  Output record i has
+ *                len + 28 (+ 28 with a private segment) bytes.
+ *   sym_decrypt  output record i has len - 28 (- 28) bytes; a record failing authentication or the
+ *                private version check keeps that size and is zero-filled.
+ * Both: d_out_off[n+1] (output offsets, computed on the device); d_out must hold d_out_off[n]
+ * bytes (<= in bytes + 56 n for sym_encrypt, <= in bytes for sym_decrypt); d_status[n]: SYM_CRYPT_*
+ * (where Go panics on the one message).  A record with a header error has no output. */
+#define SYM_CRYPT_OK 0
+#define SYM_CRYPT_TOO_SHORT 1    /* "too short for header" */
+#define SYM_CRYPT_BAD_OFFSET 2   /* "invalid offsetToPrivate" / "invalid encrypted offsetToPrivate" */
+#define SYM_CRYPT_AUTH_PUBLIC 3  /* public segment: "message authentication failed" */
+#define SYM_CRYPT_AUTH_PRIVATE 4 /* private segment: shorter than nonce + tag, or authentication failed */
+#define SYM_CRYPT_BAD_VERSION 5  /* "invalid decrypted private segment: missing or incorrect version byte" */
+#define SYM_GCM_OVERHEAD 28      /* nonce (12) + tag (16) per segment */
+
+int sym_encrypt(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_off, uint64_t n, const uint8_t* pub_key,
+                const uint8_t* priv_key, const uint8_t* d_nonces, uint8_t* d_out, uint64_t* d_out_off,
+                uint8_t* d_status, void* stream);
+int sym_decrypt(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_off, uint64_t n, const uint8_t* pub_key,
+                const uint8_t* priv_key, uint8_t* d_out, uint64_t* d_out_off, uint8_t* d_status, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
