@@ -28,7 +28,7 @@ namespace crypt {
 
 using raw::Pair;
 
-constexpr int kWaves = 4;
+constexpr int kWaves = 8;  // 512-thread workgroups: one LDS copy of the tables serves 8 waves
 
 // Device tables for one (public, private) key pair; built on the host (build_tables below).
 struct Tables {
@@ -177,25 +177,19 @@ struct Args {
     const Tables* tables;
 };
 
-// One segment's GHASH accumulation over this 64-block window: lanes with `mine` hold block b of
-// the segment, e = one past the segment's last block in the window.
-__device__ inline u32x4 ghash_window(u32x4 y, bool mine, u32x4 cblk_be, u32 b, u32 e, u32 cnt, const Tables& T, int key) {
-    u32x4 c = {0, 0, 0, 0};
-    if (mine) c = gf_mul(cblk_be, T.ghash[key][e - b - 1], T.red);
-    c = wave_xor_u32x4(c);
-    if (cnt == 0) return y;
-    return gf_mul(y, T.ghash[key][cnt - 1], T.red) ^ c;
-}
-
 __device__ inline u32x4 to_be(u32x4 v) { return u32x4{bswap(v.x), bswap(v.y), bswap(v.z), bswap(v.w)}; }
 
-// final GHASH step and tag: (Y xor [0]64 || [8n]64) * H xor E(K, J0), as little-endian words
-__device__ inline u32x4 finish_tag(u32x4 y, u64 nbytes, u32x4 ej0_le, const Tables& T, int key) {
-    const u64 bits = nbytes * 8;
-    y.z ^= (u32)(bits >> 32);
-    y.w ^= (u32)bits;
-    y = gf_mul(y, T.ghash[key][0], T.red);
-    return to_be(y) ^ ej0_le;
+// One 64-slot window of a segment's GHASH.  A segment of nb data blocks has nb + 1 slots: block i
+// (ciphertext) and, last, the length block [0]64 || [8 len]64.  Slot i of a window contributes
+// X_i * H^(e - i), e = one past the segment's last slot in the window, and the length slot adds
+// E(K, J0); the window's terms are XOR-reduced and chained by Horner (Y := Y * H^cnt xor window).
+// A segment that fits one window (63 data blocks) is therefore one parallel multiply per lane and
+// one reduction: no serial GF multiplications.
+__device__ inline u32x4 ghash_fold(u32x4 y, bool first, bool mine, u32x4 term, u32 cnt, const Tables& T, int key) {
+    u32x4 c = mine ? term : u32x4{0, 0, 0, 0};
+    c = wave_xor_u32x4(c);
+    if (cnt == 0) return y;
+    return first ? c : (gf_mul(y, T.ghash[key][cnt - 1], T.red) ^ c);
 }
 
 template <bool ENC>
@@ -242,47 +236,47 @@ __global__ __launch_bounds__(kWaves * 64) void cipher_kernel(Args a) {
         const u32x4 nonce_pub = {ld_le32(non_pub), ld_le32(non_pub + 4), ld_le32(non_pub + 8), 0};
         const u32x4 nonce_priv = priv ? u32x4{ld_le32(non_priv), ld_le32(non_priv + 4), ld_le32(non_priv + 8), 0}
                                       : u32x4{0, 0, 0, 0};
-        const u32 nbp = (u32)((np + 15) / 16), nbv = (u32)((nv + 15) / 16), nb = nbp + nbv;
+        const u32 nbp = (u32)((np + 15) / 16), nbv = (u32)((nv + 15) / 16);
+        const u32 nsp = nbp + 1, nsv = priv ? nbv + 1 : 0, ns = nsp + nsv;  // GHASH slots
         u32x4 y_pub = {0, 0, 0, 0}, y_priv = {0, 0, 0, 0};
         u32 version = 1;  // DEC: first private plaintext byte
-        // ---- pass 1: ENC encrypts, writes ciphertext and hashes it; DEC hashes the ciphertext
-        for (u32 g0 = 0; g0 < nb; g0 += 64) {
-            const u32 g = g0 + lane;
-            const bool act = g < nb, is_priv = g >= nbp;
-            const u32 b = is_priv ? g - nbp : g;
+        // ---- pass 1: ENC encrypts, writes and hashes; DEC hashes the ciphertext (+ private byte 0)
+        for (u32 w0 = 0; w0 < ns; w0 += 64) {
+            const u32 g = w0 + lane;
+            const bool act = g < ns, is_priv = g >= nsp;
+            const u32 i = is_priv ? g - nsp : g;  // slot within the segment
+            const u32 nbs = is_priv ? nbv : nbp;
+            const bool is_len = act && i == nbs, is_data = act && i < nbs;
             const u64 seg_len = is_priv ? nv : np;
-            const int m = act ? (int)min((u64)16, seg_len - 16 * (u64)b) : 0;
-            const uintptr_t src = (is_priv ? src_priv : src_pub) + 16 * (u64)b;
-            const u32x4 x = load_partial(src, m);
+            const int m = is_data ? (int)min((u64)16, seg_len - 16 * (u64)i) : 0;
+            const u32x4 x = load_partial((is_priv ? src_priv : src_pub) + 16 * (u64)i, m);
+            const bool ver = !ENC && is_priv && is_data && i == 0;
+            u32x4 ks = {0, 0, 0, 0};
+            if (is_len || (ENC && is_data) || ver)  // J0 for the tag, J0 + 1 + i for block i
+                ks = aes_block(T.te0, T.rk[is_priv ? 1 : 0],
+                               counter_block(is_priv ? nonce_priv : nonce_pub, is_len ? 1u : i + 2));
             u32x4 c = x;
-            if (ENC || (!ENC && is_priv && b == 0 && act)) {
-                const u32x4 ks = aes_block(T.te0, T.rk[is_priv ? 1 : 0], counter_block(is_priv ? nonce_priv : nonce_pub, b + 2));
-                const u32x4 pm = (x ^ ks) & u32x4{dword_mask(0, m, 0), dword_mask(0, m, 1), dword_mask(0, m, 2),
-                                                  dword_mask(0, m, 3)};
-                if (ENC) {
-                    c = pm;
-                    if (act) store_bytes((is_priv ? dst_priv : dst_pub) + 16 * (u64)b, c, m);
-                } else {
-                    version = pm.x & 0xffu;
-                }
+            if (ENC && is_data) {
+                c = (x ^ ks) & u32x4{dword_mask(0, m, 0), dword_mask(0, m, 1), dword_mask(0, m, 2), dword_mask(0, m, 3)};
+                store_bytes((is_priv ? dst_priv : dst_pub) + 16 * (u64)i, c, m);
             }
-            const u32x4 cbe = to_be(c);
-            const u32 e_pub = min(g0 + 64, nbp), cnt_pub = g0 < nbp ? e_pub - g0 : 0;
-            const u32 s_priv = (g0 > nbp ? g0 : nbp) - nbp, e_priv = min(g0 + 64, nb) - nbp;
-            const u32 cnt_priv = g0 + 64 > nbp ? e_priv - s_priv : 0;
-            y_pub = ghash_window(y_pub, act && !is_priv, cbe, b, e_pub, cnt_pub, T, 0);
-            if (nbv) y_priv = ghash_window(y_priv, act && is_priv, cbe, b, e_priv, cnt_priv, T, 1);
+            if (ver) version = (x.x ^ ks.x) & 0xffu;
+            const u64 bits = seg_len * 8;
+            const u32x4 X = is_len ? u32x4{0, 0, (u32)(bits >> 32), (u32)bits} : to_be(c);
+            const u32 seg_hi = is_priv ? ns : nsp;
+            const u32 e = min(seg_hi, w0 + 64);
+            u32x4 term = {0, 0, 0, 0};
+            if (act) term = gf_mul(X, T.ghash[is_priv ? 1 : 0][e - g - 1], T.red);
+            if (is_len) term ^= to_be(ks);
+            const u32 cnt_pub = w0 < nsp ? min(nsp, w0 + 64) - w0 : 0;
+            y_pub = ghash_fold(y_pub, w0 == 0, act && !is_priv, term, cnt_pub, T, 0);
+            if (nsv) {
+                const u32 lo = w0 > nsp ? w0 : nsp, hi = min(ns, w0 + 64);
+                y_priv = ghash_fold(y_priv, lo == nsp, act && is_priv, term, hi > lo ? hi - lo : 0, T, 1);
+            }
         }
-        if (!ENC) version = (u32)__shfl((int)version, nbp & 63, 64);  // lane holding private block 0
-        // ---- tags: E(K, J0) on lanes 0 / 1
-        u32x4 ej0 = {0, 0, 0, 0};
-        if (lane < 2) ej0 = aes_block(T.te0, T.rk[lane], counter_block(lane ? nonce_priv : nonce_pub, 1));
-        const u32x4 ej0_pub = {(u32)__shfl((int)ej0.x, 0, 64), (u32)__shfl((int)ej0.y, 0, 64),
-                               (u32)__shfl((int)ej0.z, 0, 64), (u32)__shfl((int)ej0.w, 0, 64)};
-        const u32x4 ej0_priv = {(u32)__shfl((int)ej0.x, 1, 64), (u32)__shfl((int)ej0.y, 1, 64),
-                                (u32)__shfl((int)ej0.z, 1, 64), (u32)__shfl((int)ej0.w, 1, 64)};
-        const u32x4 tag_pub = finish_tag(y_pub, np, ej0_pub, T, 0);
-        const u32x4 tag_priv = finish_tag(y_priv, nv, ej0_priv, T, 1);
+        if (!ENC) version = (u32)__shfl((int)version, nsp & 63, 64);  // the lane of private slot 0
+        const u32x4 tag_pub = to_be(y_pub), tag_priv = to_be(y_priv);  // little-endian words
         if (ENC) {
             if (lane == 0) {  // header (offsetToPrivate patched), nonces, tags
                 for (int t = 0; t < 13; ++t) q[t] = ld_u8(d + t);
@@ -313,6 +307,7 @@ __global__ __launch_bounds__(kWaves * 64) void cipher_kernel(Args a) {
             for (u64 t = (u64)lane; t < size; t += 64) q[t] = 0;
             continue;
         }
+        const u32 nb = nbp + nbv;
         for (u32 g0 = 0; g0 < nb; g0 += 64) {
             const u32 g = g0 + lane;
             if (g >= nb) continue;

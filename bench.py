@@ -216,6 +216,48 @@ def reassembly_leg(codec: Codec, data: torch.Tensor, rec_off: torch.Tensor, dev,
                     "fragmentation.go:49-183) batched; datagrams from sym_fragment_write, send order"}
 
 
+def crypto_leg(codec: Codec, data: torch.Tensor, rec_off: torch.Tensor, dev, reps: int) -> dict:
+    """SURVEY.md 8f N4 beside the headline: EncryptSymphonyData / DecryptSymphonyData
+    (pkg/transport/encryption.go:82-256) over the encoded batch with the reference's default keys,
+    device-resident, HIP events.  Algorithmic bytes: records + offsets (+ 24-byte nonces) in, sealed
+    (opened) records + offsets + status out."""
+    n = rec_off.numel() - 1
+    pk = bytes.fromhex("27e1fa17d72b1faf722362deb1974a7675058db98843705124a074c61172f796")
+    vk = bytes.fromhex("9b5300678420678a3157a4bcacdc3e864693971f8a3fab05b06913fb43c7ebf9")
+    g = torch.Generator(device=dev)
+    g.manual_seed(5)
+    nonces = torch.randint(0, 256, (n, 24), dtype=torch.uint8, device=dev, generator=g)
+    sealed = codec.encrypt(data, rec_off, nonces, pk, vk)
+    opened = codec.decrypt(sealed.data, sealed.offsets, pk, vk)
+    torch.cuda.synchronize()
+    codec.check()
+    in_b = int(rec_off[n].item() - rec_off[0].item())
+    enc_b = int(sealed.offsets[n].item())
+    ok = bool((opened.status == 0).all().item()) and bool(torch.equal(opened.data[:in_b], data[:in_b]))
+
+    def timed(fn) -> float:
+        ev = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            ev.append((e0, e1))
+        torch.cuda.synchronize()
+        codec.check()
+        return float(np.median([a.elapsed_time(b) for a, b in ev]))
+
+    enc_ms = timed(lambda: codec.encrypt(data, rec_off, nonces, pk, vk))
+    dec_ms = timed(lambda: codec.decrypt(sealed.data, sealed.offsets, pk, vk))
+    enc_alg = in_b + 8 * (n + 1) + 24 * n + enc_b + 8 * (n + 1) + n
+    dec_alg = enc_b + 8 * (n + 1) + in_b + 8 * (n + 1) + n
+    gbps = lambda a, ms: round(a / (ms * 1e-3) / 1e9, 1)
+    return {"records": n, "plain_bytes": in_b, "sealed_bytes": enc_b, "round_trip_ok": ok,
+            "encrypt_ms": round(enc_ms, 4), "encrypt_gbps": gbps(enc_alg, enc_ms),
+            "decrypt_ms": round(dec_ms, 4), "decrypt_gbps": gbps(dec_alg, dec_ms),
+            "note": "AES-256-GCM per Symphony segment, nonces supplied (encryption.go:115-121 draws them at random)"}
+
+
 def proxy_leg(codec: Codec, dev, reps: int) -> dict:
     """SURVEY.md 8f N1 beside the headline: the proxy's firewall element (GetScore, shouldBlock, and
     the passing requests compacted into a forwardable batch) and the Raw getters GetScore /
@@ -327,6 +369,7 @@ def main():
     ap.add_argument("--packetize-reps", type=int, default=5, help="packetization leg repetitions (0 = skip)")
     ap.add_argument("--proxy-reps", type=int, default=10, help="firewall / Raw getter leg repetitions (0 = skip)")
     ap.add_argument("--reassembly-reps", type=int, default=5, help="reassembly leg repetitions (0 = skip)")
+    ap.add_argument("--crypto-reps", type=int, default=3, help="segment cipher leg repetitions (0 = skip)")
     args = ap.parse_args()
 
     world, rank, local = dist_setup()
@@ -471,6 +514,8 @@ def main():
         line["packetize"] = packetize_leg(codec, enc[0][0], enc[0][1], dev, args.packetize_reps)
     if world == 1 and args.reassembly_reps > 0:
         line["reassembly"] = reassembly_leg(codec, enc[0][0], enc[0][1], dev, args.reassembly_reps)
+    if world == 1 and args.crypto_reps > 0:
+        line["crypto"] = crypto_leg(codec, enc[0][0], enc[0][1], dev, args.crypto_reps)
     if world == 1 and args.proxy_reps > 0:
         line["proxy"] = proxy_leg(codec, dev, args.proxy_reps)
     if world == 1 and args.cpu_seconds > 0:
