@@ -185,13 +185,160 @@ __device__ inline u32x4 to_be(u32x4 v) { return u32x4{bswap(v.x), bswap(v.y), bs
 // E(K, J0); the window's terms are XOR-reduced and chained by Horner (Y := Y * H^cnt xor window).
 // A segment that fits one window (63 data blocks) is therefore one parallel multiply per lane and
 // one reduction: no serial GF multiplications.
+template <int W>
+__device__ inline u32x4 subwave_xor_u32x4(u32x4 v) {
+#pragma unroll
+    for (int d = W / 2; d > 0; d >>= 1) {
+        v.x ^= (u32)__shfl_xor((int)v.x, d, 64);
+        v.y ^= (u32)__shfl_xor((int)v.y, d, 64);
+        v.z ^= (u32)__shfl_xor((int)v.z, d, 64);
+        v.w ^= (u32)__shfl_xor((int)v.w, d, 64);
+    }
+    return v;
+}
+
+template <int W>
 __device__ inline u32x4 ghash_fold(u32x4 y, bool first, bool mine, u32x4 term, u32 cnt, const Tables& T, int key) {
     u32x4 c = mine ? term : u32x4{0, 0, 0, 0};
-    c = wave_xor_u32x4(c);
+    c = subwave_xor_u32x4<W>(c);
     if (cnt == 0) return y;
     return first ? c : (gf_mul(y, T.ghash[key][cnt - 1], T.red) ^ c);
 }
 
+// GHASH slots of record r (data blocks + one length block per segment), 0 when it has no work
+__device__ inline u32 record_slots(const Args& a, u64 r, bool enc) {
+    if (r >= a.n || a.status[r] != SYM_CRYPT_OK) return 0;
+    const u64 s = a.rec_off[r], L = a.rec_off[r + 1] - s;
+    const u64 o = ld_u32((uintptr_t)(a.in + s) + 1);
+    const u64 np = enc ? o - 13 : o - 41, nv = o < L ? (enc ? L - o : L - o - 28) : 0;
+    return (u32)((np + 15) / 16 + 1 + (o < L ? (nv + 15) / 16 + 1 : 0));
+}
+
+// One record on a sub-wave of W lanes (sl = lane within it).  W = 32 packs two records per wave.
+template <bool ENC, int W>
+__device__ void seal_or_open(const Args& a, const Tables& T, u64 r, int sl) {
+    const u64 s = a.rec_off[r], L = a.rec_off[r + 1] - s;
+    const uintptr_t d = (uintptr_t)(a.in + s);
+    const u64 o = ld_u32(d + 1);
+    uint8_t* const q = a.out + a.out_off[r];
+    const bool priv = o < L;
+    // segment geometry: plaintext/ciphertext source, length, destination, nonce
+    u64 np, nv;
+    uintptr_t src_pub, src_priv, non_pub, non_priv;
+    uint8_t *dst_pub, *dst_priv;
+    if (ENC) {
+        np = o - 13;
+        nv = priv ? L - o : 0;
+        src_pub = d + 13;
+        src_priv = d + o;
+        non_pub = (uintptr_t)(a.nonces + 24 * r);
+        non_priv = non_pub + 12;
+        dst_pub = q + 25;
+        dst_priv = q + 13 + 28 + np + 12;
+    } else {
+        np = o - 41;
+        nv = priv ? L - o - 28 : 0;
+        src_pub = d + 25;
+        src_priv = d + o + 12;
+        non_pub = d + 13;
+        non_priv = d + o;
+        dst_pub = q + 13;
+        dst_priv = q + 13 + np;
+    }
+    const u32x4 nonce_pub = {ld_le32(non_pub), ld_le32(non_pub + 4), ld_le32(non_pub + 8), 0};
+    const u32x4 nonce_priv = priv ? u32x4{ld_le32(non_priv), ld_le32(non_priv + 4), ld_le32(non_priv + 8), 0}
+                                  : u32x4{0, 0, 0, 0};
+    const u32 nbp = (u32)((np + 15) / 16), nbv = (u32)((nv + 15) / 16);
+    const u32 nsp = nbp + 1, nsv = priv ? nbv + 1 : 0, ns = nsp + nsv;  // GHASH slots
+    u32x4 y_pub = {0, 0, 0, 0}, y_priv = {0, 0, 0, 0};
+    u32 version = 1;  // DEC: first private plaintext byte
+    // ---- pass 1: ENC encrypts, writes and hashes; DEC hashes the ciphertext (+ private byte 0)
+    for (u32 w0 = 0; w0 < ns; w0 += W) {
+        const u32 g = w0 + sl;
+        const bool act = g < ns, is_priv = g >= nsp;
+        const u32 i = is_priv ? g - nsp : g;  // slot within the segment
+        const u32 nbs = is_priv ? nbv : nbp;
+        const bool is_len = act && i == nbs, is_data = act && i < nbs;
+        const u64 seg_len = is_priv ? nv : np;
+        const int m = is_data ? (int)min((u64)16, seg_len - 16 * (u64)i) : 0;
+        const u32x4 x = load_partial((is_priv ? src_priv : src_pub) + 16 * (u64)i, m);
+        const bool ver = !ENC && is_priv && is_data && i == 0;
+        u32x4 ks = {0, 0, 0, 0};
+        if (is_len || (ENC && is_data) || ver)  // J0 for the tag, J0 + 1 + i for block i
+            ks = aes_block(T.te0, T.rk[is_priv ? 1 : 0],
+                           counter_block(is_priv ? nonce_priv : nonce_pub, is_len ? 1u : i + 2));
+        u32x4 c = x;
+        if (ENC && is_data) {
+            c = (x ^ ks) & u32x4{dword_mask(0, m, 0), dword_mask(0, m, 1), dword_mask(0, m, 2), dword_mask(0, m, 3)};
+            store_bytes((is_priv ? dst_priv : dst_pub) + 16 * (u64)i, c, m);
+        }
+        if (ver) version = (x.x ^ ks.x) & 0xffu;
+        const u64 bits = seg_len * 8;
+        const u32x4 X = is_len ? u32x4{0, 0, (u32)(bits >> 32), (u32)bits} : to_be(c);
+        const u32 e = min(is_priv ? ns : nsp, w0 + W);
+        u32x4 term = {0, 0, 0, 0};
+        if (act) term = gf_mul(X, T.ghash[is_priv ? 1 : 0][e - g - 1], T.red);
+        if (is_len) term ^= to_be(ks);
+        const u32 cnt_pub = w0 < nsp ? min(nsp, w0 + W) - w0 : 0;
+        y_pub = ghash_fold<W>(y_pub, w0 == 0, act && !is_priv, term, cnt_pub, T, 0);
+        if (nsv) {
+            const u32 lo = w0 > nsp ? w0 : nsp, hi = min(ns, w0 + W);
+            y_priv = ghash_fold<W>(y_priv, lo == nsp, act && is_priv, term, hi > lo ? hi - lo : 0, T, 1);
+        }
+    }
+    if (!ENC) version = (u32)__shfl((int)version, (int)(nsp & (W - 1)), W);  // the lane of private slot 0
+    const u32x4 tag_pub = to_be(y_pub), tag_priv = to_be(y_priv);  // little-endian words
+    if (ENC) {
+        if (sl == 0) {  // header (offsetToPrivate patched), nonces, tags
+            for (int t = 0; t < 13; ++t) q[t] = ld_u8(d + t);
+            const u32 no = (u32)(13 + 28 + np);
+            for (int t = 0; t < 4; ++t) q[1 + t] = (uint8_t)(no >> (8 * t));
+            for (int t = 0; t < 12; ++t) q[13 + t] = ld_u8(non_pub + t);
+            store_bytes(q + 25 + np, tag_pub, 16);
+            if (priv) {
+                uint8_t* p2 = q + 41 + np;
+                for (int t = 0; t < 12; ++t) p2[t] = ld_u8(non_priv + t);
+                store_bytes(p2 + 12 + nv, tag_priv, 16);
+            }
+        }
+        return;
+    }
+    // ---- DEC: authenticate, then decrypt (or zero the record's output)
+    auto tag_at = [&](uintptr_t p) { return u32x4{ld_le32(p), ld_le32(p + 4), ld_le32(p + 8), ld_le32(p + 12)}; };
+    const u32x4 want_pub = tag_at(d + o - 16);
+    const u32x4 want_priv = priv ? tag_at(d + L - 16) : u32x4{0, 0, 0, 0};
+    uint8_t st = SYM_CRYPT_OK;
+    const u32x4 dp = want_pub ^ tag_pub, dv = want_priv ^ tag_priv;
+    if (dp.x | dp.y | dp.z | dp.w) st = SYM_CRYPT_AUTH_PUBLIC;
+    else if (priv && (dv.x | dv.y | dv.z | dv.w)) st = SYM_CRYPT_AUTH_PRIVATE;
+    else if (priv && (nv < 1 || version != 1)) st = SYM_CRYPT_BAD_VERSION;
+    const u64 size = 13 + np + nv;
+    if (st != SYM_CRYPT_OK) {
+        if (sl == 0) a.status[r] = st;
+        for (u64 t = (u64)sl; t < size; t += W) q[t] = 0;
+        return;
+    }
+    const u32 nb = nbp + nbv;
+    for (u32 g0 = 0; g0 < nb; g0 += W) {
+        const u32 g = g0 + sl;
+        if (g >= nb) continue;
+        const bool is_priv = g >= nbp;
+        const u32 b = is_priv ? g - nbp : g;
+        const u64 seg_len = is_priv ? nv : np;
+        const int m = (int)min((u64)16, seg_len - 16 * (u64)b);
+        const u32x4 x = load_partial((is_priv ? src_priv : src_pub) + 16 * (u64)b, m);
+        const u32x4 ks = aes_block(T.te0, T.rk[is_priv ? 1 : 0], counter_block(is_priv ? nonce_priv : nonce_pub, b + 2));
+        store_bytes((is_priv ? dst_priv : dst_pub) + 16 * (u64)b, x ^ ks, m);
+    }
+    if (sl == 0) {
+        for (int t = 0; t < 13; ++t) q[t] = ld_u8(d + t);
+        const u32 no = (u32)(13 + np);
+        for (int t = 0; t < 4; ++t) q[1 + t] = (uint8_t)(no >> (8 * t));
+    }
+}
+
+// A wave takes records in pairs: when both fit 32 GHASH slots (records under ~450 bytes) each half
+// of the wave seals one of them; otherwise the whole wave takes them one after the other.
 template <bool ENC>
 __global__ __launch_bounds__(kWaves * 64) void cipher_kernel(Args a) {
     __shared__ Tables T;
@@ -203,126 +350,16 @@ __global__ __launch_bounds__(kWaves * 64) void cipher_kernel(Args a) {
     __syncthreads();
     const int lane = threadIdx.x & 63;
     const u64 nw = (u64)gridDim.x * kWaves;
-    for (u64 r = (u64)blockIdx.x * kWaves + (threadIdx.x >> 6); r < a.n; r += nw) {  // wave-uniform
-        if (a.status[r] != SYM_CRYPT_OK) continue;
-        const u64 s = a.rec_off[r], L = a.rec_off[r + 1] - s;
-        const uintptr_t d = (uintptr_t)(a.in + s);
-        const u64 o = ld_u32(d + 1);
-        uint8_t* const q = a.out + a.out_off[r];
-        const bool priv = o < L;
-        // segment geometry: plaintext/ciphertext source, length, destination, nonce
-        u64 np, nv;
-        uintptr_t src_pub, src_priv, non_pub, non_priv;
-        uint8_t *dst_pub, *dst_priv;
-        if (ENC) {
-            np = o - 13;
-            nv = priv ? L - o : 0;
-            src_pub = d + 13;
-            src_priv = d + o;
-            non_pub = (uintptr_t)(a.nonces + 24 * r);
-            non_priv = non_pub + 12;
-            dst_pub = q + 25;
-            dst_priv = q + 13 + 28 + np + 12;
+    const u64 npairs = (a.n + 1) / 2;
+    for (u64 p = (u64)blockIdx.x * kWaves + (threadIdx.x >> 6); p < npairs; p += nw) {  // wave-uniform
+        const u64 r0 = 2 * p, r1 = 2 * p + 1;
+        const u32 s0 = record_slots(a, r0, ENC), s1 = record_slots(a, r1, ENC);  // uniform
+        if (s0 <= 32 && s1 <= 32) {
+            const u64 r = lane < 32 ? r0 : r1;
+            if ((lane < 32 ? s0 : s1) != 0) seal_or_open<ENC, 32>(a, T, r, lane & 31);
         } else {
-            np = o - 41;
-            nv = priv ? L - o - 28 : 0;
-            src_pub = d + 25;
-            src_priv = d + o + 12;
-            non_pub = d + 13;
-            non_priv = d + o;
-            dst_pub = q + 13;
-            dst_priv = q + 13 + np;
-        }
-        const u32x4 nonce_pub = {ld_le32(non_pub), ld_le32(non_pub + 4), ld_le32(non_pub + 8), 0};
-        const u32x4 nonce_priv = priv ? u32x4{ld_le32(non_priv), ld_le32(non_priv + 4), ld_le32(non_priv + 8), 0}
-                                      : u32x4{0, 0, 0, 0};
-        const u32 nbp = (u32)((np + 15) / 16), nbv = (u32)((nv + 15) / 16);
-        const u32 nsp = nbp + 1, nsv = priv ? nbv + 1 : 0, ns = nsp + nsv;  // GHASH slots
-        u32x4 y_pub = {0, 0, 0, 0}, y_priv = {0, 0, 0, 0};
-        u32 version = 1;  // DEC: first private plaintext byte
-        // ---- pass 1: ENC encrypts, writes and hashes; DEC hashes the ciphertext (+ private byte 0)
-        for (u32 w0 = 0; w0 < ns; w0 += 64) {
-            const u32 g = w0 + lane;
-            const bool act = g < ns, is_priv = g >= nsp;
-            const u32 i = is_priv ? g - nsp : g;  // slot within the segment
-            const u32 nbs = is_priv ? nbv : nbp;
-            const bool is_len = act && i == nbs, is_data = act && i < nbs;
-            const u64 seg_len = is_priv ? nv : np;
-            const int m = is_data ? (int)min((u64)16, seg_len - 16 * (u64)i) : 0;
-            const u32x4 x = load_partial((is_priv ? src_priv : src_pub) + 16 * (u64)i, m);
-            const bool ver = !ENC && is_priv && is_data && i == 0;
-            u32x4 ks = {0, 0, 0, 0};
-            if (is_len || (ENC && is_data) || ver)  // J0 for the tag, J0 + 1 + i for block i
-                ks = aes_block(T.te0, T.rk[is_priv ? 1 : 0],
-                               counter_block(is_priv ? nonce_priv : nonce_pub, is_len ? 1u : i + 2));
-            u32x4 c = x;
-            if (ENC && is_data) {
-                c = (x ^ ks) & u32x4{dword_mask(0, m, 0), dword_mask(0, m, 1), dword_mask(0, m, 2), dword_mask(0, m, 3)};
-                store_bytes((is_priv ? dst_priv : dst_pub) + 16 * (u64)i, c, m);
-            }
-            if (ver) version = (x.x ^ ks.x) & 0xffu;
-            const u64 bits = seg_len * 8;
-            const u32x4 X = is_len ? u32x4{0, 0, (u32)(bits >> 32), (u32)bits} : to_be(c);
-            const u32 seg_hi = is_priv ? ns : nsp;
-            const u32 e = min(seg_hi, w0 + 64);
-            u32x4 term = {0, 0, 0, 0};
-            if (act) term = gf_mul(X, T.ghash[is_priv ? 1 : 0][e - g - 1], T.red);
-            if (is_len) term ^= to_be(ks);
-            const u32 cnt_pub = w0 < nsp ? min(nsp, w0 + 64) - w0 : 0;
-            y_pub = ghash_fold(y_pub, w0 == 0, act && !is_priv, term, cnt_pub, T, 0);
-            if (nsv) {
-                const u32 lo = w0 > nsp ? w0 : nsp, hi = min(ns, w0 + 64);
-                y_priv = ghash_fold(y_priv, lo == nsp, act && is_priv, term, hi > lo ? hi - lo : 0, T, 1);
-            }
-        }
-        if (!ENC) version = (u32)__shfl((int)version, nsp & 63, 64);  // the lane of private slot 0
-        const u32x4 tag_pub = to_be(y_pub), tag_priv = to_be(y_priv);  // little-endian words
-        if (ENC) {
-            if (lane == 0) {  // header (offsetToPrivate patched), nonces, tags
-                for (int t = 0; t < 13; ++t) q[t] = ld_u8(d + t);
-                const u32 no = (u32)(13 + 28 + np);
-                for (int t = 0; t < 4; ++t) q[1 + t] = (uint8_t)(no >> (8 * t));
-                for (int t = 0; t < 12; ++t) q[13 + t] = ld_u8(non_pub + t);
-                store_bytes(q + 25 + np, tag_pub, 16);
-                if (priv) {
-                    uint8_t* p2 = q + 41 + np;
-                    for (int t = 0; t < 12; ++t) p2[t] = ld_u8(non_priv + t);
-                    store_bytes(p2 + 12 + nv, tag_priv, 16);
-                }
-            }
-            continue;
-        }
-        // ---- DEC: authenticate, then decrypt (or zero the record's output)
-        auto tag_at = [&](uintptr_t p) { return u32x4{ld_le32(p), ld_le32(p + 4), ld_le32(p + 8), ld_le32(p + 12)}; };
-        const u32x4 want_pub = tag_at(d + o - 16);
-        const u32x4 want_priv = priv ? tag_at(d + L - 16) : u32x4{0, 0, 0, 0};
-        uint8_t st = SYM_CRYPT_OK;
-        const u32x4 dp = want_pub ^ tag_pub, dv = want_priv ^ tag_priv;
-        if (dp.x | dp.y | dp.z | dp.w) st = SYM_CRYPT_AUTH_PUBLIC;
-        else if (priv && (dv.x | dv.y | dv.z | dv.w)) st = SYM_CRYPT_AUTH_PRIVATE;
-        else if (priv && (nv < 1 || version != 1)) st = SYM_CRYPT_BAD_VERSION;
-        const u64 size = 13 + np + nv;
-        if (st != SYM_CRYPT_OK) {
-            if (lane == 0) a.status[r] = st;
-            for (u64 t = (u64)lane; t < size; t += 64) q[t] = 0;
-            continue;
-        }
-        const u32 nb = nbp + nbv;
-        for (u32 g0 = 0; g0 < nb; g0 += 64) {
-            const u32 g = g0 + lane;
-            if (g >= nb) continue;
-            const bool is_priv = g >= nbp;
-            const u32 b = is_priv ? g - nbp : g;
-            const u64 seg_len = is_priv ? nv : np;
-            const int m = (int)min((u64)16, seg_len - 16 * (u64)b);
-            const u32x4 x = load_partial((is_priv ? src_priv : src_pub) + 16 * (u64)b, m);
-            const u32x4 ks = aes_block(T.te0, T.rk[is_priv ? 1 : 0], counter_block(is_priv ? nonce_priv : nonce_pub, b + 2));
-            store_bytes((is_priv ? dst_priv : dst_pub) + 16 * (u64)b, x ^ ks, m);
-        }
-        if (lane == 0) {
-            for (int t = 0; t < 13; ++t) q[t] = ld_u8(d + t);
-            const u32 no = (u32)(13 + np);
-            for (int t = 0; t < 4; ++t) q[1 + t] = (uint8_t)(no >> (8 * t));
+            if (s0) seal_or_open<ENC, 64>(a, T, r0, lane);
+            if (s1) seal_or_open<ENC, 64>(a, T, r1, lane);
         }
     }
 }
