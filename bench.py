@@ -362,6 +362,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--overlap", type=int, default=0,
+                    help="1: encode and decode of a step on two HIP streams (independent buffer sets), overlapped")
     ap.add_argument("--config", type=int, default=2, choices=(2, 3))
     ap.add_argument("--records", type=int, default=0, help="records per GPU (default: the config's 2^20)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
@@ -401,7 +403,42 @@ def main():
 
     ev = {"enc": [], "dec": []}
 
+    s_enc = torch.cuda.current_stream(dev)
+    s_dec = torch.cuda.Stream(dev) if args.overlap else s_enc
+    enc_done: list = [None] * NSETS  # event: last encode into enc[k] finished
+    dec_done: list = [None] * NSETS  # event: last decode reading enc[k] finished
+
+    def step_overlap(i: int, timed: bool):
+        """Encode set a on one stream while set d (encoded two steps earlier) decodes on another:
+        the same work as step(), with the cross-stream hazards made explicit by events."""
+        a, d = i % NSETS, (i + 2) % NSETS
+        fx, vr = sets[a]
+        if dec_done[a] is not None:
+            s_enc.wait_event(dec_done[a])  # enc[a] is free once its previous decode is done
+        if enc_done[d] is not None:
+            s_dec.wait_event(enc_done[d])  # enc[d] is complete
+        if timed:
+            e0, e1, e2, e3 = (torch.cuda.Event(enable_timing=True) for _ in range(4))
+            e0.record(s_enc)
+        codec.encode(s, fx, vr, out=enc[a][0], out_off=enc[a][1], stream=s_enc)
+        ea = torch.cuda.Event()
+        ea.record(s_enc)
+        enc_done[a] = ea
+        if timed:
+            e1.record(s_enc)
+            e2.record(s_dec)
+        codec.decode(s, enc[d][0], enc[d][1], outputs=dec[d], stream=s_dec)
+        ed = torch.cuda.Event()
+        ed.record(s_dec)
+        dec_done[d] = ed
+        if timed:
+            e3.record(s_dec)
+            ev["enc"].append((e0, e1))
+            ev["dec"].append((e2, e3))
+
     def step(i: int, timed: bool):
+        if args.overlap:
+            return step_overlap(i, timed)
         a, d = i % NSETS, (i + 2) % NSETS
         fx, vr = sets[a]
         if timed:
@@ -419,6 +456,7 @@ def main():
     for k in range(NSETS):  # every set encoded once before any decode reads it
         fx, vr = sets[k]
         codec.encode(s, fx, vr, out=enc[k][0], out_off=enc[k][1])
+    torch.cuda.synchronize()
     for i in range(args.warmup):
         step(i, False)
     codec.check()
@@ -491,7 +529,7 @@ def main():
         "config": {"workload": ("config2: kv-store SetRequest K=64 B, V=256 B" if args.config == 2 else
                                 "config3: kv-store SetRequest K=64 B, V log-uniform 16-4096 B")
                    + ", device-resident encode+decode",
-                   "records_per_gpu": n, "global_records": n * world, "parallelism": f"shard{world}",
+                   "records_per_gpu": n, "global_records": n * world, "parallelism": f"shard{world}", "streams": 2 if args.overlap else 1,
                    "bytes_per_record_algorithmic": round((enc_b + dec_b) / n, 3)},
         "mrecords_per_s": round(world * 2 * n * args.steps / elapsed / 1e6, 2),
         "wire_gbps": round(world * 2 * total * args.steps / elapsed / 1e9, 2),
