@@ -81,10 +81,13 @@ __device__ inline void frag_of(const Layout& l, u64 M, u64 d, u64& start, u64& l
     }
 }
 
-// The datagram holding wire byte q (>= 0) of the record's datagram sequence.
+// q / D for q < 2^31 (tile positions are 32-bit) and D < 2^32: a 32-bit division, not a 64-bit one.
+__device__ inline u64 div_small(u64 q, u64 D) { return (u64)((u32)q / (u32)D); }
+
+// The datagram holding wire byte q (>= 0, < 2^31) of the record's datagram sequence.
 __device__ inline u64 dgram_at(const Layout& l, u64 M, u64 q) {
     const u64 D = M + kHdr, A = l.kpub * D;
-    if (q < A) return q / D;
+    if (q < A) return div_small(q, D);
     q -= A;
     if (l.nmeet >= 1) {
         if (q < l.meet0 + kHdr) return l.kpub;
@@ -94,7 +97,7 @@ __device__ inline u64 dgram_at(const Layout& l, u64 M, u64 q) {
         if (q < l.meet1 + kHdr) return l.kpub + 1;
         q -= l.meet1 + kHdr;
     }
-    const u64 d = l.kpub + l.nmeet + q / D;
+    const u64 d = l.kpub + l.nmeet + div_small(q, D);
     return d < l.npk ? d : l.npk - 1;
 }
 
@@ -230,9 +233,9 @@ __global__ __launch_bounds__(kWaves * 64) void frag_write_kernel(WriteParams p) 
         if (27 - b > -4 && 27 - b < 16) or_u32_at((u32)flen, 27 - b, t);           // PayloadLen
         return u32x4{t[0], t[1], t[2], t[3]};
     };
-    for (int B = firstc; B < span; B += 16 * 64) {  // wave-uniform loop
-        const int P = B + 16 * lane;
-        if (P >= span) continue;
+    // the wire chunk at tile position P (aligned 16 bytes): header bytes from the templates, payload
+    // bytes from one byte-unaligned load
+    auto chunk = [&](int P) -> u32x4 {
         const int k = lds_search_64(S.o, cnt, max(P, 0));
         const Layout l{S.kpub[k], S.nmeet[k], S.meet0[k], S.meet1[k], S.npk[k]};
         const i64 q = (i64)P - S.o[k];  // >= -15
@@ -272,8 +275,24 @@ __global__ __launch_bounds__(kWaves * 64) void frag_write_kernel(WriteParams p) 
                 r |= header_window(k2, (int)(end - q) * -1, d2, fl2);
             }
         }
-        const u32 rr[4] = {r.x, r.y, r.z, r.w};
-        store_chunk(out_t, P, 0, span, rr);
+        return r;
+    };
+    // kU chunks per lane per step: every load of the step is issued before its stores
+    constexpr int kU = 4;
+    for (int B = firstc; B < span; B += 16 * 64 * kU) {  // wave-uniform loop
+        u32x4 r[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int P = B + 16 * 64 * u + 16 * lane;
+            r[u] = P < span ? chunk(P) : u32x4{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int P = B + 16 * 64 * u + 16 * lane;
+            if (P >= span) continue;
+            const u32 rr[4] = {r[u].x, r[u].y, r[u].z, r[u].w};
+            store_chunk(out_t, P, 0, span, rr);
+        }
     }
 }
 
