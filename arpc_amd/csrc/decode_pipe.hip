@@ -185,10 +185,10 @@ __device__ void parser(const DecodeParams& p, u64* aw, u64 ntiles, u32 epoch, u3
 // Each step loads the aggregate words of the next 1024 tiles, finds the first tile whose word is not
 // yet published (the frontier), and publishes the exclusive prefix of every tile before it.  A
 // tile's prefix so depends only on earlier tiles, whoever published their aggregates.
-template <int NV, typename LdsT>
+template <int NV, int SK, typename LdsT>
 __device__ void scanner(u64* aw, u64* pw, u64 ntiles, u32 epoch, unsigned* err, LdsT& S) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    constexpr int kPer = 4;  // tiles per thread per step
+    constexpr int kPer = SK;  // tiles per thread per step
     constexpr u64 kStep = (u64)kThreads * kPer;
     u64 carry[NV];
 #pragma unroll
@@ -263,7 +263,7 @@ __device__ void scanner(u64* aw, u64* pw, u64 ntiles, u32 epoch, unsigned* err, 
 // MODE 0: the pipeline.  MODE 1: copiers only, every prefix taken as 0 (timing of the data movement
 // alone; wrong output -- tools/kbench.py variant 402).  DIAG: per-tile phase timestamps into p.dbg
 // (8 u64 per tile, s_memrealtime at 100 MHz; tools/fused_timeline.py).
-template <int NF, int NV, int MODE = 0, int DIAG = 0>
+template <int NF, int NV, int MODE = 0, int DIAG = 0, int SK = 4>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))) void decode_pipe_kernel(
     DecodeParams p, u64* flags, u32 epoch) {
     static_assert(NV == 1 || NV == 2, "decode handles one or two string columns");
@@ -284,7 +284,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
         return;
     }
     if (MODE == 0 && blockIdx.x == P) {
-        scanner<NV>(aw, pw, ntiles, epoch, p.err, S);
+        scanner<NV, SK>(aw, pw, ntiles, epoch, p.err, S);
         return;
     }
     const u64 tile = MODE == 0 ? blockIdx.x - P - 1 : blockIdx.x;
@@ -520,8 +520,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
         if (tid == 0) p.dbg[tile * 8 + 5] = blockIdx.x;
 }
 
-template <int NF, int NV, int MODE, int DIAG>
-hipError_t launch(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stream) {
+template <int NF, int NV, int MODE, int DIAG, int SK = 4>
+hipError_t launch(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stream, int pnum = 1, int pden = 1) {
     if (DIAG && !p.dbg) return hipErrorInvalidValue;  // timestamps need SYMHIP_DEBUG_PTR
     static int cus[16] = {0};
     int dev = 0;
@@ -530,21 +530,25 @@ hipError_t launch(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stre
     int& ncu = cus[dev & 15];
     if (ncu == 0 && (e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
     const u64 nt = num_tiles(p.n);
-    u64 P = MODE == 0 ? (u64)ncu : 0;  // one parser workgroup per CU
+    u64 P = MODE == 0 ? (u64)ncu * pnum / pden : 0;  // one parser workgroup per CU (tuning: pnum / pden)
     if (P > (nt + 3) / 4) P = (nt + 3) / 4;
     DecodeParams q = p;
     q.pipe_parsers = (unsigned)P;
     const u64 grid = MODE == 0 ? P + 1 + nt : nt;
-    hipLaunchKernelGGL((decode_pipe_kernel<NF, NV, MODE, DIAG>), dim3((unsigned)grid), dim3(kThreads), 0, stream, q,
-                       flags, epoch);
+    hipLaunchKernelGGL((decode_pipe_kernel<NF, NV, MODE, DIAG, SK>), dim3((unsigned)grid), dim3(kThreads), 0, stream,
+                       q, flags, epoch);
     return hipGetLastError();
 }
 
-template <int MODE, int DIAG>
-hipError_t launch_layout(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stream) {
-    if (p.lay.nfixed == 0 && p.lay.nvar == 1) return launch<0, 1, MODE, DIAG>(p, flags, epoch, stream);
-    if (p.lay.nfixed == 0 && p.lay.nvar == 2) return launch<0, 2, MODE, DIAG>(p, flags, epoch, stream);
-    if (p.lay.nfixed == 2 && p.lay.nvar == 2) return launch<2, 2, MODE, DIAG>(p, flags, epoch, stream);
+constexpr int kScanPer = 2;      // scanner tiles per thread per step (512-tile steps)
+constexpr int kParsersNum = 3;   // parser workgroups = #CUs * 3/4
+constexpr int kParsersDen = 4;
+
+template <int MODE, int DIAG, int SK = kScanPer>
+hipError_t launch_layout(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stream, int pnum = 1, int pden = 1) {
+    if (p.lay.nfixed == 0 && p.lay.nvar == 1) return launch<0, 1, MODE, DIAG, SK>(p, flags, epoch, stream, pnum, pden);
+    if (p.lay.nfixed == 0 && p.lay.nvar == 2) return launch<0, 2, MODE, DIAG, SK>(p, flags, epoch, stream, pnum, pden);
+    if (p.lay.nfixed == 2 && p.lay.nvar == 2) return launch<2, 2, MODE, DIAG, SK>(p, flags, epoch, stream, pnum, pden);
     return hipErrorInvalidValue;
 }
 
@@ -561,9 +565,27 @@ hipError_t launch_decode_pipe(const DecodeParams& p, void* flags, unsigned epoch
     u64* fl = (u64*)flags;
     switch (p.variant) {
         case 402: return pipe::launch_layout<1, 0>(p, fl, epoch, stream);
-        case 410: return pipe::launch_layout<0, 1>(p, fl, epoch, stream);
+        case 410: return pipe::launch_layout<0, 1>(p, fl, epoch, stream, pipe::kParsersNum, pipe::kParsersDen);
         case 412: return pipe::launch_layout<1, 1>(p, fl, epoch, stream);
-        default: return pipe::launch_layout<0, 0>(p, fl, epoch, stream);
+        // tuning experiments (tools/kbench.py): parser count and scanner step size
+        case 431: return pipe::launch_layout<0, 0>(p, fl, epoch, stream, 1, 2);
+        case 432: return pipe::launch_layout<0, 0>(p, fl, epoch, stream, 2, 1);
+        case 433: return pipe::launch_layout<0, 0>(p, fl, epoch, stream, 1, 4);
+        case 434: return pipe::launch_layout<0, 0>(p, fl, epoch, stream, 3, 2);
+        case 435: return pipe::launch_layout<0, 0>(p, fl, epoch, stream, 3, 4);
+        case 440: return pipe::launch_layout<0, 0, 8>(p, fl, epoch, stream);
+        case 442: return pipe::launch_layout<0, 0, 2>(p, fl, epoch, stream);
+        case 443: return pipe::launch_layout<0, 0, 1>(p, fl, epoch, stream);
+        case 444: return pipe::launch_layout<0, 0, 2>(p, fl, epoch, stream, 3, 4);
+        case 445: return pipe::launch_layout<0, 0, 2>(p, fl, epoch, stream, 7, 8);
+        case 446: return pipe::launch_layout<0, 0, 3>(p, fl, epoch, stream);
+        case 447: return pipe::launch_layout<0, 0, 2>(p, fl, epoch, stream, 5, 8);
+        case 448: return pipe::launch_layout<0, 0, 2>(p, fl, epoch, stream, 9, 16);
+        case 449: return pipe::launch_layout<0, 0, 2>(p, fl, epoch, stream, 11, 16);
+        case 450: return pipe::launch_layout<0, 0, 2>(p, fl, epoch, stream, 1, 2);
+        case 430: return pipe::launch_layout<0, 0, 4>(p, fl, epoch, stream, 1, 1);  // round-1 tuning
+        // default: 512-tile scanner steps, parsers on 3/4 of the CUs (tools/kbench.py sweep)
+        default: return pipe::launch_layout<0, 0, pipe::kScanPer>(p, fl, epoch, stream, pipe::kParsersNum, pipe::kParsersDen);
     }
 }
 

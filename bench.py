@@ -506,7 +506,7 @@ def main():
     if enc_ms >= dec_ms:
         kname, dom_ms, dom_bytes = f"encode_kernel<{s.nfixed}, {s.nvar}, 0>", enc_ms, enc_b
     else:
-        kname, dom_ms, dom_bytes = f"decode_pipe_kernel<{s.nfixed}, {s.nvar}, 0, 0>", dec_ms, dec_b
+        kname, dom_ms, dom_bytes = f"decode_pipe_kernel<{s.nfixed}, {s.nvar}, 0, 0, 2>", dec_ms, dec_b
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     traffic = load_traffic(kname)
 
@@ -537,7 +537,7 @@ def main():
                                "gbps": round(enc_b / enc_ms / 1e6, 1)},
                     "decode": {"avg_ms": round(dec_ms, 4), "alg_bytes": dec_b,
                                "gbps": round(dec_b / dec_ms / 1e6, 1),
-                               "kernel": f"decode_pipe_kernel<{s.nfixed}, {s.nvar}, 0, 0>",
+                               "kernel": f"decode_pipe_kernel<{s.nfixed}, {s.nvar}, 0, 0, 2>",
                                "three_kernel_ms": round(three_ms, 4),
                                "three_kernel_gbps": round(dec_b / three_ms / 1e6, 1),
                                "movement_only_ms": round(move_ms, 4),
