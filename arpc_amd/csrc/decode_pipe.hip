@@ -263,7 +263,7 @@ __device__ void scanner(u64* aw, u64* pw, u64 ntiles, u32 epoch, unsigned* err, 
 // MODE 0: the pipeline.  MODE 1: copiers only, every prefix taken as 0 (timing of the data movement
 // alone; wrong output -- tools/kbench.py variant 402).  DIAG: per-tile phase timestamps into p.dbg
 // (8 u64 per tile, s_memrealtime at 100 MHz; tools/fused_timeline.py).
-template <int NF, int NV, int MODE = 0, int DIAG = 0, int SK = 4>
+template <int NF, int NV, int MODE = 0, int DIAG = 0, int SK = 4, int PR = 2>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))) void decode_pipe_kernel(
     DecodeParams p, u64* flags, u32 epoch) {
     static_assert(NV == 1 || NV == 2, "decode handles one or two string columns");
@@ -280,7 +280,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
 
     const u32 P = p.pipe_parsers;
     if (MODE == 0 && blockIdx.x < P) {
-        parser<NF, NV>(p, aw, ntiles, epoch, P);
+        parser<NF, NV, PR>(p, aw, ntiles, epoch, P);
         return;
     }
     if (MODE == 0 && blockIdx.x == P) {
@@ -520,7 +520,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
         if (tid == 0) p.dbg[tile * 8 + 5] = blockIdx.x;
 }
 
-template <int NF, int NV, int MODE, int DIAG, int SK = 4>
+template <int NF, int NV, int MODE, int DIAG, int SK = 4, int PR = 2>
 hipError_t launch(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stream, int pnum = 1, int pden = 1) {
     if (DIAG && !p.dbg) return hipErrorInvalidValue;  // timestamps need SYMHIP_DEBUG_PTR
     static int cus[16] = {0};
@@ -535,7 +535,7 @@ hipError_t launch(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stre
     DecodeParams q = p;
     q.pipe_parsers = (unsigned)P;
     const u64 grid = MODE == 0 ? P + 1 + nt : nt;
-    hipLaunchKernelGGL((decode_pipe_kernel<NF, NV, MODE, DIAG, SK>), dim3((unsigned)grid), dim3(kThreads), 0, stream,
+    hipLaunchKernelGGL((decode_pipe_kernel<NF, NV, MODE, DIAG, SK, PR>), dim3((unsigned)grid), dim3(kThreads), 0, stream,
                        q, flags, epoch);
     return hipGetLastError();
 }
@@ -544,11 +544,11 @@ constexpr int kScanPer = 2;      // scanner tiles per thread per step (512-tile 
 constexpr int kParsersNum = 3;   // parser workgroups = #CUs * 3/4
 constexpr int kParsersDen = 4;
 
-template <int MODE, int DIAG, int SK = kScanPer>
+template <int MODE, int DIAG, int SK = kScanPer, int PR = 2>
 hipError_t launch_layout(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stream, int pnum = 1, int pden = 1) {
-    if (p.lay.nfixed == 0 && p.lay.nvar == 1) return launch<0, 1, MODE, DIAG, SK>(p, flags, epoch, stream, pnum, pden);
-    if (p.lay.nfixed == 0 && p.lay.nvar == 2) return launch<0, 2, MODE, DIAG, SK>(p, flags, epoch, stream, pnum, pden);
-    if (p.lay.nfixed == 2 && p.lay.nvar == 2) return launch<2, 2, MODE, DIAG, SK>(p, flags, epoch, stream, pnum, pden);
+    if (p.lay.nfixed == 0 && p.lay.nvar == 1) return launch<0, 1, MODE, DIAG, SK, PR>(p, flags, epoch, stream, pnum, pden);
+    if (p.lay.nfixed == 0 && p.lay.nvar == 2) return launch<0, 2, MODE, DIAG, SK, PR>(p, flags, epoch, stream, pnum, pden);
+    if (p.lay.nfixed == 2 && p.lay.nvar == 2) return launch<2, 2, MODE, DIAG, SK, PR>(p, flags, epoch, stream, pnum, pden);
     return hipErrorInvalidValue;
 }
 
@@ -583,6 +583,10 @@ hipError_t launch_decode_pipe(const DecodeParams& p, void* flags, unsigned epoch
         case 448: return pipe::launch_layout<0, 0, 2>(p, fl, epoch, stream, 9, 16);
         case 449: return pipe::launch_layout<0, 0, 2>(p, fl, epoch, stream, 11, 16);
         case 450: return pipe::launch_layout<0, 0, 2>(p, fl, epoch, stream, 1, 2);
+        case 460: return pipe::launch_layout<0, 0, 2, 1>(p, fl, epoch, stream, 3, 4);
+        case 461: return pipe::launch_layout<0, 0, 2, 4>(p, fl, epoch, stream, 3, 4);
+        case 462: return pipe::launch_layout<0, 0, 2, 1>(p, fl, epoch, stream, 3, 2);
+        case 463: return pipe::launch_layout<0, 0, 2, 4>(p, fl, epoch, stream, 3, 8);
         case 430: return pipe::launch_layout<0, 0, 4>(p, fl, epoch, stream, 1, 1);  // round-1 tuning
         // default: 512-tile scanner steps, parsers on 3/4 of the CUs (tools/kbench.py sweep)
         default: return pipe::launch_layout<0, 0, pipe::kScanPer>(p, fl, epoch, stream, pipe::kParsersNum, pipe::kParsersDen);
