@@ -9,8 +9,10 @@
 // The reassembler keeps one state per RPCID and its decisions for one RPCID depend only on that
 // RPCID's datagrams in arrival order, so the batch is regrouped rather than replayed:
 //  1. parse (thread per datagram): header checks, and the RPCID inserted into an open-addressing
-//     hash table whose slot index becomes a dense group key;
-//  2. a stable radix sort (rocPRIM) of (group key, arrival index) on only the key's ~log2(2n) bits:
+//     hash table (agent-scope CAS) that also keeps each RPCID's first arrival (atomicMin); that
+//     first arrival index is the group key, so groups sort in order of first appearance and an
+//     in-order stream keeps its arrival order through every later pass (coalesced);
+//  2. a stable radix sort (rocPRIM) of (group key, arrival index) on ~log2(n)+1 key bits:
 //     each group becomes a contiguous run in arrival order;
 //  3. group pass (thread per group): the ProcessFragment state machine over the group's run, with
 //     per-sequence state (fragment-index bitmap, last index, latest index-0 fragment) in a scratch
@@ -37,7 +39,8 @@ namespace rx {
 using raw::Pair;
 
 constexpr int kHdr = 31;        // DataPacket header (builtin_packets.go:68)
-constexpr u64 kEmpty = ~0ull;   // free hash slot; an RPCID equal to it gets the group key `special`
+constexpr u64 kEmpty = ~0ull;   // free hash slot; an RPCID equal to it gets the table slot `special`
+constexpr u32 kNoSlot = ~0u;    // slot of a datagram that is not a DataPacket
 
 struct SeqState {    // one sequence number of the group's current message
     u32 bits[8];     // fragment indices received (0..255)
@@ -66,7 +69,9 @@ struct Args {
     u64 n;
     u64* table;
     u64 tmask;
-    u32 special, nodata;   // group keys: RPCID == kEmpty, not a DataPacket
+    u32 special, nodata;   // table slot of the RPCID == kEmpty; group key of non-DataPackets (= n)
+    u32* first;            // per table slot (+1 for `special`): the RPCID's first arrival index
+    u32* slot;             // per datagram: its RPCID's table slot
     u64* rpc;
     u64* meta;
     u32* plen;
@@ -94,7 +99,7 @@ __global__ __launch_bounds__(256) void parse_kernel(Args a) {
     const u64 s = a.dg_off[i], L = a.dg_off[i + 1] - s;
     const uintptr_t p = (uintptr_t)(a.wire + s);
     uint8_t st = SYM_RX_PENDING;
-    u32 g = a.nodata;
+    u32 g = kNoSlot;  // table slot
     if (L < 1) {
         st = SYM_RX_TOO_SHORT;                       // "data too short to read packet type"
     } else if (const u32 t = ld_u8(p); t != 1 && t != 2) {
@@ -126,8 +131,18 @@ __global__ __launch_bounds__(256) void parse_kernel(Args a) {
         }
     }
     a.status[i] = st;
-    a.gid[i] = g;
+    a.slot[i] = g;
+    if (g != kNoSlot) atomicMin(&a.first[g], (u32)i);
     a.idx[i] = (u32)i;
+}
+
+// ---- 1b. group key = the RPCID's first arrival: groups sort in order of first appearance, so an
+// in-order stream keeps its arrival order and every later pass reads and writes it coalesced
+__global__ __launch_bounds__(256) void key_kernel(Args a) {
+    const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.n) return;
+    const u32 s = a.slot[i];
+    a.gid[i] = s == kNoSlot ? a.nodata : a.first[s];
 }
 
 __device__ inline bool seq_complete(const SeqState& x) {
@@ -149,7 +164,7 @@ __global__ __launch_bounds__(256) void group_kernel(Args a) {
     const u64 q0 = (u64)blockIdx.x * 256 + threadIdx.x;
     if (q0 >= a.n) return;
     const u32 g = a.gs[q0];
-    if (g > a.special) return;                   // not a DataPacket (sorted last)
+    if (g == a.nodata) return;                   // not a DataPacket (sorted last)
     if (q0 > 0 && a.gs[q0 - 1] == g) return;     // not the first of its group
     u64 e = q0 + 1;
     while (e < a.n && a.gs[e] == g) ++e;
@@ -292,10 +307,11 @@ inline unsigned log2u(u64 t) {
     while (((u64)1 << b) < t) ++b;
     return b;
 }
+inline unsigned key_bits(u64 n) { return log2u(n + 1) + 1; }  // keys in [0, n]
 
 struct Layout {
-    size_t table, rpc, meta, plen, gid, idx, gs, is, state, cnt, pre, agg, tpre, seg_src, seg_len, agg2, pre2, nseg,
-        temp, total;
+    size_t table, first, slot, rpc, meta, plen, gid, idx, gs, is, state, cnt, pre, agg, tpre, seg_src, seg_len, agg2,
+        pre2, nseg, temp, total;
     size_t temp_bytes;
 };
 
@@ -309,6 +325,8 @@ inline Layout layout(u64 n) {
     };
     const u64 TS = table_size(n);
     L.table = take(TS * 8);
+    L.first = take((TS + 1) * 4);
+    L.slot = take(n * 4);
     L.rpc = take(n * 8);
     L.meta = take(n * 8);
     L.plen = take(n * 4);
@@ -328,7 +346,7 @@ inline Layout layout(u64 n) {
     L.nseg = take(8);
     size_t tb = 0;
     (void)rocprim::radix_sort_pairs(nullptr, tb, (const u32*)nullptr, (u32*)nullptr, (const u32*)nullptr,
-                                    (u32*)nullptr, (size_t)n, 0u, log2u(TS) + 1);
+                                    (u32*)nullptr, (size_t)n, 0u, key_bits(n));
     L.temp_bytes = al256(tb);
     L.temp = take(L.temp_bytes);
     L.total = o;
@@ -353,7 +371,9 @@ hipError_t launch_reassemble(const uint8_t* wire, const u64* dg_off, u64 n, uint
     a.table = (u64*)(w + L.table);
     a.tmask = TS - 1;
     a.special = (u32)TS;
-    a.nodata = (u32)TS + 1;
+    a.nodata = (u32)n;
+    a.first = (u32*)(w + L.first);
+    a.slot = (u32*)(w + L.slot);
     a.rpc = (u64*)(w + L.rpc);
     a.meta = (u64*)(w + L.meta);
     a.plen = (u32*)(w + L.plen);
@@ -372,12 +392,15 @@ hipError_t launch_reassemble(const uint8_t* wire, const u64* dg_off, u64 n, uint
     a.seg_len = (u64*)(w + L.seg_len);
     const dim3 b256(256);
     hipError_t e = hipMemsetAsync(a.table, 0xff, TS * 8, stream);
+    if (e == hipSuccess) e = hipMemsetAsync(a.first, 0xff, (TS + 1) * 4, stream);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(rx::parse_kernel, dim3((unsigned)rx::tiles(n + 1)), b256, 0, stream, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(rx::key_kernel, dim3((unsigned)rx::tiles(n)), b256, 0, stream, a);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
     size_t tb = L.temp_bytes;
     e = rocprim::radix_sort_pairs(w + L.temp, tb, (const u32*)a.gid, (u32*)(w + L.gs), (const u32*)a.idx,
-                                  (u32*)(w + L.is), (size_t)n, 0u, rx::log2u(TS) + 1, stream);
+                                  (u32*)(w + L.is), (size_t)n, 0u, rx::key_bits(n), stream);
     if (e != hipSuccess) return e;
     const dim3 gq((unsigned)rx::tiles(n));
     hipLaunchKernelGGL(rx::group_kernel<0>, gq, b256, 0, stream, a);
