@@ -59,6 +59,9 @@ SIGNATURES = {
     "sym_firewall_filter": (_int, [_ctx, _u8p, _u64p, _u64, _u32, ctypes.c_int32, _vp, _u8p, _u8p, _u64, _u64p,
                                    _u64p, _u64p, _vp]),
     "sym_reassemble": (_int, [_ctx, _u8p, _u64p, _u64, _u8p, _u64, _u64p, _u64p, _u64p, _u64p, _u8p, _vp]),
+    "sym_flat_encoded_size": (_u64, [_vp, _int, _u64, _u64]),
+    "sym_flat_encode": (_int, [_ctx, _vp, _int, _u64, _vp, _vp, _u32, _u32, _u8p, _u64p, _vp]),
+    "sym_flat_decode": (_int, [_ctx, _vp, _int, _u64, _u8p, _u64p, _vp, _vp, _vp, _u8p, _vp]),
     "sym_encrypt": (_int, [_ctx, _u8p, _u64p, _u64, ctypes.c_char_p, ctypes.c_char_p, _u8p, _u8p, _u64p, _u8p, _vp]),
     "sym_decrypt": (_int, [_ctx, _u8p, _u64p, _u64, ctypes.c_char_p, ctypes.c_char_p, _u8p, _u64p, _u8p, _vp]),
 }
@@ -91,6 +94,14 @@ SYM_CRYPT_AUTH_PUBLIC = 3
 SYM_CRYPT_AUTH_PRIVATE = 4
 SYM_CRYPT_BAD_VERSION = 5
 SYM_GCM_OVERHEAD = 28
+
+
+SYM_MAX_FLAT_FIELDS = 16
+
+
+class SymField(ctypes.Structure):
+    """struct sym_field (include/symphony_hip.h)."""
+    _fields_ = [("segment", ctypes.c_uint8), ("width", ctypes.c_uint8)]
 
 
 class Endpoints(ctypes.Structure):

@@ -660,6 +660,74 @@ int sym_reassemble(sym_ctx* ctx, const uint8_t* d_wire, const uint64_t* d_dg_off
     return e == hipSuccess ? SYM_OK : hip_fail(e, "reassembly launch");
 }
 
+static int flat_check(const char* what, const sym_field* fields, int nf) {
+    if (nf < 0 || nf > SYM_MAX_FLAT_FIELDS || (nf && !fields))
+        return fail(SYM_ERR_INVALID, "%s: %d fields (0..%d)", what, nf, SYM_MAX_FLAT_FIELDS);
+    for (int k = 0; k < nf; ++k) {
+        if (fields[k].segment > 1) return fail(SYM_ERR_INVALID, "%s: field %d segment %u", what, k, fields[k].segment);
+        const unsigned w = fields[k].width;
+        if (w != 0 && w != 1 && w != 4 && w != 8) return fail(SYM_ERR_INVALID, "%s: field %d width %u", what, k, w);
+    }
+    return SYM_OK;
+}
+
+uint64_t sym_flat_encoded_size(const sym_field* fields, int nfields, uint64_t n, uint64_t var_total) {
+    if (nfields == 0) return 14 * n;
+    uint64_t per = 13 + 1;
+    for (int k = 0; k < nfields; ++k) per += fields[k].width ? fields[k].width : 8;  // table entry + length prefix
+    return per * n + var_total;
+}
+
+int sym_flat_encode(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const void* const* d_cols,
+                    const uint64_t* const* d_offs, uint32_t service_id, uint32_t method_id, uint8_t* d_out,
+                    uint64_t* d_out_off, void* stream) {
+    if (!ctx) return fail(SYM_ERR_INVALID, "sym_flat_encode: ctx is NULL");
+    int rc = flat_check("sym_flat_encode", fields, nfields);
+    if (rc != SYM_OK) return rc;
+    if (!d_out_off || (n && (!d_out || (nfields && (!d_cols || !d_offs)))))
+        return fail(SYM_ERR_INVALID, "sym_flat_encode: NULL argument");
+    for (int k = 0; k < nfields && n; ++k)
+        if (!d_cols[k] || (!fields[k].width && !d_offs[k]))
+            return fail(SYM_ERR_INVALID, "sym_flat_encode: field %d has no column", k);
+    DeviceGuard g(ctx->device);
+    if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
+    if (n == 0) {
+        hipError_t e = hipMemsetAsync(d_out_off, 0, sizeof(uint64_t), (hipStream_t)stream);
+        return e == hipSuccess ? SYM_OK : hip_fail(e, "hipMemsetAsync");
+    }
+    if ((rc = ensure_scratch(ctx, symhip::flat_ws_bytes(fields, nfields, n), "flat encode")) != SYM_OK) return rc;
+    hipError_t e = symhip::launch_flat_encode(fields, nfields, n, d_cols, d_offs, service_id, method_id, d_out,
+                                              d_out_off, ctx->frag, (hipStream_t)stream);
+    return e == hipSuccess ? SYM_OK : hip_fail(e, "flat encode launch");
+}
+
+int sym_flat_decode(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const uint8_t* d_in,
+                    const uint64_t* d_rec_off, void* const* d_cols, const uint64_t* caps, uint64_t* const* d_offs,
+                    uint8_t* d_status, void* stream) {
+    if (!ctx) return fail(SYM_ERR_INVALID, "sym_flat_decode: ctx is NULL");
+    int rc = flat_check("sym_flat_decode", fields, nfields);
+    if (rc != SYM_OK) return rc;
+    if (n && (!d_in || !d_rec_off || !d_status || (nfields && (!d_cols || !caps || !d_offs))))
+        return fail(SYM_ERR_INVALID, "sym_flat_decode: NULL argument");
+    for (int k = 0; k < nfields; ++k)
+        if ((n && !d_cols[k] && (fields[k].width || caps[k])) || (!fields[k].width && !d_offs[k]))
+            return fail(SYM_ERR_INVALID, "sym_flat_decode: field %d has no column", k);
+    DeviceGuard g(ctx->device);
+    if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
+    if (n == 0) {
+        for (int k = 0; k < nfields; ++k)
+            if (!fields[k].width) {
+                hipError_t e = hipMemsetAsync(d_offs[k], 0, sizeof(uint64_t), (hipStream_t)stream);
+                if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync");
+            }
+        return SYM_OK;
+    }
+    if ((rc = ensure_scratch(ctx, symhip::flat_ws_bytes(fields, nfields, n), "flat decode")) != SYM_OK) return rc;
+    hipError_t e = symhip::launch_flat_decode(fields, nfields, n, d_in, d_rec_off, d_cols, caps, d_offs, d_status,
+                                              ctx->frag, ctx->err, (hipStream_t)stream);
+    return e == hipSuccess ? SYM_OK : hip_fail(e, "flat decode launch");
+}
+
 static int crypt_call(bool enc, sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_off, uint64_t n,
                       const uint8_t* pub_key, const uint8_t* priv_key, const uint8_t* d_nonces, uint8_t* d_out,
                       uint64_t* d_out_off, uint8_t* d_status, void* stream) {

@@ -124,6 +124,18 @@ struct GatherArgs {
 hipError_t launch_tile_scan(const raw::Pair* agg, raw::Pair* pre, uint64_t ntiles, hipStream_t stream);
 hipError_t launch_segment_gather(const raw::GatherArgs& a, hipStream_t stream);
 
+// ---- any flat schema (flat.hip); sym_field is defined in include/symphony_hip.h
+}  // namespace symhip
+struct sym_field;
+namespace symhip {
+size_t flat_ws_bytes(const sym_field* f, int nf, uint64_t n);
+hipError_t launch_flat_encode(const sym_field* f, int nf, uint64_t n, const void* const* cols,
+                              const uint64_t* const* offs, uint32_t sid, uint32_t mid, uint8_t* out,
+                              uint64_t* out_off, void* ws, hipStream_t stream);
+hipError_t launch_flat_decode(const sym_field* f, int nf, uint64_t n, const uint8_t* in, const uint64_t* rec_off,
+                              void* const* cols, const uint64_t* caps, uint64_t* const* offs, uint8_t* status,
+                              void* ws, unsigned* err, hipStream_t stream);
+
 // ---- per-segment AES-256-GCM (crypto.hip)
 size_t crypt_tables_bytes();
 void crypt_build_tables(const uint8_t pub_key[32], const uint8_t priv_key[32], void* host_tables);

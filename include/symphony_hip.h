@@ -301,6 +301,37 @@ int sym_encrypt(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_off, ui
 int sym_decrypt(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_off, uint64_t n, const uint8_t* pub_key,
                 const uint8_t* priv_key, uint8_t* d_out, uint64_t* d_out_off, uint8_t* d_status, void* stream);
 
+/* ---- Any flat schema (the flat part) ----------------------------------------
+ *
+ * The generated MarshalSymphony / UnmarshalSymphony of a message whose fields are fixed-width or
+ * string / bytes, each public or private (generator cmd/symphony-gen-arpc/protoc-gen-symphony/
+ * main.go:196-368, 439-620 marshal; :622-800 unmarshal), described at run time: fields[k] in
+ * declaration order, `segment` SYM_SEGMENT_PUBLIC / SYM_SEGMENT_PRIVATE, `width` 1 (bool),
+ * 4 (int32 / uint32 / float / enum), 8 (int64 / uint64 / double) or 0 (string / bytes).
+ * Repeated and nested fields are not covered.  Columns are indexed by field: d_cols[k] is n
+ * little-endian values of `width` bytes (fixed) or the packed bytes (string, with d_offs[k] its
+ * n+1 offsets; d_offs[k] is ignored for fixed fields).  The kv-store and echo schemas above are the
+ * all-private cases of this (and keep their specialised kernels).
+ *   sym_flat_encode  output record i = MarshalSymphony + the client's ID patch; d_out holds
+ *                    sym_flat_encoded_size(...) bytes; d_out_off[n+1] computed on the device.
+ *   sym_flat_decode  UnmarshalSymphony into fresh structs: fixed columns (zero when not read),
+ *                    string columns of caps[k] bytes (rec_off[n] - rec_off[0] always suffices)
+ *                    with d_offs[k][n+1]; d_status[n] SYM_STATUS_*. */
+#define SYM_MAX_FLAT_FIELDS 16
+
+typedef struct sym_field {
+    uint8_t segment; /* SYM_SEGMENT_PUBLIC / SYM_SEGMENT_PRIVATE */
+    uint8_t width;   /* 1, 4, 8, or 0 for string / bytes */
+} sym_field;
+
+uint64_t sym_flat_encoded_size(const sym_field* fields, int nfields, uint64_t n, uint64_t var_total);
+int sym_flat_encode(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const void* const* d_cols,
+                    const uint64_t* const* d_offs, uint32_t service_id, uint32_t method_id, uint8_t* d_out,
+                    uint64_t* d_out_off, void* stream);
+int sym_flat_decode(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const uint8_t* d_in,
+                    const uint64_t* d_rec_off, void* const* d_cols, const uint64_t* caps, uint64_t* const* d_offs,
+                    uint8_t* d_status, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

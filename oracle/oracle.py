@@ -336,3 +336,79 @@ def decrypt_batch(data, rec_off, pub_key=DEFAULT_PUBLIC_KEY, priv_key=DEFAULT_PR
     st = np.zeros(max(1, n), np.uint8)
     _crypto_lib().sym_oracle_decrypt_batch(n, dp, _ptr(rec_off), pub_key, priv_key, _ptr(out), _ptr(off), _ptr(st))
     return out[:int(off[n])], off, st[:n]
+
+
+# ---------------------------------------------------------------- flat schemas (flat_oracle.c)
+class _Field(ctypes.Structure):
+    _fields_ = [("segment", ctypes.c_uint8), ("width", ctypes.c_uint8)]
+
+
+def _flat_lib():
+    L = lib()
+    if not getattr(L, "_flat_ready", False):
+        u64, u32, i32, vp = ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p
+        L.sym_oracle_flat_encode.restype = u64
+        L.sym_oracle_flat_encode.argtypes = [i32, vp, u64, vp, vp, vp, u32, u32, vp, vp]
+        L.sym_oracle_flat_decode.restype = None
+        L.sym_oracle_flat_decode.argtypes = [i32, vp, u64, vp, vp, vp, vp, vp, vp]
+        L._flat_ready = True
+    return L
+
+
+def _fields(fields):
+    arr = (_Field * max(1, len(fields)))()
+    for k, (seg, w) in enumerate(fields):
+        arr[k].segment, arr[k].width = seg, w
+    return arr
+
+
+def flat_encode(fields, cols, n: int, service_id: int = 0, method_id: int = 0):
+    """fields: [(segment 0/1, width 1/4/8 or 0 = string)]; cols[k]: numpy array of n values (fixed,
+    any dtype of that width) or (bytes u8, offs u64 [n+1]) (string).  -> (out u8, out_off u64)."""
+    L = _flat_lib()
+    fx, vb, vo, keep = [], [], [], []
+    total = (14 if not fields else 0) * n
+    for (seg, w), c in zip(fields, cols):
+        if w:
+            a = np.ascontiguousarray(c).view(np.uint8)
+            keep.append(a)
+            fx.append(_ptr(a)), vb.append(0), vo.append(0)
+        else:
+            b, o = np.ascontiguousarray(c[0], np.uint8), np.ascontiguousarray(c[1], np.uint64)
+            keep += [b, o]
+            fx.append(0), vb.append(_ptr(b)), vo.append(_ptr(o))
+            total += int(o[-1] - o[0]) + 4 * n
+    if fields:
+        total += n * (13 + sum(w if w else 4 for _, w in fields) + 1)
+    out = np.zeros(max(1, total), np.uint8)
+    off = np.zeros(n + 1, np.uint64)
+    arr = lambda v: (ctypes.c_void_p * max(1, len(v)))(*v)
+    f = _fields(fields)  # kept alive across the call
+    got = L.sym_oracle_flat_encode(len(fields), ctypes.addressof(f), n, arr(fx), arr(vb), arr(vo), service_id,
+                                   method_id, _ptr(out), _ptr(off))
+    assert got == total, (got, total)
+    return out[:total], off
+
+
+def flat_decode(fields, data, rec_off):
+    """-> (cols, status): cols[k] = u8 array [n, width] (fixed) or (bytes, offs [n+1]) (string)."""
+    L = _flat_lib()
+    data, rec_off, n, dp = _batch_args(data, rec_off)
+    cap = max(1, data.size)
+    outs, fx, vb, vo = [], [], [], []
+    for seg, w in fields:
+        if w:
+            a = np.zeros((max(1, n), w), np.uint8)
+            outs.append(a)
+            fx.append(_ptr(a)), vb.append(0), vo.append(0)
+        else:
+            b, o = np.zeros(cap, np.uint8), np.zeros(n + 1, np.uint64)
+            outs.append((b, o))
+            fx.append(0), vb.append(_ptr(b)), vo.append(_ptr(o))
+    st = np.zeros(max(1, n), np.uint8)
+    arr = lambda v: (ctypes.c_void_p * max(1, len(v)))(*v)
+    f = _fields(fields)
+    L.sym_oracle_flat_decode(len(fields), ctypes.addressof(f), n, dp, _ptr(rec_off), arr(fx), arr(vb), arr(vo),
+                             _ptr(st))
+    cols = [o[:n] if isinstance(o, np.ndarray) else (o[0][:int(o[1][n])], o[1]) for o in outs]
+    return cols, st[:n]
