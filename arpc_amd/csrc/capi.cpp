@@ -686,18 +686,20 @@ int sym_flat_encode(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t
     if (rc != SYM_OK) return rc;
     if (!d_out_off || (n && (!d_out || (nfields && (!d_cols || !d_offs)))))
         return fail(SYM_ERR_INVALID, "sym_flat_encode: NULL argument");
-    for (int k = 0; k < nfields && n; ++k)
+    for (int k = 0; k < nfields && n; ++k) {
         if (!d_cols[k] || (!fields[k].width && !d_offs[k]))
             return fail(SYM_ERR_INVALID, "sym_flat_encode: field %d has no column", k);
+        if (fields[k].width && (uintptr_t)d_cols[k] % fields[k].width)
+            return fail(SYM_ERR_INVALID, "sym_flat_encode: field %d column not %u-byte aligned", k, fields[k].width);
+    }
     DeviceGuard g(ctx->device);
     if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
     if (n == 0) {
         hipError_t e = hipMemsetAsync(d_out_off, 0, sizeof(uint64_t), (hipStream_t)stream);
         return e == hipSuccess ? SYM_OK : hip_fail(e, "hipMemsetAsync");
     }
-    if ((rc = ensure_scratch(ctx, symhip::flat_ws_bytes(fields, nfields, n), "flat encode")) != SYM_OK) return rc;
     hipError_t e = symhip::launch_flat_encode(fields, nfields, n, d_cols, d_offs, service_id, method_id, d_out,
-                                              d_out_off, ctx->frag, (hipStream_t)stream);
+                                              d_out_off, ctx->err, (hipStream_t)stream);
     return e == hipSuccess ? SYM_OK : hip_fail(e, "flat encode launch");
 }
 

@@ -131,7 +131,7 @@ namespace symhip {
 size_t flat_ws_bytes(const sym_field* f, int nf, uint64_t n);
 hipError_t launch_flat_encode(const sym_field* f, int nf, uint64_t n, const void* const* cols,
                               const uint64_t* const* offs, uint32_t sid, uint32_t mid, uint8_t* out,
-                              uint64_t* out_off, void* ws, hipStream_t stream);
+                              uint64_t* out_off, unsigned* err, hipStream_t stream);
 hipError_t launch_flat_decode(const sym_field* f, int nf, uint64_t n, const uint8_t* in, const uint64_t* rec_off,
                               void* const* cols, const uint64_t* caps, uint64_t* const* offs, uint8_t* status,
                               void* ws, unsigned* err, hipStream_t stream);

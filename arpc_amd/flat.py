@@ -64,10 +64,11 @@ TEST_FIXED = FlatSchema("Fixed", (FlatField("FInt32", "int32", True), FlatField(
 
 
 def encode(codec: Codec, schema: FlatSchema, cols: list, service_id: int = 0, method_id: int = 0,
-           stream=None, n: int | None = None):
+           stream=None, n: int | None = None, out=None):
     """cols[k]: tensor of n values (fixed field; any dtype of the field's width) or (uint8 bytes,
     int64 offsets [n+1]) (string field).  -> (stream uint8, offsets int64 [n+1]).  `n` is needed
-    only for a schema without fields (n empty messages)."""
+    only for a schema without fields (n empty messages).  out=(uint8 buffer, int64 [n+1]) skips
+    the size query (a device sync): the buffer must hold encoded_size bytes."""
     if len(cols) != len(schema.fields):
         raise ValueError(f"{schema.name}: {len(schema.fields)} columns expected")
     if not schema.fields and n is None:
@@ -86,7 +87,8 @@ def encode(codec: Codec, schema: FlatSchema, cols: list, service_id: int = 0, me
             _check_col(b, torch.uint8, f.name, codec.device)
             _check_col(o, torch.int64, f.name + " offsets", codec.device)
             m = o.numel() - 1
-            var_total += int(o[-1].item() - o[0].item()) if m else 0
+            if out is None:
+                var_total += int(o[-1].item() - o[0].item()) if m else 0
             ptrs.append(_dptr(b) or 1)
             offs.append(_dptr(o))
         if n is not None and m != n:
@@ -96,22 +98,33 @@ def encode(codec: Codec, schema: FlatSchema, cols: list, service_id: int = 0, me
         raise ValueError("columns disagree with n")
     n = n or 0
     cf = schema.c_fields()
-    size = codec._lib.sym_flat_encoded_size(cf, len(schema.fields), n, var_total)
-    out = torch.empty(max(1, size), dtype=torch.uint8, device=codec.device)
-    off = torch.empty(n + 1, dtype=torch.int64, device=codec.device)
+    if out is None:
+        size = codec._lib.sym_flat_encoded_size(cf, len(schema.fields), n, var_total)
+        out = torch.empty(max(1, size), dtype=torch.uint8, device=codec.device)
+        off = torch.empty(n + 1, dtype=torch.int64, device=codec.device)
+    else:
+        out, off = out
+        _check_col(out, torch.uint8, "out", codec.device)
+        _check_col(off, torch.int64, "out offsets", codec.device)
+        if off.numel() != n + 1:
+            raise ValueError("out offsets: n + 1 entries expected")
+        size = out.numel()
     _native.check(codec._lib.sym_flat_encode(codec._ctx, cf, len(schema.fields), n, _native.ptr_array(ptrs),
                                             _native.ptr_array(offs), service_id, method_id, _dptr(out), _dptr(off),
                                             _stream_handle(codec.device, stream)), "sym_flat_encode")
     return out[:size], off
 
 
-def decode(codec: Codec, schema: FlatSchema, data: torch.Tensor, rec_off: torch.Tensor, stream=None):
+def decode(codec: Codec, schema: FlatSchema, data: torch.Tensor, rec_off: torch.Tensor, stream=None,
+           span: int | None = None):
     """UnmarshalSymphony into fresh structs -> (cols, status); cols[k] a tensor of n values (fixed,
-    dtype of its kind) or (uint8 bytes, int64 offsets [n+1]) (string)."""
+    dtype of its kind) or (uint8 bytes, int64 offsets [n+1]) (string).  span = rec_off[n] -
+    rec_off[0] when the caller knows it (skips a device sync)."""
     _check_col(data, torch.uint8, "data", codec.device)
     _check_col(rec_off, torch.int64, "rec_off", codec.device)
     n = rec_off.numel() - 1
-    span = int(rec_off[-1].item() - rec_off[0].item()) if n else 0
+    if span is None:
+        span = int(rec_off[-1].item() - rec_off[0].item()) if n else 0
     cols, ptrs, caps, offs = [], [], [], []
     for f in schema.fields:
         if f.width:

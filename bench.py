@@ -310,6 +310,55 @@ def proxy_leg(codec: Codec, dev, reps: int) -> dict:
                     "getters (kv-store-symphony-element kv.syn.go:285-310) batched; outside the timed region"}
 
 
+def flat_leg(codec: Codec, dev, reps: int) -> dict:
+    """SURVEY.md 8f N5 (flat part) beside the headline: the run-time-described flat codec
+    (arpc_amd/flat.py) on the element-schema SetRequest (public Score + Username, private Key +
+    Value; kv-store-symphony-element kv.proto:18-41), 2^20 records of datagen.ELEMENT_FW, encode
+    and decode device-resident, HIP events.  Algorithmic bytes -- encode: score 4n + string bytes +
+    3 x 8(n+1) offsets read, records + 8(n+1) offsets written; decode: records + offsets read,
+    score 4n + string bytes + 3 x 8(n+1) offsets + n status written."""
+    from arpc_amd import datagen, flat
+    b = datagen.make_element_batch(**datagen.ELEMENT_FW)
+    n = len(b.score)
+    cols = [torch.from_numpy(b.score).to(dev)] + [(torch.from_numpy(x).to(dev), torch.from_numpy(o.view(np.int64)).to(dev))
+                                                  for x, o in b.strings]
+    sch = flat.ELEMENT_SET_REQUEST
+    data, off = flat.encode(codec, sch, cols)
+    dcols, st = flat.decode(codec, sch, data, off)
+    torch.cuda.synchronize()
+    codec.check()
+    rec_b = int(b.rec_off[-1])
+    str_b = sum(int(o[-1]) for _, o in b.strings)
+    ok = bool(np.array_equal(data.cpu().numpy(), b.data)) and bool((st == 0).all().item()) and \
+        bool(torch.equal(dcols[0], cols[0])) and all(torch.equal(dcols[k][0][:int(b.strings[k - 1][1][-1])], cols[k][0])
+                                                    for k in (1, 2, 3))
+
+    def timed(fn) -> float:
+        ev = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            ev.append((e0, e1))
+        torch.cuda.synchronize()
+        codec.check()
+        return float(np.median([a.elapsed_time(c) for a, c in ev]))
+
+    eout = (torch.empty_like(data), torch.empty_like(off))
+    enc_ms = timed(lambda: flat.encode(codec, sch, cols, out=eout))
+    dec_ms = timed(lambda: flat.decode(codec, sch, data, off, span=rec_b))
+    cols_b = 4 * n + str_b + 3 * 8 * (n + 1)
+    enc_alg = cols_b + rec_b + 8 * (n + 1)
+    dec_alg = rec_b + 8 * (n + 1) + cols_b + n
+    gbps = lambda a, ms: round(a / (ms * 1e-3) / 1e9, 1)
+    return {"schema": sch.name, "records": n, "record_bytes": int(b.rec_off[1]), "matches_oracle_marshal": ok,
+            "encode_ms": round(enc_ms, 4), "encode_gbps": gbps(enc_alg, enc_ms),
+            "decode_ms": round(dec_ms, 4), "decode_gbps": gbps(dec_alg, dec_ms),
+            "note": "generic flat-schema path; encode into a preallocated buffer, decode allocates its "
+                    "columns (caching allocator)"}
+
+
 def host_inclusive(codec: Codec, kw: dict, dev, steps: int) -> dict:
     """Pinned host -> H2D -> encode -> D2H, then H2D -> decode -> D2H (serial, one stream)."""
     b = datagen.make_batch(**kw)
@@ -372,6 +421,7 @@ def main():
     ap.add_argument("--proxy-reps", type=int, default=10, help="firewall / Raw getter leg repetitions (0 = skip)")
     ap.add_argument("--reassembly-reps", type=int, default=5, help="reassembly leg repetitions (0 = skip)")
     ap.add_argument("--crypto-reps", type=int, default=3, help="segment cipher leg repetitions (0 = skip)")
+    ap.add_argument("--flat-reps", type=int, default=5, help="flat-schema codec leg repetitions (0 = skip)")
     args = ap.parse_args()
 
     world, rank, local = dist_setup()
@@ -556,6 +606,8 @@ def main():
         line["crypto"] = crypto_leg(codec, enc[0][0], enc[0][1], dev, args.crypto_reps)
     if world == 1 and args.proxy_reps > 0:
         line["proxy"] = proxy_leg(codec, dev, args.proxy_reps)
+    if world == 1 and args.flat_reps > 0:
+        line["flat"] = flat_leg(codec, dev, args.flat_reps)
     if world == 1 and args.cpu_seconds > 0:
         line["cpu_baseline"] = cpu_baseline(kw, args.cpu_seconds)
     print(json.dumps(line), flush=True)

@@ -309,11 +309,13 @@ int sym_decrypt(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_off, ui
  * declaration order, `segment` SYM_SEGMENT_PUBLIC / SYM_SEGMENT_PRIVATE, `width` 1 (bool),
  * 4 (int32 / uint32 / float / enum), 8 (int64 / uint64 / double) or 0 (string / bytes).
  * Repeated and nested fields are not covered.  Columns are indexed by field: d_cols[k] is n
- * little-endian values of `width` bytes (fixed) or the packed bytes (string, with d_offs[k] its
- * n+1 offsets; d_offs[k] is ignored for fixed fields).  The kv-store and echo schemas above are the
+ * little-endian values of `width` bytes (fixed, `width`-aligned) or the packed bytes (string, with
+ * d_offs[k] its n+1 offsets; d_offs[k] is ignored for fixed fields).  The kv-store and echo schemas above are the
  * all-private cases of this (and keep their specialised kernels).
  *   sym_flat_encode  output record i = MarshalSymphony + the client's ID patch; d_out holds
  *                    sym_flat_encoded_size(...) bytes; d_out_off[n+1] computed on the device.
+ *                    A run of 64 records spanning 2 GiB or more is reported by sym_check as
+ *                    SYM_ERR_TOO_LARGE.
  *   sym_flat_decode  UnmarshalSymphony into fresh structs: fixed columns (zero when not read),
  *                    string columns of caps[k] bytes (rec_off[n] - rec_off[0] always suffices)
  *                    with d_offs[k][n+1]; d_status[n] SYM_STATUS_*. */

@@ -210,6 +210,19 @@ def test_flat_known_schemas_gpu(gcodec, gdev):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("fields", [[(0, 0)] * 16, [(1, 8)] * 16, [(0, 0)] * 8 + [(1, 0)] * 8, [(0, 1)] * 16,
+                                    [(1, 0), (0, 0)] * 8, [(0, 8), (0, 0)] * 4 + [(1, 4), (1, 0)] * 4],
+                         ids=["pub16str", "priv16u64", "pub8priv8", "pub16bool", "alt16str", "mixed16"])
+def test_flat_wide_schemas_gpu(gcodec, gdev, fields):
+    """The widest generated images (up to 142 bytes per record; fewer waves per workgroup)."""
+    rng = np.random.default_rng(len(fields) + sum(w for _, w in fields))
+    cols = random_columns(rng, fields, 1500)
+    data, off = _check_encode(gcodec, gdev, fields, cols, 1500, sid=3, mid=4)
+    _check_decode(gcodec, gdev, fields, data, off)
+    _check_decode(gcodec, gdev, fields, *corrupt(data, off, rng, frac=0.4))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n", [0, 1, 255, 256, 257])
 def test_flat_edge_counts_gpu(gcodec, gdev, n):
     rng = np.random.default_rng(n + 50)
