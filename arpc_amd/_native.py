@@ -97,6 +97,7 @@ SYM_GCM_OVERHEAD = 28
 
 
 SYM_MAX_FLAT_FIELDS = 16
+SYM_FIELD_REPEATED = 0x80
 
 
 class SymField(ctypes.Structure):

@@ -665,16 +665,21 @@ static int flat_check(const char* what, const sym_field* fields, int nf) {
         return fail(SYM_ERR_INVALID, "%s: %d fields (0..%d)", what, nf, SYM_MAX_FLAT_FIELDS);
     for (int k = 0; k < nf; ++k) {
         if (fields[k].segment > 1) return fail(SYM_ERR_INVALID, "%s: field %d segment %u", what, k, fields[k].segment);
-        const unsigned w = fields[k].width;
-        if (w != 0 && w != 1 && w != 4 && w != 8) return fail(SYM_ERR_INVALID, "%s: field %d width %u", what, k, w);
+        const unsigned w = fields[k].width & ~SYM_FIELD_REPEATED, rep = fields[k].width & SYM_FIELD_REPEATED;
+        if ((w != 0 && w != 1 && w != 4 && w != 8) || (rep && w == 0))
+            return fail(SYM_ERR_INVALID, "%s: field %d width 0x%x", what, k, fields[k].width);
     }
     return SYM_OK;
 }
 
+// scalar fixed-width field (a value column, no offsets); else string or repeated (bytes + offsets)
+static bool flat_scalar(const sym_field& f) { return f.width != 0 && !(f.width & SYM_FIELD_REPEATED); }
+
 uint64_t sym_flat_encoded_size(const sym_field* fields, int nfields, uint64_t n, uint64_t var_total) {
     if (nfields == 0) return 14 * n;
     uint64_t per = 13 + 1;
-    for (int k = 0; k < nfields; ++k) per += fields[k].width ? fields[k].width : 8;  // table entry + length prefix
+    for (int k = 0; k < nfields; ++k)  // scalar inline, else table entry + length / count prefix
+        per += flat_scalar(fields[k]) ? fields[k].width : 8;
     return per * n + var_total;
 }
 
@@ -687,9 +692,9 @@ int sym_flat_encode(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t
     if (!d_out_off || (n && (!d_out || (nfields && (!d_cols || !d_offs)))))
         return fail(SYM_ERR_INVALID, "sym_flat_encode: NULL argument");
     for (int k = 0; k < nfields && n; ++k) {
-        if (!d_cols[k] || (!fields[k].width && !d_offs[k]))
+        if (!d_cols[k] || (!flat_scalar(fields[k]) && !d_offs[k]))
             return fail(SYM_ERR_INVALID, "sym_flat_encode: field %d has no column", k);
-        if (fields[k].width && (uintptr_t)d_cols[k] % fields[k].width)
+        if (flat_scalar(fields[k]) && (uintptr_t)d_cols[k] % fields[k].width)
             return fail(SYM_ERR_INVALID, "sym_flat_encode: field %d column not %u-byte aligned", k, fields[k].width);
     }
     DeviceGuard g(ctx->device);
@@ -712,13 +717,13 @@ int sym_flat_decode(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t
     if (n && (!d_in || !d_rec_off || !d_status || (nfields && (!d_cols || !caps || !d_offs))))
         return fail(SYM_ERR_INVALID, "sym_flat_decode: NULL argument");
     for (int k = 0; k < nfields; ++k)
-        if ((n && !d_cols[k] && (fields[k].width || caps[k])) || (!fields[k].width && !d_offs[k]))
+        if ((n && !d_cols[k] && (flat_scalar(fields[k]) || caps[k])) || (!flat_scalar(fields[k]) && !d_offs[k]))
             return fail(SYM_ERR_INVALID, "sym_flat_decode: field %d has no column", k);
     DeviceGuard g(ctx->device);
     if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
     if (n == 0) {
         for (int k = 0; k < nfields; ++k)
-            if (!fields[k].width) {
+            if (!flat_scalar(fields[k])) {
                 hipError_t e = hipMemsetAsync(d_offs[k], 0, sizeof(uint64_t), (hipStream_t)stream);
                 if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync");
             }

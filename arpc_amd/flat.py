@@ -5,7 +5,8 @@ whose layout follows the fields' kinds and `is_public` flags
 (cmd/symphony-gen-arpc/protoc-gen-symphony/main.go:196-368 marshal, :622-800 unmarshal; field
 classification :1172-1239).  Here the message is described at run time -- `FlatSchema` lists the
 fields in declaration order -- and one pair of kernels serves every flat schema (arpc_amd/csrc/
-flat.hip, `sym_flat_encode` / `sym_flat_decode`).  Repeated and nested fields are not covered.
+flat.hip, `sym_flat_encode` / `sym_flat_decode`).  Repeated fixed-width fields are covered;
+repeated string and nested fields are not.
 
 Kinds (protobuf scalar -> table width): bool 1; int32, uint32, float, enum 4; int64, uint64,
 double 8; string, bytes 0 (a 4-byte payload offset in the table, then length + bytes).
@@ -27,13 +28,26 @@ DTYPE = {"bool": torch.uint8, "int32": torch.int32, "uint32": torch.int32, "floa
 
 @dataclass(frozen=True)
 class FlatField:
+    """One field; `repeated` with a fixed-width kind is `repeated int32 xs` etc. (payload: u32
+    count + elements, main.go:493-535, :795-841), carried like a string column: (element bytes,
+    int64 byte offsets [n+1])."""
     name: str
     kind: str
     public: bool = False
+    repeated: bool = False
+
+    def __post_init__(self):
+        if self.repeated and not WIDTH[self.kind]:
+            raise ValueError(f"{self.name}: repeated {self.kind} fields are not covered")
 
     @property
     def width(self) -> int:
-        return WIDTH[self.kind]
+        """Scalar width of a fixed field's value column; 0 for string and repeated fields."""
+        return 0 if self.repeated else WIDTH[self.kind]
+
+    @property
+    def c_width(self) -> int:
+        return (_native.SYM_FIELD_REPEATED | WIDTH[self.kind]) if self.repeated else WIDTH[self.kind]
 
 
 @dataclass(frozen=True)
@@ -45,7 +59,7 @@ class FlatSchema:
         arr = (_native.SymField * max(1, len(self.fields)))()
         for k, f in enumerate(self.fields):
             arr[k].segment = _native.SYM_SEGMENT_PUBLIC if f.public else _native.SYM_SEGMENT_PRIVATE
-            arr[k].width = f.width
+            arr[k].width = f.c_width
         return arr
 
 

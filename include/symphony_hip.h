@@ -307,11 +307,15 @@ int sym_decrypt(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_off, ui
  * string / bytes, each public or private (generator cmd/symphony-gen-arpc/protoc-gen-symphony/
  * main.go:196-368, 439-620 marshal; :622-800 unmarshal), described at run time: fields[k] in
  * declaration order, `segment` SYM_SEGMENT_PUBLIC / SYM_SEGMENT_PRIVATE, `width` 1 (bool),
- * 4 (int32 / uint32 / float / enum), 8 (int64 / uint64 / double) or 0 (string / bytes).
- * Repeated and nested fields are not covered.  Columns are indexed by field: d_cols[k] is n
- * little-endian values of `width` bytes (fixed, `width`-aligned) or the packed bytes (string, with
- * d_offs[k] its n+1 offsets; d_offs[k] is ignored for fixed fields).  The kv-store and echo schemas above are the
- * all-private cases of this (and keep their specialised kernels).
+ * 4 (int32 / uint32 / float / enum), 8 (int64 / uint64 / double) or 0 (string / bytes), or
+ * SYM_FIELD_REPEATED | 1 / 4 / 8 for a repeated fixed-width field (`repeated int32 xs`: a 4-byte
+ * table entry, then a u32 element count and the elements, main.go:493-535 / :795-841).
+ * Repeated string and nested fields are not covered.  Columns are indexed by field: d_cols[k] is n
+ * little-endian values of `width` bytes (fixed, `width`-aligned) or the packed bytes (string and
+ * repeated fixed, with d_offs[k] its n+1 BYTE offsets; a repeated field's record lengths must be
+ * multiples of its element width -- the count written is length / width; d_offs[k] is ignored
+ * for scalar fields).  Bool values (scalar or repeated) are the wire byte, read as `!= 0`.  The
+ * kv-store and echo schemas above are the all-private cases of this (and keep their specialised kernels).
  *   sym_flat_encode  output record i = MarshalSymphony + the client's ID patch; d_out holds
  *                    sym_flat_encoded_size(...) bytes; d_out_off[n+1] computed on the device.
  *                    A run of 64 records spanning 2 GiB or more is reported by sym_check as
@@ -320,10 +324,11 @@ int sym_decrypt(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_off, ui
  *                    string columns of caps[k] bytes (rec_off[n] - rec_off[0] always suffices)
  *                    with d_offs[k][n+1]; d_status[n] SYM_STATUS_*. */
 #define SYM_MAX_FLAT_FIELDS 16
+#define SYM_FIELD_REPEATED 0x80 /* or'ed into sym_field.width: repeated fixed-width field */
 
 typedef struct sym_field {
     uint8_t segment; /* SYM_SEGMENT_PUBLIC / SYM_SEGMENT_PRIVATE */
-    uint8_t width;   /* 1, 4, 8, or 0 for string / bytes */
+    uint8_t width;   /* 1, 4, 8, or 0 for string / bytes; SYM_FIELD_REPEATED | 1/4/8 for repeated */
 } sym_field;
 
 uint64_t sym_flat_encoded_size(const sym_field* fields, int nfields, uint64_t n, uint64_t var_total);

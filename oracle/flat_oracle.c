@@ -35,10 +35,16 @@
 #define ST_NO_PRIVATE 3
 #define ST_FIELD_TOO_SHORT 4
 
-/* A field: segment (0 public, 1 private) and width (1, 4, 8; 0 = string / bytes). */
+/* A field: segment (0 public, 1 private) and width (1, 4, 8; 0 = string / bytes; REP | 1/4/8 =
+ * repeated fixed-width: payload [u32 count][count * w bytes], main.go:493-535, decode :795-841). */
 typedef struct {
     uint8_t segment, width;
 } Field;
+
+#define REP 0x80
+/* scalar fixed width (0 for payload fields) and a payload field's element width (1 for strings) */
+static int scalar_w(const Field* f) { return (f->width & REP) ? 0 : f->width; }
+static int elem_w(const Field* f) { return (f->width & REP) ? (f->width & 0x7f) : 1; }
 
 static void wr32(uint8_t* p, uint32_t v) {
     for (int b = 0; b < 4; ++b) p[b] = (uint8_t)(v >> (8 * b));
@@ -52,7 +58,7 @@ static uint64_t rd(const uint8_t* p, int w) {
 static uint64_t table_size(const Field* f, int nf, int seg) {
     uint64_t t = 0;
     for (int k = 0; k < nf; ++k)
-        if (f[k].segment == seg) t += f[k].width ? f[k].width : 4;
+        if (f[k].segment == seg) t += scalar_w(&f[k]) ? scalar_w(&f[k]) : 4;
     return t;
 }
 
@@ -80,7 +86,7 @@ uint64_t sym_oracle_flat_encode(int nf, const Field* f, uint64_t n, const uint8_
         uint64_t pos[2] = {13 + pt, 0}; /* payload cursor per segment (absolute) */
         uint64_t off2p = 13 + pt;
         for (int k = 0; k < nf; ++k)
-            if (f[k].segment == 0 && !f[k].width) off2p += 4 + (var_off[k][i + 1] - var_off[k][i]);
+            if (f[k].segment == 0 && !scalar_w(&f[k])) off2p += 4 + (var_off[k][i + 1] - var_off[k][i]);
         memset(b, 0, 13);
         b[0] = 1;
         wr32(b + 1, (uint32_t)off2p);
@@ -91,13 +97,15 @@ uint64_t sym_oracle_flat_encode(int nf, const Field* f, uint64_t n, const uint8_
         uint64_t tab[2] = {13, off2p + 1};
         for (int k = 0; k < nf; ++k) {
             const int s = f[k].segment;
-            if (f[k].width) {
-                memcpy(b + tab[s], fixed[k] + (uint64_t)f[k].width * i, f[k].width);
-                tab[s] += f[k].width;
+            const int sw = scalar_w(&f[k]);
+            if (sw) {
+                memcpy(b + tab[s], fixed[k] + (uint64_t)sw * i, sw);
+                tab[s] += sw;
             } else {
+                /* string: u32 byte length; repeated fixed: u32 element count (:506-507) */
                 const uint64_t L = var_off[k][i + 1] - var_off[k][i];
                 wr32(b + tab[s], (uint32_t)(s ? pos[s] - off2p : pos[s]));
-                wr32(b + pos[s], (uint32_t)L);
+                wr32(b + pos[s], (uint32_t)(L / elem_w(&f[k])));
                 if (L) memcpy(b + pos[s] + 4, var[k] + var_off[k][i], L);
                 pos[s] += 4 + L;
                 tab[s] += 4;
@@ -118,7 +126,7 @@ void sym_oracle_flat_decode(int nf, const Field* f, uint64_t n, const uint8_t* i
         const uint8_t* d = in + rec_off[i];
         const uint64_t L = rec_off[i + 1] - rec_off[i];
         for (int k = 0; k < nf; ++k) {
-            if (f[k].width) memset(fixed[k] + (uint64_t)f[k].width * i, 0, f[k].width);
+            if (scalar_w(&f[k])) memset(fixed[k] + (uint64_t)scalar_w(&f[k]) * i, 0, scalar_w(&f[k]));
             else var_off[k][i] = w[k];
         }
         int st = ST_OK;
@@ -133,19 +141,21 @@ void sym_oracle_flat_decode(int nf, const Field* f, uint64_t n, const uint8_t* i
                     uint64_t t = 0;
                     for (int k = 0; k < nf && st == ST_OK; ++k) {
                         if (f[k].segment != s) continue;
-                        if (f[k].width) {
-                            if (L < ts + t + f[k].width) {
+                        const int sw = scalar_w(&f[k]);
+                        if (sw) {
+                            if (L < ts + t + sw) {
                                 st = ST_FIELD_TOO_SHORT;
                                 break;
                             }
-                            memcpy(fixed[k] + (uint64_t)f[k].width * i, d + ts + t, f[k].width);
-                            t += f[k].width;
+                            memcpy(fixed[k] + (uint64_t)sw * i, d + ts + t, sw);
+                            t += sw;
                         } else {
                             if (L >= ts + t + 4) {
                                 uint64_t po = rd(d + ts + t, 4);
                                 if (s && po > 0) po += o;
                                 if (po > 0 && L >= po + 4) {
-                                    const uint64_t dl = rd(d + po, 4);
+                                    /* string: length (:781-782); repeated: count * width (:812-813) */
+                                    const uint64_t dl = rd(d + po, 4) * (uint64_t)elem_w(&f[k]);
                                     if (L >= po + 4 + dl) {
                                         memcpy(var[k] + w[k], d + po + 4, dl);
                                         w[k] += dl;
@@ -161,5 +171,5 @@ void sym_oracle_flat_decode(int nf, const Field* f, uint64_t n, const uint8_t* i
         status[i] = (uint8_t)st;
     }
     for (int k = 0; k < nf; ++k)
-        if (!f[k].width) var_off[k][n] = w[k];
+        if (!scalar_w(&f[k])) var_off[k][n] = w[k];
 }

@@ -343,6 +343,9 @@ class _Field(ctypes.Structure):
     _fields_ = [("segment", ctypes.c_uint8), ("width", ctypes.c_uint8)]
 
 
+REPEATED = 0x80  # or'ed into a field's width: repeated fixed-width field (payload: u32 count + elements)
+
+
 def _flat_lib():
     L = lib()
     if not getattr(L, "_flat_ready", False):
@@ -369,7 +372,7 @@ def flat_encode(fields, cols, n: int, service_id: int = 0, method_id: int = 0):
     fx, vb, vo, keep = [], [], [], []
     total = (14 if not fields else 0) * n
     for (seg, w), c in zip(fields, cols):
-        if w:
+        if w and not w & REPEATED:
             a = np.ascontiguousarray(c).view(np.uint8)
             keep.append(a)
             fx.append(_ptr(a)), vb.append(0), vo.append(0)
@@ -379,7 +382,7 @@ def flat_encode(fields, cols, n: int, service_id: int = 0, method_id: int = 0):
             fx.append(0), vb.append(_ptr(b)), vo.append(_ptr(o))
             total += int(o[-1] - o[0]) + 4 * n
     if fields:
-        total += n * (13 + sum(w if w else 4 for _, w in fields) + 1)
+        total += n * (13 + sum(4 if (not w or w & REPEATED) else w for _, w in fields) + 1)
     out = np.zeros(max(1, total), np.uint8)
     off = np.zeros(n + 1, np.uint64)
     arr = lambda v: (ctypes.c_void_p * max(1, len(v)))(*v)
@@ -397,7 +400,7 @@ def flat_decode(fields, data, rec_off):
     cap = max(1, data.size)
     outs, fx, vb, vo = [], [], [], []
     for seg, w in fields:
-        if w:
+        if w and not w & REPEATED:
             a = np.zeros((max(1, n), w), np.uint8)
             outs.append(a)
             fx.append(_ptr(a)), vb.append(0), vo.append(0)

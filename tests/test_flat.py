@@ -20,20 +20,26 @@ from oracle import oracle
 from test_raw_fields import corrupted_batch, fixed_message
 
 KIND_NP = {1: np.uint8, 4: np.uint32, 8: np.uint64}
+REP = oracle.REPEATED  # width | REP: repeated fixed-width field
+
+
+def scalar(w):
+    return bool(w) and not w & REP
 
 
 def random_schema(rng, nf=None):
     nf = int(rng.integers(0, 17)) if nf is None else nf
-    return [(int(rng.integers(0, 2)), int(rng.choice([0, 0, 1, 4, 8]))) for _ in range(nf)]
+    return [(int(rng.integers(0, 2)), int(rng.choice([0, 0, 1, 4, 8, REP | 1, REP | 4, REP | 8]))) for _ in range(nf)]
 
 
 def random_columns(rng, fields, n):
     cols = []
     for seg, w in fields:
-        if w:
+        if scalar(w):
             cols.append(rng.integers(0, 256, (n, w), dtype=np.uint8))
         else:
-            ln = rng.choice([rng.integers(0, 8, n), rng.integers(0, 200, n)]).astype(np.uint64)
+            ew = w & ~REP if w else 1  # repeated: whole elements
+            ln = rng.choice([rng.integers(0, 8, n), rng.integers(0, 200, n)]).astype(np.uint64) // ew * ew
             off = np.zeros(n + 1, np.uint64)
             np.cumsum(ln, out=off[1:])
             cols.append((rng.integers(0, 256, int(off[-1]), dtype=np.uint8), off))
@@ -110,6 +116,32 @@ def test_oracle_fixed_message_kat():
     assert st[0] == oracle.STATUS_NO_PRIVATE
 
 
+def test_oracle_repeated_fixed_kats():
+    """Repeated fixed-width fields, bytes hand-derived from generateRepeatedFixedFieldMarshal
+    (main.go:493-535): a 4-byte table entry, then [u32 count][count elements] in the payload."""
+    # message {repeated int32 xs = 1;} xs = [1, -2]: private table entry 5 (relative), count 2
+    xs = np.array([1, -2], np.int32).view(np.uint8)
+    got, off = oracle.flat_encode([(1, REP | 4)], [(xs, np.array([0, 8], np.uint64))], 1)
+    want = bytes.fromhex("01 0d000000 00000000 00000000 01 05000000 02000000 01000000 feffffff".replace(" ", ""))
+    assert got.tobytes() == want
+    cols, st = oracle.flat_decode([(1, REP | 4)], got, off)
+    assert st[0] == 0 and cols[0][0].tobytes() == xs.tobytes()
+    # message {repeated uint64 ys = 1 [is_public]; string s = 2;} ys = [7], s = "ab": public
+    # segment 13 + 4 + 4 + 8 = 29; public entry absolute 17; private entry (34 - 29) = 5
+    ys = np.array([7], np.uint64).view(np.uint8)
+    fields = [(0, REP | 8), (1, 0)]
+    got, off = oracle.flat_encode(fields, [(ys, np.array([0, 8], np.uint64)),
+                                           (np.frombuffer(b"ab", np.uint8), np.array([0, 2], np.uint64))], 1)
+    want = bytes.fromhex("01 1d000000 00000000 00000000 11000000 01000000 0700000000000000 01 05000000 02000000 6162"
+                         .replace(" ", ""))
+    assert got.tobytes() == want
+    # decode: a count whose elements run past the end leaves the field empty (:811-813)
+    bad = bytearray(want)
+    struct.pack_into("<I", bad, 17, 3)  # 17 + 4 + 24 > 40
+    cols, st = oracle.flat_decode(fields, np.frombuffer(bytes(bad), np.uint8), np.array([0, len(bad)], np.uint64))
+    assert st[0] == 0 and cols[0][0].size == 0 and cols[1][0].tobytes() == b"ab"
+
+
 def test_oracle_empty_message():
     got, off = oracle.flat_encode([], [], 3)
     assert got.tobytes() == (b"\x01" + struct.pack("<I", 13) + bytes(8) + b"\x01") * 3
@@ -137,14 +169,15 @@ def gcodec(gdev):
 def _schema(fields):
     from arpc_amd import flat
     kinds = {1: "bool", 4: "uint32", 8: "uint64", 0: "bytes"}
-    return flat.FlatSchema("random", tuple(flat.FlatField(f"f{k}", kinds[w], seg == 0) for k, (seg, w) in enumerate(fields)))
+    return flat.FlatSchema("random", tuple(flat.FlatField(f"f{k}", kinds[w & ~REP], seg == 0, bool(w & REP))
+                                           for k, (seg, w) in enumerate(fields)))
 
 
 def _to_dev(cols, fields, dev):
     import torch
     out = []
     for (seg, w), c in zip(fields, cols):
-        if w:
+        if scalar(w):
             t = torch.from_numpy(np.ascontiguousarray(c).view(KIND_NP[w]).reshape(-1).view(
                 {1: np.uint8, 4: np.int32, 8: np.int64}[w]).copy()).to(dev)
             out.append(t)
@@ -165,7 +198,7 @@ def _check_decode(codec, dev, fields, data, off):
     codec.check()
     np.testing.assert_array_equal(got_st.cpu().numpy(), want_st, err_msg="status")
     for k, (seg, w) in enumerate(fields):
-        if w:
+        if scalar(w):
             np.testing.assert_array_equal(got_cols[k].cpu().numpy().view(np.uint8).reshape(-1, w),
                                           want_cols[k].reshape(-1, w), err_msg=f"fixed field {k}")
         else:
@@ -211,8 +244,9 @@ def test_flat_known_schemas_gpu(gcodec, gdev):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("fields", [[(0, 0)] * 16, [(1, 8)] * 16, [(0, 0)] * 8 + [(1, 0)] * 8, [(0, 1)] * 16,
-                                    [(1, 0), (0, 0)] * 8, [(0, 8), (0, 0)] * 4 + [(1, 4), (1, 0)] * 4],
-                         ids=["pub16str", "priv16u64", "pub8priv8", "pub16bool", "alt16str", "mixed16"])
+                                    [(1, 0), (0, 0)] * 8, [(0, 8), (0, 0)] * 4 + [(1, 4), (1, 0)] * 4,
+                                    [(0, REP | 4), (1, REP | 8), (1, 0), (0, REP | 1)] * 4],
+                         ids=["pub16str", "priv16u64", "pub8priv8", "pub16bool", "alt16str", "mixed16", "rep16"])
 def test_flat_wide_schemas_gpu(gcodec, gdev, fields):
     """The widest generated images (up to 142 bytes per record; fewer waves per workgroup)."""
     rng = np.random.default_rng(len(fields) + sum(w for _, w in fields))
