@@ -9,7 +9,9 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libsymphony_hip.so")
+# SYMHIP_LIBRARY names another build of the same ABI (tools/ use the tuning library, make tuning);
+# the product path, the tests and bench.py load the default.
+LIB_PATH = os.environ.get("SYMHIP_LIBRARY") or os.path.join(HERE, "lib", "libsymphony_hip.so")
 CSRC = os.path.join(HERE, "csrc")
 
 SYM_OK = 0
@@ -35,6 +37,7 @@ SIGNATURES = {
     "sym_ctx_destroy": (_int, [_ctx]),
     "sym_ctx_reserve": (_int, [_ctx, _u64]),
     "sym_ctx_check": (_int, [_ctx, _vp]),
+    "sym_ctx_set_decode_impl": (_int, [_ctx, _int]),
     "sym_schema_info": (_int, [_int, ctypes.POINTER(_int), ctypes.POINTER(_int)]),
     "sym_record_overhead": (_u64, [_int]),
     "sym_encoded_size": (_u64, [_int, _u64, _u64]),
@@ -49,6 +52,11 @@ SIGNATURES = {
     "sym_decode_kv_response": (_int, [_ctx, _int, _u8p, _u64p, _u64, _u8p, _u64, _u64p, _u8p, _vp]),
     "sym_decode_echo": (_int, [_ctx, _u8p, _u64p, _u64, _vp, _vp, _u8p, _u64, _u64p, _u8p, _u64, _u64p, _u8p,
                                _vp]),
+    "sym_encoded_size_kv_mixed": (_u64, [_u64, _u64, _u64, _u64]),
+    "sym_encode_kv_mixed": (_int, [_ctx, _u8p, _u8p, _u64p, _u8p, _u64p, _u64, _u32, _u32, _u32, _u8p, _u64p, _vp]),
+    "sym_decode_kv_mixed": (_int, [_ctx, _u8p, _u64p, _u8p, _u64, _u8p, _u64, _u64p, _u8p, _u64, _u64p, _u8p, _vp]),
+    "sym_host_alloc": (_int, [_ctx, _u64, ctypes.POINTER(ctypes.c_void_p)]),
+    "sym_host_free": (_int, [_ctx, _vp]),
     "sym_encode_host": (_int, [_ctx, _int, _u64, _vp, _vp, _vp, _u32, _u32, _u8p, _u64p]),
     "sym_decode_host": (_int, [_ctx, _int, _u64, _u8p, _u64p, _vp, _vp, _vp, _vp, _u8p]),
     "sym_fragment_plan": (_int, [_ctx, _u8p, _u64p, _u64, _u32, _u64p, _u64p, _u8p, _vp]),
@@ -65,6 +73,10 @@ SIGNATURES = {
     "sym_encrypt": (_int, [_ctx, _u8p, _u64p, _u64, ctypes.c_char_p, ctypes.c_char_p, _u8p, _u8p, _u64p, _u8p, _vp]),
     "sym_decrypt": (_int, [_ctx, _u8p, _u64p, _u64, ctypes.c_char_p, ctypes.c_char_p, _u8p, _u64p, _u8p, _vp]),
 }
+
+SYM_DECODE_PIPELINE = 0
+SYM_DECODE_THREE_KERNEL = 1
+SYM_DECODE_LOOKBACK = 2
 
 SYM_MAX_UDP_PAYLOAD = 1400
 SYM_DATA_PACKET_HEADER = 31

@@ -78,8 +78,12 @@ class Codec:
         _native.check(self._lib.sym_ctx_reserve(self._ctx, max_records), "sym_ctx_reserve")
 
     def check(self, stream=None):
-        """Synchronize and raise if a decode reported a capacity overflow or a look-back timeout."""
+        """Synchronize and raise if a call reported a device-side error (capacity, unplaceable batch)."""
         _native.check(self._lib.sym_ctx_check(self._ctx, _stream_handle(self.device, stream)), "sym_ctx_check")
+
+    def set_decode_impl(self, impl: int):
+        """SYM_DECODE_PIPELINE (default), SYM_DECODE_THREE_KERNEL or SYM_DECODE_LOOKBACK (same results)."""
+        _native.check(self._lib.sym_ctx_set_decode_impl(self._ctx, impl), "sym_ctx_set_decode_impl")
 
     # ------------------------------------------------------------------ encode
     def encode(self, schema: schemas.Schema | str, fixed, var, service_id: int = 0, method_id: int = 0,
@@ -142,6 +146,64 @@ class Codec:
             _stream_handle(self.device, stream))
         _native.check(rc, f"sym_decode({s.name})")
         return outputs
+
+
+# ------------------------------------------------------------------ mixed Get/Set batches
+def _encode_kv_mixed(codec: "Codec", rtype: torch.Tensor, key, val, service_id: int = 0, get_method_id: int = 0,
+                     set_method_id: int = 0, out: torch.Tensor | None = None, out_off: torch.Tensor | None = None,
+                     out_bytes: int | None = None, stream=None) -> EncodedBatch:
+    """A batch of GetRequests (rtype == 0) and SetRequests (else) in one call (sym_encode_kv_mixed).
+    key / val: (uint8 column, int64 offsets [n+1]); a GetRequest's value slice is not encoded.
+    `out_bytes` (sym_encoded_size_kv_mixed) avoids a host sync when `out` is not given."""
+    _check_col(rtype, torch.uint8, "type", codec.device)
+    for what, (b, o) in (("key", key), ("val", val)):
+        _check_col(b, torch.uint8, f"{what} bytes", codec.device)
+        _check_col(o, torch.int64, f"{what} offsets", codec.device)
+    n = key[1].numel() - 1
+    if val[1].numel() != n + 1 or rtype.numel() < n:
+        raise ValueError("type / key / val columns disagree on the record count")
+    if out is None:
+        if out_bytes is None:
+            is_set = (rtype[:n] != 0).to(torch.int64)
+            vlen = (val[1][1:] - val[1][:-1]) * is_set
+            out_bytes = 22 * n + int((8 * is_set + vlen).sum().item()) + int((key[1][-1] - key[1][0]).item()) if n else 0
+        out = torch.empty(max(1, out_bytes), dtype=torch.uint8, device=codec.device)
+    if out_off is None:
+        out_off = torch.empty(n + 1, dtype=torch.int64, device=codec.device)
+    _native.check(codec._lib.sym_encode_kv_mixed(
+        codec._ctx, _dptr(rtype) if n else 1, _dptr(key[0]) if key[0].numel() else 1, _dptr(key[1]),
+        _dptr(val[0]) if val[0].numel() else 1, _dptr(val[1]), n, service_id, get_method_id, set_method_id,
+        _dptr(out), _dptr(out_off), _stream_handle(codec.device, stream)), "sym_encode_kv_mixed")
+    return EncodedBatch(out, out_off)
+
+
+def _decode_kv_mixed(codec: "Codec", data: torch.Tensor, rec_off: torch.Tensor, rtype: torch.Tensor,
+                     caps: list | None = None, outputs: DecodedBatch | None = None, stream=None) -> DecodedBatch:
+    """Unmarshal each record as its type (0 GetRequest, else SetRequest) into a key and a value column
+    (empty values for GetRequests), sym_decode_kv_mixed."""
+    _check_col(data, torch.uint8, "data", codec.device)
+    _check_col(rec_off, torch.int64, "rec_off", codec.device)
+    _check_col(rtype, torch.uint8, "type", codec.device)
+    n = rec_off.numel() - 1
+    if outputs is None:
+        if caps is None:
+            span = int(rec_off[-1].item() - rec_off[0].item()) if n else 0
+            caps = [span, span]
+        outputs = DecodedBatch(fixed=[], var=[(torch.empty(max(1, c), dtype=torch.uint8, device=codec.device),
+                                               torch.empty(n + 1, dtype=torch.int64, device=codec.device)) for c in caps],
+                               status=torch.empty(max(1, n), dtype=torch.uint8, device=codec.device))
+    elif caps is None:
+        caps = [b.numel() for b, _ in outputs.var]
+    (kb, ko), (vb, vo) = outputs.var
+    _native.check(codec._lib.sym_decode_kv_mixed(
+        codec._ctx, _dptr(data) if data.numel() else 1, _dptr(rec_off), _dptr(rtype) if n else 1, n, _dptr(kb),
+        caps[0], _dptr(ko), _dptr(vb), caps[1], _dptr(vo), _dptr(outputs.status), _stream_handle(codec.device, stream)),
+        "sym_decode_kv_mixed")
+    return outputs
+
+
+Codec.encode_kv_mixed = _encode_kv_mixed
+Codec.decode_kv_mixed = _decode_kv_mixed
 
 
 @dataclass

@@ -1,8 +1,8 @@
 // capi.cpp -- the extern "C" boundary declared in include/symphony_hip.h.
 //
-// Argument checking, schema dispatch, the per-ctx decode workspace, device error
-// reporting and the host-memory entry points.  All compute goes to the HIP kernels in
-// encode.hip / decode.hip; there is no CPU codec in this library.
+// Argument checking, schema dispatch, the per-ctx workspaces and device error reporting.  All
+// compute goes to the HIP kernels (encode.hip, decode_pipe.hip, ...); the host-memory entry points
+// are in host.cpp.  There is no CPU codec in this library.
 #include <hip/hip_runtime.h>
 
 #include <cstdarg>
@@ -14,34 +14,14 @@
 
 #include "../../include/symphony_hip.h"
 #include "codec.hpp"
+#include "ctx.hpp"
 
 using symhip::DecodeParams;
 using symhip::EncodeParams;
 using symhip::Layout;
 
-struct sym_ctx {
-    int device = 0;
-    void* ws = nullptr;  // three-kernel decode workspace
-    size_t ws_bytes = 0;
-    void* flags = nullptr;  // default decode's aggregate / prefix words (epoch-tagged)
-    size_t flag_bytes = 0;
-    unsigned epoch = 0;     // tag of the last decode call's look-back words
-    unsigned* err = nullptr;  // device error word (kErr* bits)
-    // host entry points: device staging pool and a private stream
-    void* pool = nullptr;
-    size_t pool_bytes = 0;
-    hipStream_t stream = nullptr;
-    // scan workspace of the packetizer and the field getters: per-record scan inputs / outputs
-    // and the rocPRIM scan storage (stream-ordered, so calls on one stream share it)
-    void* frag = nullptr;
-    size_t frag_bytes = 0;
-    // segment cipher: device key schedule + GHASH tables of the last key pair, and that pair
-    void* crypt_tables = nullptr;
-    uint8_t crypt_keys[64] = {0};
-    int num_cus = 0;
-};
-
-namespace {
+namespace symhip {
+namespace capi {
 
 thread_local char g_err[512] = "";
 
@@ -66,21 +46,12 @@ const Layout kLayouts[SYM_SCHEMA_COUNT] = {
     {2, 2},  // EchoResponse
 };
 
-bool schema_ok(int schema) { return schema >= 0 && schema < SYM_SCHEMA_COUNT; }
+}  // namespace capi
+}  // namespace symhip
 
-// Runs the body with ctx->device current, restoring the caller's device after.
-struct DeviceGuard {
-    int prev = -1;
-    hipError_t err = hipSuccess;
-    explicit DeviceGuard(int dev) {
-        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-        if (prev != dev) err = hipSetDevice(dev);
-    }
-    ~DeviceGuard() {
-        int cur = -1;
-        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
-    }
-};
+using namespace symhip::capi;
+
+namespace {
 
 int ensure_ws(sym_ctx* ctx, int nvar, uint64_t n) {
     const size_t need = symhip::decode_workspace_bytes(nvar, n);
@@ -121,19 +92,6 @@ int next_epoch(sym_ctx* ctx, hipStream_t stream, unsigned* epoch) {
     return SYM_OK;
 }
 
-int ensure_pool(sym_ctx* ctx, size_t need) {
-    if (need <= ctx->pool_bytes) return SYM_OK;
-    if (ctx->pool) (void)hipFree(ctx->pool);
-    ctx->pool = nullptr;
-    ctx->pool_bytes = 0;
-    hipError_t e = hipMalloc(&ctx->pool, need);
-    if (e != hipSuccess) return fail(SYM_ERR_NOMEM, "staging pool of %zu bytes: %s", need, hipGetErrorString(e));
-    ctx->pool_bytes = need;
-    return SYM_OK;
-}
-
-size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
-
 int ensure_scratch(sym_ctx* ctx, size_t need, const char* what) {
     if (need <= ctx->frag_bytes) return SYM_OK;
     if (ctx->frag) (void)hipFree(ctx->frag);
@@ -147,10 +105,12 @@ int ensure_scratch(sym_ctx* ctx, size_t need, const char* what) {
 
 }  // namespace
 
+#ifdef SYMHIP_TUNING
 int symhip::tuning_variant(const char* env_name) {
     const char* v = getenv(env_name);
     return v ? atoi(v) : 0;
 }
+#endif
 
 extern "C" {
 
@@ -170,8 +130,7 @@ int sym_ctx_create(int device, sym_ctx** out_ctx) {
     sym_ctx* c = new (std::nothrow) sym_ctx;
     if (!c) return fail(SYM_ERR_NOMEM, "sym_ctx_create: out of host memory");
     c->device = device;
-    if ((e = hipMalloc(&c->err, 16)) != hipSuccess || (e = hipMemset(c->err, 0, 16)) != hipSuccess ||
-        (e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
+    if ((e = hipMalloc(&c->err, 16)) != hipSuccess || (e = hipMemset(c->err, 0, 16)) != hipSuccess) {
         sym_ctx_destroy(c);
         return hip_fail(e, "sym_ctx_create");
     }
@@ -182,14 +141,12 @@ int sym_ctx_create(int device, sym_ctx** out_ctx) {
 int sym_ctx_destroy(sym_ctx* ctx) {
     if (!ctx) return SYM_OK;
     DeviceGuard g(ctx->device);
-    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    host_slots_destroy(ctx);
     if (ctx->ws) (void)hipFree(ctx->ws);
     if (ctx->flags) (void)hipFree(ctx->flags);
     if (ctx->frag) (void)hipFree(ctx->frag);
     if (ctx->crypt_tables) (void)hipFree(ctx->crypt_tables);
     if (ctx->err) (void)hipFree(ctx->err);
-    if (ctx->pool) (void)hipFree(ctx->pool);
-    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return SYM_OK;
 }
@@ -214,7 +171,18 @@ int sym_ctx_check(sym_ctx* ctx, void* stream) {
     if (bits & symhip::kErrTimeout) return fail(SYM_ERR_DEVICE, "decode look-back timed out (device error bits 0x%x)", bits);
     if (bits & symhip::kErrTooLarge)
         return fail(SYM_ERR_INVALID, "64 consecutive records span >= 2 GiB; split the batch (device error bits 0x%x)", bits);
+    if (bits & symhip::kErrBadLength)
+        return fail(SYM_ERR_INVALID, "a repeated field's byte length is not a multiple of its element width "
+                    "(device error bits 0x%x)", bits);
     return fail(SYM_ERR_CAPACITY, "output capacity exceeded (decode column, Raw getter values or firewall kept bytes; device error bits 0x%x)", bits);
+}
+
+int sym_ctx_set_decode_impl(sym_ctx* ctx, int impl) {
+    if (!ctx) return fail(SYM_ERR_INVALID, "sym_ctx_set_decode_impl: ctx is NULL");
+    if (impl != SYM_DECODE_PIPELINE && impl != SYM_DECODE_THREE_KERNEL && impl != SYM_DECODE_LOOKBACK)
+        return fail(SYM_ERR_INVALID, "sym_ctx_set_decode_impl: unknown implementation %d", impl);
+    ctx->decode_impl = impl;
+    return SYM_OK;
 }
 
 int sym_schema_info(int schema, int* nfixed, int* nvar) {
@@ -234,9 +202,12 @@ uint64_t sym_encoded_size(int schema, uint64_t n, uint64_t var_total) {
     return n * sym_record_overhead(schema) + var_total;
 }
 
-int sym_encode(sym_ctx* ctx, int schema, uint64_t n, const int32_t* const* d_fixed, const uint8_t* const* d_bytes,
-               const uint64_t* const* d_offs, uint32_t service_id, uint32_t method_id, uint8_t* d_out,
-               uint64_t* d_out_off, void* stream) {
+}  // extern "C"
+
+int symhip::capi::encode_call(sym_ctx* ctx, int schema, uint64_t n, const int32_t* const* d_fixed,
+                              const uint8_t* const* d_bytes, const uint64_t* const* d_offs, uint32_t service_id,
+                              uint32_t method_id, uint8_t* d_out, uint64_t* d_out_off, uint64_t out_base,
+                              void* stream) {
     if (!ctx) return fail(SYM_ERR_INVALID, "sym_encode: ctx is NULL");
     if (!schema_ok(schema)) return fail(SYM_ERR_INVALID, "sym_encode: unknown schema %d", schema);
     const Layout lay = kLayouts[schema];
@@ -262,31 +233,44 @@ int sym_encode(sym_ctx* ctx, int schema, uint64_t n, const int32_t* const* d_fix
     p.method_id = method_id;
     p.out = d_out;
     p.out_off = d_out_off;
+    p.out_base = out_base;
     p.err = ctx->err;
+#ifdef SYMHIP_TUNING
     p.variant = symhip::tuning_variant("SYMHIP_ENCODE_VARIANT");
+#endif
     DeviceGuard g(ctx->device);
     if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
+    if (n == 0 && out_base) return fail(SYM_ERR_INVALID, "sym_encode: empty batch with an output base");
     hipError_t e = symhip::launch_encode(p, (hipStream_t)stream);
     return e == hipSuccess ? SYM_OK : hip_fail(e, "encode launch");
 }
 
-int sym_decode(sym_ctx* ctx, int schema, uint64_t n, const uint8_t* d_in, const uint64_t* d_rec_off,
-               int32_t* const* d_fixed, uint8_t* const* d_bytes, const uint64_t* caps, uint64_t* const* d_offs,
-               uint8_t* d_status, void* stream) {
-    if (!ctx) return fail(SYM_ERR_INVALID, "sym_decode: ctx is NULL");
-    if (!schema_ok(schema)) return fail(SYM_ERR_INVALID, "sym_decode: unknown schema %d", schema);
-    const Layout lay = kLayouts[schema];
-    if (!d_offs) return fail(SYM_ERR_INVALID, "sym_decode: d_offs is NULL");
+extern "C" {
+
+int sym_encode(sym_ctx* ctx, int schema, uint64_t n, const int32_t* const* d_fixed, const uint8_t* const* d_bytes,
+               const uint64_t* const* d_offs, uint32_t service_id, uint32_t method_id, uint8_t* d_out,
+               uint64_t* d_out_off, void* stream) {
+    return encode_call(ctx, schema, n, d_fixed, d_bytes, d_offs, service_id, method_id, d_out, d_out_off, 0, stream);
+}
+
+}  // extern "C"
+
+// One decode call of a flat layout; `type` non-null: a mixed kv batch (layout {0, 2}).
+int symhip::capi::decode_call(const char* what, sym_ctx* ctx, Layout lay, const uint8_t* d_type, uint64_t n,
+                       const uint8_t* d_in, const uint64_t* d_rec_off, int32_t* const* d_fixed,
+                       uint8_t* const* d_bytes, const uint64_t* caps, uint64_t* const* d_offs, uint8_t* d_status,
+                       void* stream) {
+    if (!d_offs) return fail(SYM_ERR_INVALID, "%s: d_offs is NULL", what);
     for (int f = 0; f < lay.nvar; ++f)
-        if (!d_offs[f]) return fail(SYM_ERR_INVALID, "sym_decode: offset column %d is NULL", f);
+        if (!d_offs[f]) return fail(SYM_ERR_INVALID, "%s: offset column %d is NULL", what, f);
     if (n > 0) {
-        if (!d_in || !d_rec_off || !d_status) return fail(SYM_ERR_INVALID, "sym_decode: d_in/d_rec_off/d_status is NULL");
-        if (lay.nfixed && !d_fixed) return fail(SYM_ERR_INVALID, "sym_decode: d_fixed is NULL");
+        if (!d_in || !d_rec_off || !d_status) return fail(SYM_ERR_INVALID, "%s: d_in/d_rec_off/d_status is NULL", what);
+        if (lay.nfixed && !d_fixed) return fail(SYM_ERR_INVALID, "%s: d_fixed is NULL", what);
         for (int f = 0; f < lay.nfixed; ++f)
-            if (!d_fixed[f]) return fail(SYM_ERR_INVALID, "sym_decode: fixed column %d is NULL", f);
-        if (!d_bytes || !caps) return fail(SYM_ERR_INVALID, "sym_decode: d_bytes/caps is NULL");
+            if (!d_fixed[f]) return fail(SYM_ERR_INVALID, "%s: fixed column %d is NULL", what, f);
+        if (!d_bytes || !caps) return fail(SYM_ERR_INVALID, "%s: d_bytes/caps is NULL", what);
         for (int f = 0; f < lay.nvar; ++f)
-            if (!d_bytes[f] && caps[f]) return fail(SYM_ERR_INVALID, "sym_decode: byte column %d is NULL", f);
+            if (!d_bytes[f] && caps[f]) return fail(SYM_ERR_INVALID, "%s: byte column %d is NULL", what, f);
     }
     DeviceGuard g(ctx->device);
     if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
@@ -300,6 +284,7 @@ int sym_decode(sym_ctx* ctx, int schema, uint64_t n, const uint8_t* d_in, const 
     p.n = n;
     p.in = d_in;
     p.rec_off = d_rec_off;
+    p.type = d_type;
     for (int f = 0; f < lay.nfixed; ++f) p.fixed[f] = d_fixed[f];
     for (int f = 0; f < lay.nvar; ++f) {
         p.bytes[f] = n ? d_bytes[f] : nullptr;
@@ -311,10 +296,24 @@ int sym_decode(sym_ctx* ctx, int schema, uint64_t n, const uint8_t* d_in, const 
     p.flags = ctx->flags;
     p.epoch = epoch;
     p.err = ctx->err;
+    p.impl = ctx->decode_impl;
+#ifdef SYMHIP_TUNING
     p.variant = symhip::tuning_variant("SYMHIP_DECODE_VARIANT");
     if (const char* d = getenv("SYMHIP_DEBUG_PTR")) p.dbg = (uint64_t*)(uintptr_t)strtoull(d, nullptr, 16);
+#endif
     hipError_t e = symhip::launch_decode(p, (hipStream_t)stream);
     return e == hipSuccess ? SYM_OK : hip_fail(e, "decode launch");
+}
+
+extern "C" {
+
+int sym_decode(sym_ctx* ctx, int schema, uint64_t n, const uint8_t* d_in, const uint64_t* d_rec_off,
+               int32_t* const* d_fixed, uint8_t* const* d_bytes, const uint64_t* caps, uint64_t* const* d_offs,
+               uint8_t* d_status, void* stream) {
+    if (!ctx) return fail(SYM_ERR_INVALID, "sym_decode: ctx is NULL");
+    if (!schema_ok(schema)) return fail(SYM_ERR_INVALID, "sym_decode: unknown schema %d", schema);
+    return decode_call("sym_decode", ctx, kLayouts[schema], nullptr, n, d_in, d_rec_off, d_fixed, d_bytes, caps, d_offs,
+                       d_status, stream);
 }
 
 // ---- typed entry points ----
@@ -390,134 +389,53 @@ int sym_decode_echo(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_off
     return sym_decode(ctx, SYM_SCHEMA_ECHO_REQUEST, n, d_in, d_rec_off, fx, b, caps, o, d_status, stream);
 }
 
-// ---- host-memory entry points ----
-// Stage through one device pool: inputs H2D, kernel, outputs D2H, all on the ctx stream.
-// Offsets are passed through unchanged; the device column base is shifted by -offs[0] so
-// the kernels see the same absolute offsets the caller used.
+// ---- mixed GetRequest / SetRequest batches ----
 
-int sym_encode_host(sym_ctx* ctx, int schema, uint64_t n, const int32_t* const* h_fixed,
-                    const uint8_t* const* h_bytes, const uint64_t* const* h_offs, uint32_t service_id,
-                    uint32_t method_id, uint8_t* h_out, uint64_t* h_out_off) {
-    if (!ctx) return fail(SYM_ERR_INVALID, "sym_encode_host: ctx is NULL");
-    if (!schema_ok(schema)) return fail(SYM_ERR_INVALID, "sym_encode_host: unknown schema %d", schema);
-    if (!h_out_off) return fail(SYM_ERR_INVALID, "sym_encode_host: h_out_off is NULL");
-    const Layout lay = kLayouts[schema];
-    if (n == 0) {
-        h_out_off[0] = 0;
-        return SYM_OK;
-    }
-    if (!h_out || !h_bytes || !h_offs || (lay.nfixed && !h_fixed))
-        return fail(SYM_ERR_INVALID, "sym_encode_host: NULL column");
-    uint64_t col_lo[2] = {0, 0}, col_len[2] = {0, 0}, var_total = 0;
-    for (int f = 0; f < lay.nvar; ++f) {
-        if (!h_offs[f] || !h_bytes[f]) return fail(SYM_ERR_INVALID, "sym_encode_host: NULL var column %d", f);
-        col_lo[f] = h_offs[f][0];
-        if (h_offs[f][n] < col_lo[f]) return fail(SYM_ERR_INVALID, "sym_encode_host: offsets of field %d decrease", f);
-        col_len[f] = h_offs[f][n] - col_lo[f];
-        var_total += col_len[f];
-    }
-    const uint64_t out_bytes = sym_encoded_size(schema, n, var_total);
-    size_t at = 0, o_fixed[2], o_bytes[2], o_offs[2];
-    for (int f = 0; f < lay.nfixed; ++f) { o_fixed[f] = at; at = align256(at + 4 * n); }
-    for (int f = 0; f < lay.nvar; ++f) {
-        o_bytes[f] = at; at = align256(at + col_len[f] + 16);
-        o_offs[f] = at; at = align256(at + 8 * (n + 1));
-    }
-    const size_t o_out = at; at = align256(at + out_bytes + 16);
-    const size_t o_out_off = at; at = align256(at + 8 * (n + 1));
-    DeviceGuard g(ctx->device);
-    if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
-    int rc = ensure_pool(ctx, at);
-    if (rc != SYM_OK) return rc;
-    char* base = (char*)ctx->pool;
-    hipStream_t s = ctx->stream;
-    hipError_t e = hipSuccess;
-    const int32_t* d_fixed[2] = {nullptr, nullptr};
-    const uint8_t* d_bytes[2] = {nullptr, nullptr};
-    const uint64_t* d_offs[2] = {nullptr, nullptr};
-    for (int f = 0; f < lay.nfixed && e == hipSuccess; ++f) {
-        e = hipMemcpyAsync(base + o_fixed[f], h_fixed[f], 4 * n, hipMemcpyHostToDevice, s);
-        d_fixed[f] = (const int32_t*)(base + o_fixed[f]);
-    }
-    for (int f = 0; f < lay.nvar && e == hipSuccess; ++f) {
-        if (col_len[f]) e = hipMemcpyAsync(base + o_bytes[f], h_bytes[f] + col_lo[f], col_len[f], hipMemcpyHostToDevice, s);
-        if (e == hipSuccess) e = hipMemcpyAsync(base + o_offs[f], h_offs[f], 8 * (n + 1), hipMemcpyHostToDevice, s);
-        d_bytes[f] = (const uint8_t*)(base + o_bytes[f]) - col_lo[f];
-        d_offs[f] = (const uint64_t*)(base + o_offs[f]);
-    }
-    if (e != hipSuccess) return hip_fail(e, "sym_encode_host H2D");
-    rc = sym_encode(ctx, schema, n, d_fixed, d_bytes, d_offs, service_id, method_id, (uint8_t*)(base + o_out),
-                    (uint64_t*)(base + o_out_off), s);
-    if (rc != SYM_OK) return rc;
-    if ((e = hipMemcpyAsync(h_out, base + o_out, out_bytes, hipMemcpyDeviceToHost, s)) != hipSuccess ||
-        (e = hipMemcpyAsync(h_out_off, base + o_out_off, 8 * (n + 1), hipMemcpyDeviceToHost, s)) != hipSuccess ||
-        (e = hipStreamSynchronize(s)) != hipSuccess)
-        return hip_fail(e, "sym_encode_host D2H");
-    return SYM_OK;
+uint64_t sym_encoded_size_kv_mixed(uint64_t n, uint64_t n_set, uint64_t key_total, uint64_t set_value_total) {
+    return 22 * n + 8 * n_set + key_total + set_value_total;
 }
 
-int sym_decode_host(sym_ctx* ctx, int schema, uint64_t n, const uint8_t* h_in, const uint64_t* h_rec_off,
-                    int32_t* const* h_fixed, uint8_t* const* h_bytes, const uint64_t* caps, uint64_t* const* h_offs,
-                    uint8_t* h_status) {
-    if (!ctx) return fail(SYM_ERR_INVALID, "sym_decode_host: ctx is NULL");
-    if (!schema_ok(schema)) return fail(SYM_ERR_INVALID, "sym_decode_host: unknown schema %d", schema);
-    const Layout lay = kLayouts[schema];
-    if (!h_offs) return fail(SYM_ERR_INVALID, "sym_decode_host: h_offs is NULL");
-    for (int f = 0; f < lay.nvar; ++f)
-        if (!h_offs[f]) return fail(SYM_ERR_INVALID, "sym_decode_host: h_offs[%d] is NULL", f);
-    if (n == 0) {
-        for (int f = 0; f < lay.nvar; ++f) h_offs[f][0] = 0;
-        return SYM_OK;
-    }
-    if (!h_in || !h_rec_off || !h_status || !h_bytes || !caps || (lay.nfixed && !h_fixed))
-        return fail(SYM_ERR_INVALID, "sym_decode_host: NULL argument");
-    const uint64_t in_lo = h_rec_off[0];
-    if (h_rec_off[n] < in_lo) return fail(SYM_ERR_INVALID, "sym_decode_host: record offsets decrease");
-    const uint64_t in_len = h_rec_off[n] - in_lo;
-    size_t at = 0;
-    const size_t o_in = at; at = align256(at + in_len + 16);
-    const size_t o_rec = at; at = align256(at + 8 * (n + 1));
-    const size_t o_status = at; at = align256(at + n);
-    size_t o_fixed[2], o_bytes[2], o_offs[2];
-    for (int f = 0; f < lay.nfixed; ++f) { o_fixed[f] = at; at = align256(at + 4 * n); }
-    for (int f = 0; f < lay.nvar; ++f) {
-        o_bytes[f] = at; at = align256(at + caps[f] + 16);
-        o_offs[f] = at; at = align256(at + 8 * (n + 1));
-    }
+int sym_encode_kv_mixed(sym_ctx* ctx, const uint8_t* d_type, const uint8_t* d_key, const uint64_t* d_key_off,
+                        const uint8_t* d_val, const uint64_t* d_val_off, uint64_t n, uint32_t service_id,
+                        uint32_t get_method_id, uint32_t set_method_id, uint8_t* d_out, uint64_t* d_out_off,
+                        void* stream) {
+    if (!ctx) return fail(SYM_ERR_INVALID, "sym_encode_kv_mixed: ctx is NULL");
+    if (!d_out_off || (n && (!d_type || !d_key || !d_key_off || !d_val || !d_val_off || !d_out)))
+        return fail(SYM_ERR_INVALID, "sym_encode_kv_mixed: NULL argument");
     DeviceGuard g(ctx->device);
     if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
-    int rc = ensure_pool(ctx, at);
-    if (rc != SYM_OK) return rc;
-    char* base = (char*)ctx->pool;
-    hipStream_t s = ctx->stream;
-    hipError_t e = hipSuccess;
-    if (in_len) e = hipMemcpyAsync(base + o_in, h_in + in_lo, in_len, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(base + o_rec, h_rec_off, 8 * (n + 1), hipMemcpyHostToDevice, s);
-    if (e != hipSuccess) return hip_fail(e, "sym_decode_host H2D");
-    int32_t* d_fixed[2] = {nullptr, nullptr};
-    uint8_t* d_bytes[2] = {nullptr, nullptr};
-    uint64_t* d_offs[2] = {nullptr, nullptr};
-    for (int f = 0; f < lay.nfixed; ++f) d_fixed[f] = (int32_t*)(base + o_fixed[f]);
-    for (int f = 0; f < lay.nvar; ++f) {
-        d_bytes[f] = (uint8_t*)(base + o_bytes[f]);
-        d_offs[f] = (uint64_t*)(base + o_offs[f]);
+    EncodeParams p{};
+    p.lay = kLayouts[SYM_SCHEMA_KV_SET_REQUEST];
+    p.n = n;
+    p.bytes[0] = d_key;
+    p.offs[0] = d_key_off;
+    p.bytes[1] = d_val;
+    p.offs[1] = d_val_off;
+    p.service_id = service_id;
+    p.method_id = set_method_id;
+    p.method_get = get_method_id;
+    p.type = d_type;
+    p.out = d_out;
+    p.out_off = d_out_off;
+    p.err = ctx->err;
+    if (n) {
+        const int rc = ensure_scratch(ctx, symhip::encode_mixed_ws_bytes(n), "mixed encode");
+        if (rc != SYM_OK) return rc;
     }
-    rc = sym_decode(ctx, schema, n, (const uint8_t*)(base + o_in) - in_lo, (const uint64_t*)(base + o_rec), d_fixed,
-                    d_bytes, caps, d_offs, (uint8_t*)(base + o_status), s);
-    if (rc != SYM_OK) return rc;
-    for (int f = 0; f < lay.nvar && e == hipSuccess; ++f)
-        e = hipMemcpyAsync(h_offs[f], d_offs[f], 8 * (n + 1), hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
-    if (e != hipSuccess) return hip_fail(e, "sym_decode_host D2H offsets");
-    rc = sym_ctx_check(ctx, s);
-    if (rc != SYM_OK) return rc;
-    for (int f = 0; f < lay.nfixed && e == hipSuccess; ++f)
-        e = hipMemcpyAsync(h_fixed[f], d_fixed[f], 4 * n, hipMemcpyDeviceToHost, s);
-    for (int f = 0; f < lay.nvar && e == hipSuccess; ++f)
-        if (h_offs[f][n]) e = hipMemcpyAsync(h_bytes[f], d_bytes[f], h_offs[f][n], hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(h_status, base + o_status, n, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
-    return e == hipSuccess ? SYM_OK : hip_fail(e, "sym_decode_host D2H");
+    hipError_t e = symhip::launch_encode_mixed(p, ctx->frag, ctx->err + 1, (hipStream_t)stream);
+    return e == hipSuccess ? SYM_OK : hip_fail(e, "mixed encode launch");
+}
+
+int sym_decode_kv_mixed(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_off, const uint8_t* d_type,
+                        uint64_t n, uint8_t* d_key, uint64_t key_cap, uint64_t* d_key_off, uint8_t* d_val,
+                        uint64_t val_cap, uint64_t* d_val_off, uint8_t* d_status, void* stream) {
+    if (!ctx) return fail(SYM_ERR_INVALID, "sym_decode_kv_mixed: ctx is NULL");
+    if (n && !d_type) return fail(SYM_ERR_INVALID, "sym_decode_kv_mixed: d_type is NULL");
+    uint8_t* b[2] = {d_key, d_val};
+    const uint64_t caps[2] = {key_cap, val_cap};
+    uint64_t* o[2] = {d_key_off, d_val_off};
+    return decode_call("sym_decode_kv_mixed", ctx, kLayouts[SYM_SCHEMA_KV_SET_REQUEST], n ? d_type : nullptr, n, d_in,
+                       d_rec_off, nullptr, b, caps, o, d_status, stream);
 }
 
 // ---- packetization ----

@@ -30,8 +30,22 @@ struct EncodeParams {
     uint8_t* out;
     uint64_t* out_off;
     unsigned* err;  // persistent device error word (kErr* bits), cleared by the host
-    int variant;    // kernel tuning variant (tuning_variant("SYMHIP_ENCODE_VARIANT"))
+    // mixed kv batch (sym_encode_kv_mixed): per-record type (0 GetRequest, else SetRequest) and the
+    // record-size prefixes from launch_encode_mixed's size pass (tile t starts at
+    // group_pre[t / 64] + tile_loc[t]); null otherwise
+    const uint8_t* type;
+    const uint64_t* group_pre;
+    const uint64_t* tile_loc;
+    uint32_t method_get;  // method id written into [9:13] of GetRequest records (mixed batches)
+    uint64_t out_base;    // added to every out_off value written (chunked host staging), 0 otherwise
+    int variant;    // kernel tuning variant (tuning builds only, tuning_variant("SYMHIP_ENCODE_VARIANT"))
 };
+
+// Decode implementations selectable per ctx (sym_ctx_set_decode_impl).
+constexpr int kImplPipeline = 0;      // one launch: parsers, streaming scanner, copiers (default)
+constexpr int kImplThreeKernel = 1;   // parse -> scan -> copy, three stream-ordered launches
+constexpr int kImplLookback = 2;      // the pipeline with parsers and scanner idle: every copier
+                                      // resolves its prefix by look-back (the fallback path, forced)
 
 struct DecodeParams {
     Layout lay;
@@ -43,13 +57,15 @@ struct DecodeParams {
     uint64_t cap[kMaxVar];
     uint64_t* offs[kMaxVar];
     uint8_t* status;
-    void* ws;       // decode_workspace_bytes() bytes (three-kernel decode, variant 300)
+    const uint8_t* type;  // mixed kv batch: per-record type (0 GetRequest, else SetRequest); else null
+    void* ws;       // decode_workspace_bytes() bytes (three-kernel decode)
     void* flags;    // decode_pipe_flag_bytes() bytes of aggregate / prefix words (default decode)
     unsigned epoch; // word tag of this call, in [1, kEpochLimit)
-    u64_t* dbg;     // diagnostics only (tools/fused_timeline.py): per-tile timestamps, else null
+    u64_t* dbg;     // tuning builds only (tools/fused_timeline.py): per-tile timestamps, else null
     unsigned pipe_parsers;  // set by launch_decode_pipe: parser workgroups of the launch
     unsigned* err;  // persistent device error word (kErr* bits), cleared by the host
-    int variant;    // kernel tuning variant (tuning_variant("SYMHIP_DECODE_VARIANT"))
+    int impl;       // kImpl*
+    int variant;    // kernel tuning variant (tuning builds only, tuning_variant("SYMHIP_DECODE_VARIANT"))
 };
 
 // Device workspace for the single-pass decode scan: [0,16) tile ticket, then per var
@@ -59,8 +75,9 @@ struct DecodeWsHeader {
     unsigned int pad[3];
 };
 constexpr unsigned kErrCapacity = 1u;
-constexpr unsigned kErrTimeout = 2u;
+constexpr unsigned kErrTimeout = 2u;   // a bounded device-side wait gave up (no kernel sets it today)
 constexpr unsigned kErrTooLarge = 4u;  // 64 consecutive records spanning >= 2 GiB
+constexpr unsigned kErrBadLength = 8u;  // flat encode: a repeated field's byte length is not a multiple of its width
 
 size_t decode_workspace_bytes(int nvar, uint64_t n);
 // Aggregate / prefix words of the default decode (decode_pipe.hip): tagged with the call's epoch, so
@@ -69,9 +86,12 @@ size_t decode_pipe_flag_bytes(int nvar, uint64_t n);
 constexpr unsigned kEpochLimit = 1u << 20;
 hipError_t launch_decode_pipe(const DecodeParams& p, void* flags, unsigned epoch, hipStream_t stream);
 
-// Kernel variant selected by an environment variable (0 = default); lets tools/kbench.py
-// compare variants inside one process.
+#ifdef SYMHIP_TUNING
+// Kernel variant selected by an environment variable (0 = default); lets tools/kbench.py compare
+// variants inside one process.  Only the tuning library (make tuning) has variants: the product
+// library never reads the environment.
 int tuning_variant(const char* env_name);
+#endif
 
 // ---- packetization (packetize.hip)
 struct FragWriteArgs {
@@ -164,6 +184,9 @@ hipError_t launch_firewall(const uint8_t* in, const uint64_t* rec_off, uint64_t 
                            hipStream_t stream);
 
 hipError_t launch_encode(const EncodeParams& p, hipStream_t stream);
+// Mixed Get/Set batch: size pass (per-tile record-size totals, last workgroup scans them) + encode.
+size_t encode_mixed_ws_bytes(uint64_t n);
+hipError_t launch_encode_mixed(EncodeParams p, void* ws, unsigned* ticket, hipStream_t stream);
 hipError_t launch_decode(const DecodeParams& p, hipStream_t stream);
 
 }  // namespace symhip

@@ -1,0 +1,79 @@
+// ctx.hpp -- the sym_ctx object behind the C ABI and the helpers capi.cpp and host.cpp share.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "../../include/symphony_hip.h"
+#include "codec.hpp"
+
+namespace symhip {
+namespace host {
+constexpr int kSlots = 3;  // chunks in flight in the host-memory entry points
+// One in-flight chunk of a *_host call: its stream, device buffers and pinned staging.
+struct Slot {
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;    // the chunk's last copy
+    hipEvent_t kernel = nullptr;  // the chunk's kernel (kernels of consecutive chunks are ordered)
+    void* dev = nullptr;
+    size_t dev_bytes = 0;
+    void* pin = nullptr;  // pinned staging for pageable caller memory (inputs, then outputs)
+    size_t pin_bytes = 0;
+};
+}  // namespace host
+}  // namespace symhip
+
+struct sym_ctx {
+    int device = 0;
+    void* ws = nullptr;  // three-kernel decode workspace
+    size_t ws_bytes = 0;
+    void* flags = nullptr;  // default decode's aggregate / prefix words (epoch-tagged)
+    size_t flag_bytes = 0;
+    unsigned epoch = 0;     // tag of the last decode call's look-back words
+    unsigned* err = nullptr;  // [0] device error word (kErr* bits); [1] mixed-encode ticket (zero between calls)
+    // scan workspace of the packetizer, the field getters, the flat decode and the mixed encode
+    // (stream-ordered, so calls on one stream share it)
+    void* frag = nullptr;
+    size_t frag_bytes = 0;
+    // segment cipher: device key schedule + GHASH tables of the last key pair, and that pair
+    void* crypt_tables = nullptr;
+    uint8_t crypt_keys[64] = {0};
+    int num_cus = 0;
+    int decode_impl = SYM_DECODE_PIPELINE;
+    // host-memory entry points: chunk slots (created on first use)
+    symhip::host::Slot slots[symhip::host::kSlots];
+    bool slots_ready = false;
+};
+
+namespace symhip {
+namespace capi {
+int fail(int code, const char* fmt, ...);
+int hip_fail(hipError_t e, const char* what);
+extern const Layout kLayouts[SYM_SCHEMA_COUNT];
+inline bool schema_ok(int schema) { return schema >= 0 && schema < SYM_SCHEMA_COUNT; }
+inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// Runs the body with ctx->device current, restoring the caller's device after.
+struct DeviceGuard {
+    int prev = -1;
+    hipError_t err = hipSuccess;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) err = hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+// sym_encode with every out_off value written offset by out_base (capi.cpp)
+int encode_call(sym_ctx* ctx, int schema, uint64_t n, const int32_t* const* d_fixed, const uint8_t* const* d_bytes,
+                const uint64_t* const* d_offs, uint32_t service_id, uint32_t method_id, uint8_t* d_out,
+                uint64_t* d_out_off, uint64_t out_base, void* stream);
+// one decode of a flat layout; d_type non-null: a mixed kv batch (capi.cpp)
+int decode_call(const char* what, sym_ctx* ctx, Layout lay, const uint8_t* d_type, uint64_t n, const uint8_t* d_in,
+                const uint64_t* d_rec_off, int32_t* const* d_fixed, uint8_t* const* d_bytes, const uint64_t* caps,
+                uint64_t* const* d_offs, uint8_t* d_status, void* stream);
+void host_slots_destroy(sym_ctx* ctx);  // host.cpp
+}  // namespace capi
+}  // namespace symhip

@@ -62,6 +62,8 @@ size_t decode_workspace_bytes(int nvar, uint64_t n) {
 }
 
 // ------------------------------------------------------------------ 1. parse
+// Mixed kv batches (MIX, p.type != null): a record of type 0 is a GetRequest (one string field,
+// kv.syn.go:134-185), any other a SetRequest (two, :680-745).
 // Each lane parses kParseRecs records (tile t's record `lane` for the wave's kParseRecs tiles),
 // in phases so that every record's loads of one kind are in flight together: offsets, then the
 // header windows, then the length prefixes that lie past the window.
@@ -69,7 +71,7 @@ constexpr int kParseRecs = 2;
 template <int NF>
 constexpr int parse_win() { return NF > 0 ? 48 : 32; }  // table + first length prefix fit
 
-template <int NF, int NV>
+template <int NF, int NV, bool MIX>
 __global__ __launch_bounds__(kThreads) void decode_parse_kernel(DecodeParams p, DecodeWs w, u64 tb, u64 te) {
     constexpr int kW = parse_win<NF>();
     constexpr int R = kParseRecs;
@@ -86,6 +88,7 @@ __global__ __launch_bounds__(kThreads) void decode_parse_kernel(DecodeParams p, 
     u64 start[R], len[R];
     bool live[R], win[R];
     u64 endv[R];
+    int nvr[R];
 #pragma unroll
     for (int h = 0; h < R; ++h) {
         const u64 r = (tile0 + h) * kWaveRecs + lane;
@@ -93,6 +96,7 @@ __global__ __launch_bounds__(kThreads) void decode_parse_kernel(DecodeParams p, 
         const u64 rc = live[h] ? r : p.n;  // branch-free loads: rec_off has n+1 entries
         start[h] = p.rec_off[rc];
         endv[h] = p.rec_off[live[h] ? rc + 1 : rc];
+        nvr[h] = MIX ? (p.type[live[h] ? r : 0] != 0 ? NV : 1) : NV;
     }
     __builtin_amdgcn_sched_barrier(0);  // issue every record's offset loads before using any
 #pragma unroll
@@ -155,7 +159,7 @@ __global__ __launch_bounds__(kThreads) void decode_parse_kernel(DecodeParams p, 
                 if (st[h] == 0) {
 #pragma unroll
                     for (int f = 0; f < NV; ++f, toff += 4) {
-                        if (L >= pts + toff + 4) {
+                        if (f < nvr[h] && L >= pts + toff + 4) {
                             u64 q = rd32(pts + toff);
                             if (q > 0) q += off2p;
                             if (q > 0 && L >= q + 4) po[h][f] = q;  // length prefix at q
@@ -412,22 +416,24 @@ __global__ __launch_bounds__(kThreads) void decode_copy_kernel(DecodeParams p, D
 }
 
 // ------------------------------------------------------------------ launch
-template <int NF, int NV>
+template <int NF, int NV, bool MIX>
 static hipError_t launch_layout(const DecodeParams& p, const DecodeWs& w, hipStream_t stream) {
     const u64 ntiles = num_tiles(p.n);
     constexpr u64 kGroup = kWaves * kParseRecs;  // tiles per parse workgroup
     const unsigned pg = (unsigned)((ntiles + kGroup - 1) / kGroup);
     const unsigned cg = (unsigned)((ntiles + kWaves - 1) / kWaves);
-    hipLaunchKernelGGL((decode_parse_kernel<NF, NV>), dim3(pg), dim3(kThreads), 0, stream, p, w, (u64)0, ntiles);
+    hipLaunchKernelGGL((decode_parse_kernel<NF, NV, MIX>), dim3(pg), dim3(kThreads), 0, stream, p, w, (u64)0, ntiles);
     hipLaunchKernelGGL(decode_scan_kernel, dim3(NV), dim3(kScanThreads), 0, stream, p, w, (u64)0, ntiles);
-    if (p.variant != 301)  // 301: timing of parse + scan alone
-        hipLaunchKernelGGL((decode_copy_kernel<NV>), dim3(cg), dim3(kThreads), 0, stream, p, w, (u64)0, ntiles);
+#ifdef SYMHIP_TUNING
+    if (p.variant == 301) return hipGetLastError();  // timing of parse + scan alone
+#endif
+    hipLaunchKernelGGL((decode_copy_kernel<NV>), dim3(cg), dim3(kThreads), 0, stream, p, w, (u64)0, ntiles);
     return hipGetLastError();
 }
 
-// Decode dispatch: the single-launch pipeline (decode_pipe.hip) by default; variants 300/301 run
-// the three-kernel path above (parse -> scan -> copy), kept as a second, independently tested
-// implementation of the same contract.
+// Decode dispatch by the ctx's implementation (sym_ctx_set_decode_impl): the single-launch pipeline
+// (decode_pipe.hip) by default, or its forced look-back mode; kImplThreeKernel runs the path above
+// (parse -> scan -> copy), kept as a second, independently tested implementation of the contract.
 hipError_t launch_decode(const DecodeParams& p, hipStream_t stream) {
     if (p.n == 0) {
         for (int f = 0; f < p.lay.nvar; ++f) {
@@ -436,11 +442,16 @@ hipError_t launch_decode(const DecodeParams& p, hipStream_t stream) {
         }
         return hipSuccess;
     }
-    if (p.variant != 300 && p.variant != 301) return launch_decode_pipe(p, p.flags, p.epoch, stream);
+    bool three = p.impl == kImplThreeKernel;
+#ifdef SYMHIP_TUNING
+    three = three || p.variant == 300 || p.variant == 301;
+#endif
+    if (!three) return launch_decode_pipe(p, p.flags, p.epoch, stream);
     const DecodeWs w = ws_layout(p.ws, p.lay.nvar, p.n);
-    if (p.lay.nfixed == 0 && p.lay.nvar == 1) return launch_layout<0, 1>(p, w, stream);
-    if (p.lay.nfixed == 0 && p.lay.nvar == 2) return launch_layout<0, 2>(p, w, stream);
-    if (p.lay.nfixed == 2 && p.lay.nvar == 2) return launch_layout<2, 2>(p, w, stream);
+    if (p.type) return p.lay.nfixed == 0 && p.lay.nvar == 2 ? launch_layout<0, 2, true>(p, w, stream) : hipErrorInvalidValue;
+    if (p.lay.nfixed == 0 && p.lay.nvar == 1) return launch_layout<0, 1, false>(p, w, stream);
+    if (p.lay.nfixed == 0 && p.lay.nvar == 2) return launch_layout<0, 2, false>(p, w, stream);
+    if (p.lay.nfixed == 2 && p.lay.nvar == 2) return launch_layout<2, 2, false>(p, w, stream);
     return hipErrorInvalidValue;
 }
 

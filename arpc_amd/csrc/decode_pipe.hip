@@ -25,6 +25,18 @@
 // atomics -- the word is its own flag (MI355X_MICROARCH.md visibility, form "R2") -- tagged with the
 // call's epoch so they never need clearing between calls.
 //
+// Progress does not depend on which workgroups are resident.  The fast path assumes the hardware's
+// in-order dispatch (parsers and scanner resident before the copiers that wait on them); a copier
+// whose prefix word has not appeared after kFallbackTicks resolves its prefix itself by a decoupled
+// look-back that never waits: it walks back over earlier tiles' words, and a tile with no published
+// aggregate is parsed from HBM on the spot (its aggregate then published for everyone).  The copier
+// publishes the prefix it found, so later look-backs stop there.  kImplLookback forces this path
+// (parsers and scanner exit at once) so the tests can exercise it.
+//
+// Mixed kv batches (p.type != null, sym_decode_kv_mixed): a record of type 0 is a GetRequest (one
+// string field, kv.syn.go:134-185), any other a SetRequest (two, :680-745); column 1 is empty for
+// GetRequests.
+//
 // Why this shape (measured on MI355X): a separate parse pass costs ~65 us of
 // scattered header reads before any byte moves; an in-kernel decoupled look-back between copiers
 // stalls on cross-XCD round trips (~2 us each) once ~1500 tiles are in flight; parsers that run
@@ -50,7 +62,8 @@ constexpr u64 kStPre = 2ull << 42;
 constexpr u64 kValMask = (1ull << 42) - 1;
 // Bounded waits, in wall time (s_memrealtime runs at 100 MHz): a wait that outlives this reports
 // kErrTimeout (SYM_ERR_DEVICE from sym_ctx_check) and gives up, so the grid always drains.
-constexpr u64 kWaitTicks = 25000000;  // 250 ms
+constexpr u64 kWaitTicks = 25000000;  // 250 ms: the scanner gives up (copiers fall back) after this idle time
+constexpr u64 kFallbackTicks = 100000; // 1 ms: a copier waits this long for its prefix before looking back
 __device__ __forceinline__ u64 now_ticks() { return __builtin_amdgcn_s_memrealtime(); }
 
 __host__ __device__ inline u64 num_tiles(u64 n) { return (n + kRecs - 1) / kRecs; }
@@ -100,7 +113,14 @@ __device__ __forceinline__ u32 win_u32(const u32 (&w)[NW], u32 q) {
 // Step k covers tiles [k*4PR, (k+1)*4PR): wave (b, w) takes R consecutive tiles, lane = record; every
 // load of the R records a lane handles is issued before any is used.  Field lengths follow the same
 // Go checks as the copier's parse (kv.syn.go:681-745), so both publish identical aggregates.
-template <int NF, int NV, int R = 2, int WB = 32>
+// String fields of record r: NV, or 1 for a GetRequest of a mixed kv batch.
+template <int NV, bool MIX>
+__device__ __forceinline__ int rec_nvar(const DecodeParams& p, u64 r) {
+    if constexpr (MIX) return p.type[r] != 0 ? NV : 1;
+    else return NV;
+}
+
+template <int NF, int NV, bool MIX, int R = 2, int WB = 32>
 __device__ void parser(const DecodeParams& p, u64* aw, u64 ntiles, u32 epoch, u32 P) {
     constexpr int NW = WB / 4;  // window dwords
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -109,6 +129,7 @@ __device__ void parser(const DecodeParams& p, u64* aw, u64 ntiles, u32 epoch, u3
     for (u64 t0 = ((u64)blockIdx.x * 4 + wave) * R; t0 < ntiles; t0 += (u64)P * 4 * R) {
         bool live[R], win[R];
         u64 start[R], L[R];
+        int nvr[R];
         u32 w[R][NW];
 #pragma unroll
         for (int h = 0; h < R; ++h) {
@@ -117,6 +138,7 @@ __device__ void parser(const DecodeParams& p, u64* aw, u64 ntiles, u32 epoch, u3
             const u64 rc = live[h] ? r : n;
             start[h] = p.rec_off[rc];
             L[h] = p.rec_off[live[h] ? rc + 1 : rc] - start[h];
+            nvr[h] = rec_nvar<NV, MIX>(p, live[h] ? r : 0);
         }
 #pragma unroll
         for (int h = 0; h < R; ++h) {
@@ -156,7 +178,7 @@ __device__ void parser(const DecodeParams& p, u64* aw, u64 ntiles, u32 epoch, u3
 #pragma unroll
                         for (int f = 0; f < NV; ++f) {
                             const u64 te = vt + 4 * (u64)f;
-                            if (Lh >= te + 4) {
+                            if (f < nvr[h] && Lh >= te + 4) {
                                 u64 q = rd32(te);
                                 if (q > 0) q += off2p;
                                 if (q > 0 && Lh >= q + 4) {
@@ -186,7 +208,7 @@ __device__ void parser(const DecodeParams& p, u64* aw, u64 ntiles, u32 epoch, u3
 // yet published (the frontier), and publishes the exclusive prefix of every tile before it.  A
 // tile's prefix so depends only on earlier tiles, whoever published their aggregates.
 template <int NV, int SK, typename LdsT>
-__device__ void scanner(u64* aw, u64* pw, u64 ntiles, u32 epoch, unsigned* err, LdsT& S) {
+__device__ void scanner(u64* aw, u64* pw, u64 ntiles, u32 epoch, LdsT& S) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     constexpr int kPer = SK;  // tiles per thread per step
     constexpr u64 kStep = (u64)kThreads * kPer;
@@ -220,10 +242,7 @@ __device__ void scanner(u64* aw, u64* pw, u64 ntiles, u32 epoch, unsigned* err, 
         if (m == 0) {  // the frontier has not moved: wait a little (bounded)
             const u64 t = uniform_i64((i64)now_ticks());
             if (idle_since == 0) idle_since = t;
-            if (t - idle_since > kWaitTicks) {
-                if (tid == 0) atomicOr(err, kErrTimeout);
-                return;
-            }
+            if (t - idle_since > kWaitTicks) return;  // the copiers resolve the rest by look-back
             __builtin_amdgcn_s_sleep(2);
             continue;
         }
@@ -259,11 +278,103 @@ __device__ void scanner(u64* aw, u64* pw, u64 ntiles, u32 epoch, unsigned* err, 
     }
 }
 
+// ---------------------------------------------------------------- look-back (the fallback)
+// Field lengths of record r with Go's checks (kv.syn.go:681-745, echo.syn.go:223-231), read straight
+// from HBM: the same values the parsers and the copiers' parse compute.
+template <int NF, int NV, bool MIX>
+__device__ void record_flen_global(const DecodeParams& p, u64 r, u64 (&flen)[NV]) {
+#pragma unroll
+    for (int f = 0; f < NV; ++f) flen[f] = 0;
+    const u64 start = p.rec_off[r], L = p.rec_off[r + 1] - start;
+    const uintptr_t A = (uintptr_t)p.in + start;
+    if (L < 13 || ld_u8(A) != 0x01) return;
+    const u64 off2p = *(gc_u32*)(A + 1);  // unaligned OK
+    if (off2p >= L || ld_u8(A + off2p) != 0x01) return;
+    const u64 vt = off2p + 1 + 4 * (u64)NF;  // var table: only if every int32 field fits
+    if (L < vt) return;
+    const int nvr = rec_nvar<NV, MIX>(p, r);
+#pragma unroll
+    for (int f = 0; f < NV; ++f) {
+        const u64 te = vt + 4 * (u64)f;
+        if (f < nvr && L >= te + 4) {
+            u64 q = *(gc_u32*)(A + te);
+            if (q > 0) q += off2p;
+            if (q > 0 && L >= q + 4) {
+                const u64 nb = *(gc_u32*)(A + q);
+                if (L >= q + 4 + nb) flen[f] = nb;
+            }
+        }
+    }
+}
+
+// Per-column aggregate of `tile` (whole wave, lane = record; wave-uniform result).
+template <int NF, int NV, bool MIX>
+__device__ void tile_agg_global(const DecodeParams& p, u64 tile, u64 (&agg)[NV]) {
+    const int lane = threadIdx.x & 63;
+    const u64 r = tile * kRecs + lane;
+    u64 flen[NV];
+    if (r < p.n) {
+        record_flen_global<NF, NV, MIX>(p, r, flen);
+    } else {
+#pragma unroll
+        for (int f = 0; f < NV; ++f) flen[f] = 0;
+    }
+#pragma unroll
+    for (int f = 0; f < NV; ++f) agg[f] = (u64)uniform_i64((i64)wave_sum_u64(flen[f]));
+}
+
+// Exclusive prefix of `tile` per column (wave 0 of its copier; lane k looks at tile hi - k).  The
+// nearest earlier tile with a published prefix word ends the walk: prefix = its prefix + its
+// aggregate + the aggregates of the tiles in between.  Never waits: a missing aggregate is computed
+// here and published.
+template <int NF, int NV, bool MIX>
+__device__ void lookback(const DecodeParams& p, u64* aw, u64* pw, u64 ntiles, u64 tile, u32 epoch, i64 (&pre)[NV]) {
+    const int lane = threadIdx.x & 63;
+    u64 sum[NV];
+#pragma unroll
+    for (int f = 0; f < NV; ++f) sum[f] = 0;
+    for (i64 hi = (i64)tile - 1; hi >= 0; hi -= 64) {  // wave-uniform loop
+        const i64 t = hi - lane;
+        const bool valid = t >= 0;
+        u64 pv[NV], av[NV];
+        bool hp = valid, ha = valid;
+#pragma unroll
+        for (int f = 0; f < NV; ++f) {
+            pv[f] = valid ? load_word(&pw[(size_t)f * ntiles + t]) : 0;
+            av[f] = valid ? load_word(&aw[(size_t)f * ntiles + t]) : 0;
+            hp = hp && tagged(pv[f], epoch);
+            ha = ha && tagged(av[f], epoch);
+        }
+        const u64 pm = __ballot(hp);
+        const int stop = pm ? (int)__builtin_ctzll(pm) : 64;  // lanes [0, stop] contribute
+        u64 need = __ballot(valid && lane <= stop && !ha);
+        while (need) {  // wave-uniform
+            const int k = (int)__builtin_ctzll(need);
+            need &= need - 1;
+            u64 a[NV];
+            tile_agg_global<NF, NV, MIX>(p, (u64)(hi - k), a);
+#pragma unroll
+            for (int f = 0; f < NV; ++f) {
+                if (lane == k) av[f] = make_word(epoch, kStAgg, a[f]);
+                if (lane == 0) store_word(&aw[(size_t)f * ntiles + (u64)(hi - k)], make_word(epoch, kStAgg, a[f]));
+            }
+        }
+#pragma unroll
+        for (int f = 0; f < NV; ++f) {
+            const u64 c = valid && lane <= stop ? (av[f] & kValMask) + (lane == stop ? pv[f] & kValMask : 0) : 0;
+            sum[f] += (u64)uniform_i64((i64)wave_sum_u64(c));
+        }
+        if (pm) break;
+    }
+#pragma unroll
+    for (int f = 0; f < NV; ++f) pre[f] = (i64)sum[f];
+}
+
 // ---------------------------------------------------------------- the kernel
 // MODE 0: the pipeline.  MODE 1: copiers only, every prefix taken as 0 (timing of the data movement
 // alone; wrong output -- tools/kbench.py variant 402).  DIAG: per-tile phase timestamps into p.dbg
 // (8 u64 per tile, s_memrealtime at 100 MHz; tools/fused_timeline.py).
-template <int NF, int NV, int MODE = 0, int DIAG = 0, int SK = 4, int PR = 2>
+template <int NF, int NV, bool MIX, int MODE = 0, int DIAG = 0, int SK = 4, int PR = 2>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))) void decode_pipe_kernel(
     DecodeParams p, u64* flags, u32 epoch) {
     static_assert(NV == 1 || NV == 2, "decode handles one or two string columns");
@@ -279,12 +390,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
     u64* pw = flags + (size_t)NV * ntiles;    // prefix words [NV][ntiles]
 
     const u32 P = p.pipe_parsers;
+    const bool forced = p.impl == kImplLookback;  // parsers and scanner idle: look-back only
     if (MODE == 0 && blockIdx.x < P) {
-        parser<NF, NV, PR>(p, aw, ntiles, epoch, P);
+        if (!forced) parser<NF, NV, MIX, PR>(p, aw, ntiles, epoch, P);
         return;
     }
     if (MODE == 0 && blockIdx.x == P) {
-        scanner<NV, SK>(aw, pw, ntiles, epoch, p.err, S);
+        if (!forced) scanner<NV, SK>(aw, pw, ntiles, epoch, S);
         return;
     }
     const u64 tile = MODE == 0 ? blockIdx.x - P - 1 : blockIdx.x;
@@ -341,6 +453,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
         u64 flen[NV], fpos[NV];
 #pragma unroll
         for (int f = 0; f < NV; ++f) flen[f] = fpos[f] = 0;
+        const int nvr = rec_nvar<NV, MIX>(p, live ? r0 + lane : 0);
         if (live) {
             if (L < 13) {
                 st = SYM_STATUS_TOO_SHORT;  // "invalid data: too short" (kv.syn.go:681-683)
@@ -363,7 +476,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
                     if (st == 0) {
 #pragma unroll
                         for (int f = 0; f < NV; ++f, toff += 4) {  // kv.syn.go:717-742
-                            if (L >= pts + toff + 4) {
+                            if (f < nvr && L >= pts + toff + 4) {
                                 u64 q = rd32(pts + toff);
                                 if (q > 0) q += off2p;
                                 if (q > 0 && L >= q + 4) {
@@ -401,23 +514,29 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
         i64 pre[NV];
         if constexpr (MODE == 0) {
             u64 wv = 0;
+            bool got = true;
             if (lane < NV) {
                 // this tile's aggregate (a parser may have published the same value), then its prefix
                 store_word(&aw[(size_t)lane * ntiles + tile], make_word(epoch, kStAgg, lane == 0 ? agg[0] : agg[NV - 1]));
                 u64* a = &pw[(size_t)lane * ntiles + tile];
                 wv = load_word(a);
-                for (const u64 t0 = now_ticks(); !tagged(wv, epoch);) {
-                    if (now_ticks() - t0 > kWaitTicks) {
-                        atomicOr(p.err, kErrTimeout);
-                        wv = make_word(epoch, kStPre, 0);
-                        break;
+                if (!forced) {
+                    for (const u64 t0 = now_ticks(); !tagged(wv, epoch) && now_ticks() - t0 <= kFallbackTicks;) {
+                        __builtin_amdgcn_s_sleep(2);
+                        wv = load_word(a);
                     }
-                    __builtin_amdgcn_s_sleep(2);
-                    wv = load_word(a);
                 }
+                got = tagged(wv, epoch);
             }
-            pre[0] = (i64)((u64)__shfl((long long)wv, 0, 64) & kValMask);
-            if constexpr (NV == 2) pre[1] = (i64)((u64)__shfl((long long)wv, 1, 64) & kValMask);
+            if (__ballot(!got)) {  // no prefix from the scanner: resolve it here (never waits)
+                lookback<NF, NV, MIX>(p, aw, pw, ntiles, tile, epoch, pre);
+#pragma unroll
+                for (int f = 0; f < NV; ++f)
+                    if (lane == 0) store_word(&pw[(size_t)f * ntiles + tile], make_word(epoch, kStPre, (u64)pre[f]));
+            } else {
+                pre[0] = (i64)((u64)__shfl((long long)wv, 0, 64) & kValMask);
+                if constexpr (NV == 2) pre[1] = (i64)((u64)__shfl((long long)wv, 1, 64) & kValMask);
+            }
         } else {  // timing only: spread the tiles over the columns in proportion to their stream offset
             const double frac = (double)(s0 - p.rec_off[0]) / (double)(p.rec_off[n] - p.rec_off[0] + 1);
 #pragma unroll
@@ -520,9 +639,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
         if (tid == 0) p.dbg[tile * 8 + 5] = blockIdx.x;
 }
 
-template <int NF, int NV, int MODE, int DIAG, int SK = 4, int PR = 2>
+template <int NF, int NV, bool MIX, int MODE, int DIAG, int SK = 4, int PR = 2>
 hipError_t launch(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stream, int pnum = 1, int pden = 1) {
-    if (DIAG && !p.dbg) return hipErrorInvalidValue;  // timestamps need SYMHIP_DEBUG_PTR
+    if (DIAG && !p.dbg) return hipErrorInvalidValue;  // timestamps need SYMHIP_DEBUG_PTR (tuning builds)
     static int cus[16] = {0};
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
@@ -530,13 +649,13 @@ hipError_t launch(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stre
     int& ncu = cus[dev & 15];
     if (ncu == 0 && (e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
     const u64 nt = num_tiles(p.n);
-    u64 P = MODE == 0 ? (u64)ncu * pnum / pden : 0;  // one parser workgroup per CU (tuning: pnum / pden)
+    u64 P = MODE == 0 ? (u64)ncu * pnum / pden : 0;  // parser workgroups: pnum / pden per CU
     if (P > (nt + 3) / 4) P = (nt + 3) / 4;
     DecodeParams q = p;
     q.pipe_parsers = (unsigned)P;
     const u64 grid = MODE == 0 ? P + 1 + nt : nt;
-    hipLaunchKernelGGL((decode_pipe_kernel<NF, NV, MODE, DIAG, SK, PR>), dim3((unsigned)grid), dim3(kThreads), 0, stream,
-                       q, flags, epoch);
+    hipLaunchKernelGGL((decode_pipe_kernel<NF, NV, MIX, MODE, DIAG, SK, PR>), dim3((unsigned)grid), dim3(kThreads), 0,
+                       stream, q, flags, epoch);
     return hipGetLastError();
 }
 
@@ -545,10 +664,16 @@ constexpr int kParsersNum = 3;   // parser workgroups = #CUs * 3/4
 constexpr int kParsersDen = 4;
 
 template <int MODE, int DIAG, int SK = kScanPer, int PR = 2>
-hipError_t launch_layout(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stream, int pnum = 1, int pden = 1) {
-    if (p.lay.nfixed == 0 && p.lay.nvar == 1) return launch<0, 1, MODE, DIAG, SK, PR>(p, flags, epoch, stream, pnum, pden);
-    if (p.lay.nfixed == 0 && p.lay.nvar == 2) return launch<0, 2, MODE, DIAG, SK, PR>(p, flags, epoch, stream, pnum, pden);
-    if (p.lay.nfixed == 2 && p.lay.nvar == 2) return launch<2, 2, MODE, DIAG, SK, PR>(p, flags, epoch, stream, pnum, pden);
+hipError_t launch_layout(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stream, int pnum = kParsersNum,
+                         int pden = kParsersDen) {
+    if (p.type) {  // mixed kv batch: GetRequest / SetRequest per record
+        if (p.lay.nfixed == 0 && p.lay.nvar == 2)
+            return launch<0, 2, true, MODE, DIAG, SK, PR>(p, flags, epoch, stream, pnum, pden);
+        return hipErrorInvalidValue;
+    }
+    if (p.lay.nfixed == 0 && p.lay.nvar == 1) return launch<0, 1, false, MODE, DIAG, SK, PR>(p, flags, epoch, stream, pnum, pden);
+    if (p.lay.nfixed == 0 && p.lay.nvar == 2) return launch<0, 2, false, MODE, DIAG, SK, PR>(p, flags, epoch, stream, pnum, pden);
+    if (p.lay.nfixed == 2 && p.lay.nvar == 2) return launch<2, 2, false, MODE, DIAG, SK, PR>(p, flags, epoch, stream, pnum, pden);
     return hipErrorInvalidValue;
 }
 
@@ -559,38 +684,31 @@ size_t decode_pipe_flag_bytes(int nvar, uint64_t n) {
     return ((size_t)nvar * 2 * pipe::num_tiles(n) * sizeof(u64) + 256 + 255) & ~(size_t)255;
 }
 
-// variants: 0 the pipeline; 402 data movement only (timing, wrong output); 410 / 412 the same with
-// per-tile timestamps (SYMHIP_DEBUG_PTR)
+// The pipeline: 512-tile scanner steps, parsers on 3/4 of the CUs (tools/kbench.py sweep).
+// Tuning builds (make tuning) add the measurement variants: 402 data movement only (copiers without
+// the scan: WRONG output, a timing bound), 410 / 412 per-tile timestamps, 43x-46x geometry sweeps.
 hipError_t launch_decode_pipe(const DecodeParams& p, void* flags, unsigned epoch, hipStream_t stream) {
     u64* fl = (u64*)flags;
+#ifdef SYMHIP_TUNING
     switch (p.variant) {
         case 402: return pipe::launch_layout<1, 0>(p, fl, epoch, stream);
-        case 410: return pipe::launch_layout<0, 1>(p, fl, epoch, stream, pipe::kParsersNum, pipe::kParsersDen);
+        case 410: return pipe::launch_layout<0, 1>(p, fl, epoch, stream);
         case 412: return pipe::launch_layout<1, 1>(p, fl, epoch, stream);
-        // tuning experiments (tools/kbench.py): parser count and scanner step size
         case 431: return pipe::launch_layout<0, 0>(p, fl, epoch, stream, 1, 2);
         case 432: return pipe::launch_layout<0, 0>(p, fl, epoch, stream, 2, 1);
         case 433: return pipe::launch_layout<0, 0>(p, fl, epoch, stream, 1, 4);
         case 434: return pipe::launch_layout<0, 0>(p, fl, epoch, stream, 3, 2);
-        case 435: return pipe::launch_layout<0, 0>(p, fl, epoch, stream, 3, 4);
         case 440: return pipe::launch_layout<0, 0, 8>(p, fl, epoch, stream);
-        case 442: return pipe::launch_layout<0, 0, 2>(p, fl, epoch, stream);
         case 443: return pipe::launch_layout<0, 0, 1>(p, fl, epoch, stream);
-        case 444: return pipe::launch_layout<0, 0, 2>(p, fl, epoch, stream, 3, 4);
-        case 445: return pipe::launch_layout<0, 0, 2>(p, fl, epoch, stream, 7, 8);
         case 446: return pipe::launch_layout<0, 0, 3>(p, fl, epoch, stream);
         case 447: return pipe::launch_layout<0, 0, 2>(p, fl, epoch, stream, 5, 8);
-        case 448: return pipe::launch_layout<0, 0, 2>(p, fl, epoch, stream, 9, 16);
         case 449: return pipe::launch_layout<0, 0, 2>(p, fl, epoch, stream, 11, 16);
-        case 450: return pipe::launch_layout<0, 0, 2>(p, fl, epoch, stream, 1, 2);
-        case 460: return pipe::launch_layout<0, 0, 2, 1>(p, fl, epoch, stream, 3, 4);
-        case 461: return pipe::launch_layout<0, 0, 2, 4>(p, fl, epoch, stream, 3, 4);
-        case 462: return pipe::launch_layout<0, 0, 2, 1>(p, fl, epoch, stream, 3, 2);
-        case 463: return pipe::launch_layout<0, 0, 2, 4>(p, fl, epoch, stream, 3, 8);
-        case 430: return pipe::launch_layout<0, 0, 4>(p, fl, epoch, stream, 1, 1);  // round-1 tuning
-        // default: 512-tile scanner steps, parsers on 3/4 of the CUs (tools/kbench.py sweep)
-        default: return pipe::launch_layout<0, 0, pipe::kScanPer>(p, fl, epoch, stream, pipe::kParsersNum, pipe::kParsersDen);
+        case 460: return pipe::launch_layout<0, 0, 2, 1>(p, fl, epoch, stream);
+        case 461: return pipe::launch_layout<0, 0, 2, 4>(p, fl, epoch, stream);
+        default: break;
     }
+#endif
+    return pipe::launch_layout<0, 0>(p, fl, epoch, stream);
 }
 
 }  // namespace symhip

@@ -44,12 +44,17 @@ struct EncWaveLds {
     u32 len[NV][kWaveRecs];
     u64 delta[NV][kWaveRecs];          // payload byte address = delta + chunk position
     uint8_t flags[64];                 // record-start marks of one phase-2 step
+    uint8_t h0[kWaveRecs];             // mixed batches: the record's bytes before field 0's payload
 };
 
-template <int NF, int NV, int kVariant>
+// MIXED: a kv batch of GetRequests (type 0: 22 + K bytes, kv.syn.go:74-132) and SetRequests (else:
+// 30 + K + V bytes, :611-678); the layout constants below are the SetRequest's, and every per-record
+// difference (header image, table, where the key payload starts, no value) is taken per record.
+template <int NF, int NV, int kVariant, bool MIXED = false>
 __global__ __launch_bounds__(256) void encode_kernel(EncodeParams p) {
+    static_assert(!MIXED || (NF == 0 && NV == 2 && kVariant == 0), "mixed batches are kv Get/Set");
     constexpr int NT = NF + NV;
-    constexpr int H0 = 14 + 4 * NT + 4;        // bytes before field 0's payload
+    constexpr int H0 = 14 + 4 * NT + 4;        // bytes before field 0's payload (the largest, in mixed batches)
     constexpr i64 OVH = 14 + 4 * NT + 4 * NV;  // fixed bytes per record
     constexpr int SLOT = slot_bytes(H0);
     static_assert(SLOT - 16 >= H0 && OVH >= 16, "layout assumptions");
@@ -68,7 +73,29 @@ __global__ __launch_bounds__(256) void encode_kernel(EncodeParams p) {
     // ---------------- phase 1: per-record offsets and header image ----------------
     i64 o = 0, size = 0;
     u64 L[NV];
-    if (lane < cnt) {
+    bool isset = true;  // mixed batches: SetRequest (else GetRequest)
+    if constexpr (MIXED) {
+        // sizes depend on the type: the size pass's tile prefix plus a wave scan of this tile's sizes
+#pragma unroll
+        for (int f = 0; f < NV; ++f) L[f] = 0;
+        if (lane < cnt) {
+            const u64 r = r0 + lane;
+            isset = p.type[r] != 0;
+            L[0] = p.offs[0][r + 1] - p.offs[0][r];
+            if (isset) L[1] = p.offs[1][r + 1] - p.offs[1][r];
+            size = (i64)(22 + L[0] + (isset ? 8 + L[1] : 0));
+        }
+        const u64 tile = r0 / kWaveRecs;
+        const i64 tp = uniform_i64((i64)(p.group_pre[tile >> 6] + p.tile_loc[tile]));
+        o = tp + (i64)(wave_incl_scan_u64((u64)size, lane) - (u64)size);
+        if (lane < cnt) {
+            const u64 r = r0 + lane;
+#pragma unroll
+            for (int f = 0; f < NV; ++f) S.len[f][lane] = (u32)L[f];
+            p.out_off[r] = p.out_base + (u64)o;
+            if (r == p.n - 1) p.out_off[p.n] = p.out_base + (u64)(o + size);
+        }
+    } else if (lane < cnt) {
         const u64 r = r0 + lane;
         o = (i64)r * OVH;
         size = OVH;
@@ -80,8 +107,8 @@ __global__ __launch_bounds__(256) void encode_kernel(EncodeParams p) {
             size += (i64)L[f];
             S.len[f][lane] = (u32)L[f];
         }
-        p.out_off[r] = (u64)o;
-        if (r == p.n - 1) p.out_off[p.n] = (u64)(o + size);
+        p.out_off[r] = p.out_base + (u64)o;
+        if (r == p.n - 1) p.out_off[p.n] = p.out_base + (u64)(o + size);
     }
     // wave-uniform: readfirstlane keeps them (and the phase-2 loop bounds) in SGPRs
     const i64 T0 = uniform_i64((i64)__shfl((long long)o, 0, 64));
@@ -95,7 +122,8 @@ __global__ __launch_bounds__(256) void encode_kernel(EncodeParams p) {
         const int orel = (int)(o - T0);
         S.o[lane] = orel;
         if (lane == cnt - 1) S.o[cnt] = (int)(T1 - T0);
-        int ps = H0;
+        const int h0 = MIXED && !isset ? 22 : H0;
+        int ps = h0;
 #pragma unroll
         for (int f = 0; f < NV; ++f) {
             S.delta[f][lane] = (u64)(uintptr_t)(p.bytes[f] + p.offs[f][r]) - (u64)(i64)(orel + ps);
@@ -108,15 +136,21 @@ __global__ __launch_bounds__(256) void encode_kernel(EncodeParams p) {
         img_put_u8<0>(h, 1);
         img_put_u32<1>(h, 13);
         img_put_u32<5>(h, p.service_id);
-        img_put_u32<9>(h, p.method_id);
+        img_put_u32<9>(h, MIXED && !isset ? p.method_get : p.method_id);
         img_put_u8<13>(h, 1);
         if constexpr (NF > 0) img_put_u32<14>(h, (u32)p.fixed[0][r]);
         if constexpr (NF > 1) img_put_u32<18>(h, (u32)p.fixed[1][r]);
         // private-table entries: offset of the field's length prefix relative to privateStart
         // (13), truncated to u32 (kv.syn.go:664, :671).
-        img_put_u32<14 + 4 * NF>(h, (u32)(H0 - 4 - 13));
-        if constexpr (NV > 1) img_put_u32<18 + 4 * NF>(h, (u32)(H0 + L[0] + 4 - 4 - 13));
-        img_put_u32<H0 - 4>(h, (u32)L[0]);
+        if (MIXED && !isset) {  // GetRequest{Key} (kv.syn.go:119-127)
+            img_put_u32<14>(h, 5u);
+            img_put_u32<18>(h, (u32)L[0]);
+        } else {
+            img_put_u32<14 + 4 * NF>(h, (u32)(H0 - 4 - 13));
+            if constexpr (NV > 1) img_put_u32<18 + 4 * NF>(h, (u32)(H0 + L[0] + 4 - 4 - 13));
+            img_put_u32<H0 - 4>(h, (u32)L[0]);
+        }
+        if constexpr (MIXED) S.h0[lane] = (uint8_t)h0;
         uint2* slot = (uint2*)&S.hdr[(lane + 1) * SLOT];
 #pragma unroll
         for (int k = 0; k < SLOT / 8; ++k) slot[k] = make_uint2(h[2 * k], h[2 * k + 1]);
@@ -162,7 +196,8 @@ __global__ __launch_bounds__(256) void encode_kernel(EncodeParams p) {
     auto chunk = [&](int P, int j, bool careful) {
         const int oj = S.o[j];
         const int b = P - oj;  // chunk start relative to record j (> -16)
-        int t = H0 - b;        // chunk offset where field 0's payload starts
+        const int h0j = MIXED ? (int)S.h0[j] : H0;
+        int t = h0j - b;       // chunk offset where field 0's payload starts
         int Lf[NV];
         uintptr_t X[NV];
         bool need[NV], fast[NV];
@@ -171,7 +206,7 @@ __global__ __launch_bounds__(256) void encode_kernel(EncodeParams p) {
         for (int f = 0; f < NV; ++f) {
             Lf[f] = (int)S.len[f][j];
             X[f] = (uintptr_t)(S.delta[f][j] + (u64)(i64)P);
-            need[f] = t < 16 && t + Lf[f] > 0;
+            need[f] = t < 16 && t + Lf[f] > 0 && (!MIXED || Lf[f] > 0);  // a GetRequest has no value
             fast[f] = need[f];
             if (careful) {  // the 16-byte window must lie inside the column's 16-byte-rounded extent
                 const uintptr_t c0 = (uintptr_t)(p.bytes[f] + p.offs[f][0]) & ~(uintptr_t)15;
@@ -182,8 +217,8 @@ __global__ __launch_bounds__(256) void encode_kernel(EncodeParams p) {
             t += Lf[f] + 4;
         }
         u32x4 r = {0, 0, 0, 0};
-        if (b < H0) r = lds16u(S.hdr, (j + 1) * SLOT + b);
-        t = H0 - b;
+        if (b < H0) r = lds16u(S.hdr, (j + 1) * SLOT + b);  // a GetRequest's slot is zero past its 22 bytes
+        t = h0j - b;
 #pragma unroll
         for (int f = 0; f < NV; ++f) {
             if (f > 0 && t > 0 && t < 20) {  // inner length prefix of field f at [t-4, t)
@@ -280,13 +315,16 @@ __global__ __launch_bounds__(256) void encode_kernel(EncodeParams p) {
 
 template <int NF, int NV>
 static void launch_layout(const EncodeParams& p, dim3 grid, dim3 block, hipStream_t stream) {
+#ifdef SYMHIP_TUNING
     // variants 2/4: that many steps' loads in flight per wave (measured no faster on MI355X: the
     // one-step loop already runs at ~92 % of a plain 350 MB copy, tools/ubench_copy.hip)
     switch (p.variant) {
-        case 2: hipLaunchKernelGGL((encode_kernel<NF, NV, 2>), grid, block, 0, stream, p); break;
-        case 4: hipLaunchKernelGGL((encode_kernel<NF, NV, 4>), grid, block, 0, stream, p); break;
-        default: hipLaunchKernelGGL((encode_kernel<NF, NV, 0>), grid, block, 0, stream, p); break;
+        case 2: hipLaunchKernelGGL((encode_kernel<NF, NV, 2>), grid, block, 0, stream, p); return;
+        case 4: hipLaunchKernelGGL((encode_kernel<NF, NV, 4>), grid, block, 0, stream, p); return;
+        default: break;
     }
+#endif
+    hipLaunchKernelGGL((encode_kernel<NF, NV, 0>), grid, block, 0, stream, p);
 }
 
 hipError_t launch_encode(const EncodeParams& p, hipStream_t stream) {
@@ -302,6 +340,124 @@ hipError_t launch_encode(const EncodeParams& p, hipStream_t stream) {
         launch_layout<2, 2>(p, grid, block, stream);
     else
         return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- mixed Get/Set batches
+// Record sizes depend on the type column, so record offsets are a scan.  The size pass reads the
+// type bytes and the value offsets (Σ over Sets of 8 + V; keys contribute 22 + K per record, taken
+// from the key offsets at tile edges) and writes, per 64-record tile, its exclusive size prefix
+// inside its group of kGroupTiles tiles, and per group its total.  The last workgroup to finish
+// (ticket) scans the group totals.  The encode kernel starts tile t at group_pre[t/64] + tile_loc[t].
+constexpr int kGroupTiles = 64;                 // tiles per size-pass workgroup (4096 records)
+constexpr int kTilesPerWave = kGroupTiles / 4;  // 16
+
+struct MixedWs {
+    u64* group_pre;
+    u64* tile_loc;
+    u64* group_tot;
+};
+__host__ __device__ static inline u64 mixed_ntiles(u64 n) { return (n + kWaveRecs - 1) / kWaveRecs; }
+__host__ __device__ static inline u64 mixed_ngroups(u64 n) { return (mixed_ntiles(n) + kGroupTiles - 1) / kGroupTiles; }
+static MixedWs mixed_layout(void* ws, u64 n) {
+    MixedWs w;
+    w.group_pre = (u64*)ws;
+    w.group_tot = w.group_pre + mixed_ngroups(n);
+    w.tile_loc = w.group_tot + mixed_ngroups(n);
+    return w;
+}
+size_t encode_mixed_ws_bytes(uint64_t n) { return (size_t)(2 * mixed_ngroups(n) + mixed_ntiles(n)) * 8; }
+
+__global__ __launch_bounds__(256) void mixed_size_kernel(EncodeParams p, MixedWs w, unsigned* ticket) {
+    __shared__ u64 s_agg[kGroupTiles];
+    __shared__ u64 s_wsum[4];
+    __shared__ int s_last;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const u64 n = p.n, ntiles = mixed_ntiles(n), g = blockIdx.x;
+    const u64 t0 = g * kGroupTiles + (u64)wave * kTilesPerWave;  // this wave's first tile
+    // every load of the wave's 16 tiles in flight before any is used (clamped, unconditional)
+    uint8_t ty[kTilesPerWave];
+    u64 v0[kTilesPerWave], v1[kTilesPerWave];
+#pragma unroll
+    for (int k = 0; k < kTilesPerWave; ++k) {
+        const u64 r = min((t0 + k) * kWaveRecs + lane, n - 1);
+        ty[k] = p.type[r];
+        v0[k] = p.offs[1][r];
+        v1[k] = p.offs[1][r + 1];
+    }
+#pragma unroll
+    for (int k = 0; k < kTilesPerWave; ++k) {
+        const u64 t = t0 + k, r = t * kWaveRecs + lane;
+        const u64 extra = r < n && ty[k] != 0 ? 8 + (v1[k] - v0[k]) : 0;
+        const u64 sum = wave_sum_u64(extra);
+        if (lane == 0) {
+            u64 agg = 0;
+            if (t < ntiles) {
+                const u64 a = t * kWaveRecs, b = min(a + kWaveRecs, n);
+                agg = 22 * (b - a) + (p.offs[0][b] - p.offs[0][a]) + sum;
+            }
+            s_agg[wave * kTilesPerWave + k] = agg;
+        }
+    }
+    __syncthreads();
+    if (wave == 0) {
+        const u64 v = s_agg[lane];
+        const u64 inc = wave_incl_scan_u64(v, lane);
+        const u64 t = g * kGroupTiles + lane;
+        if (t < ntiles) w.tile_loc[t] = inc - v;
+        if (lane == 63) __hip_atomic_store(&w.group_tot[g], inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (tid == 0) {  // release this group's total, acquire everyone's when last
+        const unsigned tk = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = tk == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    // last workgroup: exclusive scan of the group totals, 16 per thread per round
+    const u64 ng = gridDim.x;
+    u64 carry = 0;
+    for (u64 base = 0; base < ng; base += 256 * 16) {
+        u64 v[16], sum = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const u64 i = base + (u64)tid * 16 + k;
+            v[k] = i < ng ? __hip_atomic_load(&w.group_tot[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+            sum += v[k];
+        }
+        const u64 inc = wave_incl_scan_u64(sum, lane);
+        if (lane == 63) s_wsum[wave] = inc;
+        __syncthreads();
+        u64 wpre = 0, tot = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (q < wave) wpre += s_wsum[q];
+            tot += s_wsum[q];
+        }
+        __syncthreads();
+        u64 run = carry + wpre + inc - sum;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const u64 i = base + (u64)tid * 16 + k;
+            if (i < ng) w.group_pre[i] = run;
+            run += v[k];
+        }
+        carry += tot;
+    }
+    if (tid == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next call
+}
+
+// `ticket`: a device word that is zero between calls (the last workgroup resets it).
+hipError_t launch_encode_mixed(EncodeParams p, void* ws, unsigned* ticket, hipStream_t stream) {
+    if (p.n == 0) return hipMemsetAsync(p.out_off, 0, sizeof(uint64_t), stream);
+    if (!p.type || p.lay.nfixed != 0 || p.lay.nvar != 2) return hipErrorInvalidValue;
+    const MixedWs w = mixed_layout(ws, p.n);
+    hipLaunchKernelGGL(mixed_size_kernel, dim3((unsigned)mixed_ngroups(p.n)), dim3(256), 0, stream, p, w, ticket);
+    p.group_pre = w.group_pre;
+    p.tile_loc = w.tile_loc;
+    const u64 tiles = mixed_ntiles(p.n);
+    hipLaunchKernelGGL((encode_kernel<0, 2, 0, true>), dim3((unsigned)((tiles + kWaves - 1) / kWaves)), dim3(64 * kWaves),
+                       0, stream, p);
     return hipGetLastError();
 }
 

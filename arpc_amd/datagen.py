@@ -97,6 +97,45 @@ CONFIG2 = dict(schema="kv_set_request", n=1 << 20, lens=(64, 256), seed=0x5EED00
 CONFIG3 = dict(schema="kv_set_request", n=1 << 20, lens=(64, ("loguniform", 16, 4096)), seed=0x5EED0002)
 
 
+# BASELINE config 2's Get/Set mix: the SET share of benchmark/meta-kv-trace/trace_large.req
+# (9,267 SET of 25,125 requests, 36.9 %).
+TRACE_SET_FRACTION = 9267 / 25125
+CONFIG2_MIXED = dict(n=1 << 20, key=64, value=256, set_fraction=TRACE_SET_FRACTION, seed=0x5EED0001)
+
+
+@dataclass
+class MixedBatch:
+    type: np.ndarray  # u8 [n]: 0 GetRequest, 1 SetRequest
+    key: tuple        # (u8 bytes, u64 offs [n+1])
+    val: tuple        # (u8 bytes, u64 offs [n+1]); empty slices for GetRequests
+
+    @property
+    def n(self) -> int:
+        return len(self.type)
+
+    def encoded_size(self) -> int:
+        kl = int(self.key[1][-1] - self.key[1][0])
+        vl = int(self.val[1][-1] - self.val[1][0])
+        return 22 * self.n + 8 * int((self.type != 0).sum()) + kl + vl
+
+
+def make_mixed_batch(n: int, key, value, set_fraction: float, seed: int, **_ignored) -> MixedBatch:
+    """A kv request stream: record i is a SetRequest with probability `set_fraction` (splitmix64
+    stream seed + 0x7000), else a GetRequest; key lengths from `key`, value lengths from `value` for
+    SetRequests (GetRequests carry no value)."""
+    u = (splitmix64(seed + 0x7000, n) >> np.uint64(11)).astype(np.float64) * (1.0 / (1 << 53))
+    rtype = (u < set_fraction).astype(np.uint8)
+    cols = []
+    for f, spec in enumerate((key, value)):
+        ln = lengths(spec, n, seed + 0x10000 * (f + 1))
+        if f == 1:
+            ln = ln * rtype.astype(np.uint64)
+        offs = np.zeros(n + 1, dtype=np.uint64)
+        np.cumsum(ln, out=offs[1:])
+        cols.append((random_bytes(seed + 0x100000000 * (f + 1), int(offs[-1])), offs))
+    return MixedBatch(rtype, cols[0], cols[1])
+
+
 def config4_shard(g: int, records_per_gpu: int = 1 << 23) -> dict:
     return dict(schema="kv_set_request", n=records_per_gpu, lens=(64, 256), seed=0x5EED0003 + g)
 

@@ -89,8 +89,20 @@ int sym_ctx_destroy(sym_ctx* ctx);
 /* Pre-size the decode workspace for up to max_records per call (so later calls never allocate). */
 int sym_ctx_reserve(sym_ctx* ctx, uint64_t max_records);
 /* Synchronize `stream` and report device-side errors of this ctx's calls since the last check
- * (SYM_ERR_CAPACITY, SYM_ERR_DEVICE); clears them. */
+ * (SYM_ERR_CAPACITY, SYM_ERR_INVALID for a batch the kernels cannot place, SYM_ERR_DEVICE); clears them. */
 int sym_ctx_check(sym_ctx* ctx, void* stream);
+/* Decode implementation of this ctx's decode calls (all produce identical results):
+ *   SYM_DECODE_PIPELINE     (default) one launch: parser, scanner and copier workgroups.  A copier
+ *                           whose prefix has not arrived within 1 ms resolves it by a look-back that
+ *                           never waits, so progress never depends on which workgroups are resident.
+ *   SYM_DECODE_THREE_KERNEL parse -> scan -> copy as three stream-ordered launches (no
+ *                           inter-workgroup waiting at all).
+ *   SYM_DECODE_LOOKBACK     the pipeline with its parsers and scanner idle: every copier takes the
+ *                           look-back path (what the fallback does; slower, for testing it). */
+#define SYM_DECODE_PIPELINE 0
+#define SYM_DECODE_THREE_KERNEL 1
+#define SYM_DECODE_LOOKBACK 2
+int sym_ctx_set_decode_impl(sym_ctx* ctx, int impl);
 
 /* ---- schema metadata (host-side, no GPU needed) -------------------------------- */
 int sym_schema_info(int schema, int* nfixed, int* nvar);
@@ -142,10 +154,36 @@ int sym_decode_echo(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_off
                     int32_t* d_score, uint8_t* d_user, uint64_t user_cap, uint64_t* d_user_off, uint8_t* d_content,
                     uint64_t content_cap, uint64_t* d_content_off, uint8_t* d_status, void* stream);
 
-/* ---- host-memory entry points (synchronous) ------------------------------------- */
-/* Same contracts with every pointer in host memory.  Staged through the ctx's pinned buffers
- * (H2D, kernel, D2H pipelined in chunks of records).  These are what the per-record Go
- * Serializer adapter and the UDP buffers of pkg/transport hand over. */
+/* ---- mixed GetRequest / SetRequest batches (the kv-store's request stream) -------------
+ * One batch of records of both types, in any order: d_type[i] == 0 is a GetRequest{Key}
+ * (kv.syn.go:74-185, 22 + K bytes), any other value a SetRequest{Key, Value} (:611-745, 30 + K + V).
+ * Columns as above; a GetRequest's value slice is not part of its record (it is normally empty, and
+ * decode writes it empty).  Record sizes depend on the type, so the record offsets are a device-wide
+ * scan (a size pass over the type column + the encode); d_out must hold
+ * sym_encoded_size_kv_mixed(...) bytes.  The client's ID patch writes get_method_id into GetRequests
+ * and set_method_id into SetRequests (KVService: service 1, Get 1, Set 2, kv_arpc.syn.go:11-28);
+ * 0/0/0 reproduces MarshalSymphony.  Decode takes the type column the server's method dispatch
+ * produced (pkg/rpc/server.go:104-153) and unmarshals each record as its type. */
+uint64_t sym_encoded_size_kv_mixed(uint64_t n, uint64_t n_set, uint64_t key_total, uint64_t set_value_total);
+int sym_encode_kv_mixed(sym_ctx* ctx, const uint8_t* d_type, const uint8_t* d_key, const uint64_t* d_key_off,
+                        const uint8_t* d_val, const uint64_t* d_val_off, uint64_t n, uint32_t service_id,
+                        uint32_t get_method_id, uint32_t set_method_id, uint8_t* d_out, uint64_t* d_out_off,
+                        void* stream);
+int sym_decode_kv_mixed(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_off, const uint8_t* d_type,
+                        uint64_t n, uint8_t* d_key, uint64_t key_cap, uint64_t* d_key_off, uint8_t* d_val,
+                        uint64_t val_cap, uint64_t* d_val_off, uint8_t* d_status, void* stream);
+
+/* ---- host-memory entry points (synchronous) -------------------------------------
+ * Same contracts with every pointer in host memory: what the per-record Go Serializer adapter and
+ * the UDP buffers of pkg/transport hand over.  The batch moves through the GPU in chunks of about
+ * 8 MiB of records on three streams of the ctx, so one chunk's H2D, another's kernel and a third's
+ * D2H overlap.  Host memory that is pinned (sym_host_alloc, hipHostMalloc, a hipHostRegister'ed
+ * range) is transferred by DMA in place; pageable memory is staged through the ctx's pinned buffers
+ * with a host copy.  sym_decode_host: caps[f] is the capacity of h_bytes[f]; a column that does not
+ * fit returns SYM_ERR_CAPACITY with the bytes that fit written.  Device-side errors of the chunks
+ * are returned (no sym_ctx_check needed). */
+int sym_host_alloc(sym_ctx* ctx, uint64_t bytes, void** out); /* pinned host memory (hipHostMalloc) */
+int sym_host_free(sym_ctx* ctx, void* p);
 int sym_encode_host(sym_ctx* ctx, int schema, uint64_t n, const int32_t* const* h_fixed,
                     const uint8_t* const* h_bytes, const uint64_t* const* h_offs, uint32_t service_id,
                     uint32_t method_id, uint8_t* h_out, uint64_t* h_out_off);

@@ -51,6 +51,11 @@ def lib():
         L.sym_oracle_encode_batch.argtypes = [i32, i32, u64, vp, vp, vp, ctypes.c_uint32, ctypes.c_uint32, vp, vp]
         L.sym_oracle_decode_batch.restype = None
         L.sym_oracle_decode_batch.argtypes = [i32, i32, u64, vp, vp, vp, vp, vp, vp]
+        u32 = ctypes.c_uint32
+        L.sym_oracle_encode_kv_mixed.restype = u64
+        L.sym_oracle_encode_kv_mixed.argtypes = [u64, vp, vp, vp, vp, vp, u32, u32, u32, vp, vp]
+        L.sym_oracle_decode_kv_mixed.restype = None
+        L.sym_oracle_decode_kv_mixed.argtypes = [u64, vp, vp, vp, vp, vp, vp, vp, vp]
         _lib = L
     return _lib
 
@@ -122,6 +127,39 @@ def decode_batch(nfixed: int, nvar: int, data: np.ndarray, rec_off: np.ndarray):
     lib().sym_oracle_decode_batch(nfixed, nvar, n, _ptr(data) if data.size else 0, _ptr(rec_off),
                                   _ptr_array(fixed), _ptr_array(cols), _ptr_array(offs), _ptr(status))
     return ([f[:n] for f in fixed], [(cols[i][:int(offs[i][-1])], offs[i]) for i in range(nvar)], status[:n])
+
+
+# ---------------------------------------------------------------- mixed Get/Set batches
+def encode_kv_mixed(rtype, key, val, service_id: int = 0, get_method_id: int = 0, set_method_id: int = 0):
+    """rtype: u8 [n] (0 GetRequest, else SetRequest); key / val: (u8 bytes, u64 offs [n+1]).
+    Returns (stream u8, rec_off u64 [n+1])."""
+    rtype = np.ascontiguousarray(rtype, dtype=np.uint8)
+    kb, ko = np.ascontiguousarray(key[0], dtype=np.uint8), np.ascontiguousarray(key[1], dtype=np.uint64)
+    vb, vo = np.ascontiguousarray(val[0], dtype=np.uint8), np.ascontiguousarray(val[1], dtype=np.uint64)
+    n = len(ko) - 1
+    is_set = rtype[:n] != 0
+    total = 22 * n + int(ko[-1] - ko[0]) + int((8 + np.diff(vo).astype(np.int64))[is_set].sum()) if n else 0
+    out = np.zeros(max(1, total), dtype=np.uint8)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    got = lib().sym_oracle_encode_kv_mixed(n, _ptr(rtype), _ptr(kb), _ptr(ko), _ptr(vb), _ptr(vo), service_id,
+                                           get_method_id, set_method_id, _ptr(out), _ptr(off))
+    assert got == total, (got, total)
+    return out[:total], off
+
+
+def decode_kv_mixed(data: np.ndarray, rec_off: np.ndarray, rtype: np.ndarray):
+    """Returns ([(key bytes, key offs), (val bytes, val offs)], status)."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    rec_off = np.ascontiguousarray(rec_off, dtype=np.uint64)
+    rtype = np.ascontiguousarray(rtype, dtype=np.uint8)
+    n = len(rec_off) - 1
+    cap = max(1, int(rec_off[-1] - rec_off[0]))
+    cols = [np.zeros(cap, dtype=np.uint8) for _ in range(2)]
+    offs = [np.zeros(n + 1, dtype=np.uint64) for _ in range(2)]
+    status = np.zeros(max(1, n), dtype=np.uint8)
+    lib().sym_oracle_decode_kv_mixed(n, _ptr(data) if data.size else 0, _ptr(rec_off), _ptr(rtype), _ptr(cols[0]),
+                                     _ptr(offs[0]), _ptr(cols[1]), _ptr(offs[1]), _ptr(status))
+    return [(cols[i][:int(offs[i][-1])], offs[i]) for i in range(2)], status[:n]
 
 
 # ---------------------------------------------------------------- packetization (fragment_oracle.c)

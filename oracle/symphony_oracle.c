@@ -179,3 +179,48 @@ void sym_oracle_decode_batch(int nfixed, int nvar, uint64_t n, const uint8_t* in
     }
     for (int f = 0; f < nvar; ++f) offs_out[f][n] = col[f];
 }
+
+/* ---- mixed kv batches: GetRequest and SetRequest records in one batch ----
+ * Record i is a GetRequest{Key} when type[i] == 0 (kv.syn.go:74-132 marshal, :134-185 unmarshal)
+ * and a SetRequest{Key, Value} otherwise (:611-678, :680-745); the client's ID patch
+ * (client.go:267-271) writes the method of the record's type (KVService: Get 1, Set 2,
+ * kv_arpc.syn.go:25-28).  A GetRequest's value slice is not part of its record. */
+uint64_t sym_oracle_encode_kv_mixed(uint64_t n, const uint8_t* type, const uint8_t* key, const uint64_t* key_off,
+                                    const uint8_t* val, const uint64_t* val_off, uint32_t sid, uint32_t get_mid,
+                                    uint32_t set_mid, uint8_t* out, uint64_t* out_off) {
+    uint64_t pos = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const int set = type[i] != 0;
+        const uint8_t* fp[2] = {key + key_off[i], val + val_off[i]};
+        const uint64_t fl[2] = {key_off[i + 1] - key_off[i], set ? val_off[i + 1] - val_off[i] : 0};
+        out_off[i] = pos;
+        pos += sym_oracle_marshal(0, set ? 2 : 1, NULL, fp, fl, sid, set ? set_mid : get_mid, out + pos);
+    }
+    out_off[n] = pos;
+    return pos;
+}
+
+/* Each record unmarshalled as its type into a fresh struct; GetRequests leave the value column empty. */
+void sym_oracle_decode_kv_mixed(uint64_t n, const uint8_t* in, const uint64_t* rec_off, const uint8_t* type,
+                                uint8_t* key_out, uint64_t* key_off_out, uint8_t* val_out, uint64_t* val_off_out,
+                                uint8_t* status) {
+    uint64_t col[2] = {0, 0};
+    uint8_t* outs[2] = {key_out, val_out};
+    uint64_t* offs[2] = {key_off_out, val_off_out};
+    int32_t fx[1];
+    uint64_t pos[2], ln[2];
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint8_t* rec = in + rec_off[i];
+        const uint64_t len = rec_off[i + 1] - rec_off[i];
+        const int nv = type[i] != 0 ? 2 : 1;
+        pos[1] = ln[1] = 0;
+        status[i] = (uint8_t)sym_oracle_unmarshal(0, nv, rec, len, fx, pos, ln);
+        for (int f = 0; f < 2; ++f) {
+            offs[f][i] = col[f];
+            if (ln[f]) memcpy(outs[f] + col[f], rec + pos[f], ln[f]);
+            col[f] += ln[f];
+        }
+    }
+    offs[0][n] = col[0];
+    offs[1][n] = col[1];
+}

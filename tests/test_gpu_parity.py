@@ -23,23 +23,26 @@ def dev():
     return torch.device("cuda", 0)
 
 
-@pytest.fixture(autouse=True, params=["pipe", "three_kernel"])
-def decode_impl(request, monkeypatch):
-    """Every test runs against both decode implementations behind the same C ABI: the default
-    single-launch pipeline (decode_pipe.hip) and the three-kernel path (decode.hip, variant 300)."""
-    if request.param == "three_kernel":
-        monkeypatch.setenv("SYMHIP_DECODE_VARIANT", "300")
-    else:
-        monkeypatch.delenv("SYMHIP_DECODE_VARIANT", raising=False)
-    return request.param
-
-
 @pytest.fixture(scope="module")
 def codec(dev):
     from arpc_amd.codec import Codec
     c = Codec(dev)
     yield c
     c.close()
+
+
+DECODE_IMPLS = {"pipe": 0, "three_kernel": 1, "lookback": 2}  # SYM_DECODE_* (include/symphony_hip.h)
+
+
+@pytest.fixture(autouse=True, params=sorted(DECODE_IMPLS))
+def decode_impl(request, codec):
+    """Every test runs against each decode implementation behind the same C ABI, selected with
+    sym_ctx_set_decode_impl: the default single-launch pipeline (decode_pipe.hip), its forced
+    look-back mode (the progress fallback: parsers and scanner idle, every copier resolves its own
+    prefix), and the three-kernel path (decode.hip)."""
+    codec.set_decode_impl(DECODE_IMPLS[request.param])
+    yield request.param
+    codec.set_decode_impl(0)
 
 
 def put(arr: np.ndarray, dev, misalign: int = 0, guard: int = 32, fill: int = 0xA5):

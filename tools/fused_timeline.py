@@ -12,6 +12,8 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+# the measurement variants live only in the tuning build (make -C arpc_amd/csrc tuning)
+os.environ.setdefault("SYMHIP_LIBRARY", os.path.join(ROOT, "tools", "lib", "libsymphony_hip_tuning.so"))
 from arpc_amd import datagen  # noqa: E402
 from arpc_amd.codec import Codec, to_device  # noqa: E402
 
