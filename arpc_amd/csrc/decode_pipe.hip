@@ -52,7 +52,6 @@ namespace pipe {
 constexpr int kRecs = 64;       // records per tile
 constexpr int kThreads = 256;   // 4 waves
 constexpr int kStage = 22528;   // staged bytes per tile: a whole 64-record tile of 350-B records
-constexpr int kStageLoads = (kStage / 16 + kThreads - 1) / kThreads;
 constexpr int kU = 2;           // copy chunks per lane per step
 
 // Word: [63:44] epoch, [43:42] status (1 = aggregate, 2 = exclusive prefix), [41:0] value.
@@ -68,9 +67,9 @@ __device__ __forceinline__ u64 now_ticks() { return __builtin_amdgcn_s_memrealti
 
 __host__ __device__ inline u64 num_tiles(u64 n) { return (n + kRecs - 1) / kRecs; }
 
-template <int NV>
+template <int NV, int STG>
 struct alignas(16) Lds {
-    uint8_t stage[kStage + 16];
+    uint8_t stage[STG + 16];
     u64 src[NV][kRecs];      // field payload position (stream offset)
     int dst[NV][kRecs + 1];  // field start in the tile's column range; [cnt..] = aggregate
     int cs[kRecs + 1];       // record's first copy chunk (record-major chunk sequence)
@@ -120,21 +119,45 @@ __device__ __forceinline__ int rec_nvar(const DecodeParams& p, u64 r) {
     else return NV;
 }
 
-template <int NF, int NV, bool MIX, int R = 2, int WB = 32>
-__device__ void parser(const DecodeParams& p, u64* aw, u64 ntiles, u32 epoch, u32 P) {
+// PACE > 0: a parser wave starts a step only once tile t0 - PACE has its prefix (bounded wait), so
+// the header lines it reads are still cached when that tile's copier stages them.  XCDP: a parser
+// takes only tiles whose copier shares its blockIdx % 8 group (one XCD under round-robin placement),
+// so those lines are in that XCD's L2 (speed only; any placement gives the same results).
+template <int NF, int NV, bool MIX, int R = 2, int WB = 32, bool LIGHT = false, int PACE = 0, bool XCDP = false>
+__device__ void parser(const DecodeParams& p, u64* aw, u64* pw, u64 ntiles, u32 epoch, u32 P) {
     constexpr int NW = WB / 4;  // window dwords
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const u64 n = p.n;
     const uintptr_t in = (uintptr_t)p.in;
-    for (u64 t0 = ((u64)blockIdx.x * 4 + wave) * R; t0 < ntiles; t0 += (u64)P * 4 * R) {
+    // tile of (sequence index j, slot h) = tb + ts * (j + h)
+    u64 tb = 0, ts = 1, j0 = ((u64)blockIdx.x * 4 + wave) * R, jstep = (u64)P * 4 * R;
+    if (XCDP && P % 8 == 0) {
+        const u64 g = blockIdx.x & 7, i = blockIdx.x >> 3;
+        tb = (g + 8 - ((P + 1) & 7)) & 7;  // copier of tile t is block P + 1 + t
+        ts = 8;
+        j0 = (i * 4 + wave) * R;
+        jstep = (u64)(P / 8) * 4 * R;
+    }
+    for (u64 j = j0; tb + ts * j < ntiles; j += jstep) {
+        u64 th[R];
+#pragma unroll
+        for (int h = 0; h < R; ++h) th[h] = tb + ts * (j + h);
+        const u64 t0 = th[0];
+        if constexpr (PACE > 0) {
+            if (t0 >= (u64)PACE) {
+                u64* w = &pw[t0 - PACE];
+                for (const u64 ts0 = now_ticks(); !tagged(load_word(w), epoch) && now_ticks() - ts0 <= kFallbackTicks;)
+                    __builtin_amdgcn_s_sleep(8);
+            }
+        }
         bool live[R], win[R];
         u64 start[R], L[R];
         int nvr[R];
         u32 w[R][NW];
 #pragma unroll
         for (int h = 0; h < R; ++h) {
-            const u64 r = (t0 + h) * kRecs + lane;
-            live[h] = t0 + h < ntiles && r < n;
+            const u64 r = th[h] * kRecs + lane;
+            live[h] = th[h] < ntiles && r < n;
             const u64 rc = live[h] ? r : n;
             start[h] = p.rec_off[rc];
             L[h] = p.rec_off[live[h] ? rc + 1 : rc] - start[h];
@@ -143,6 +166,7 @@ __device__ void parser(const DecodeParams& p, u64* aw, u64 ntiles, u32 epoch, u3
 #pragma unroll
         for (int h = 0; h < R; ++h) {
             win[h] = live[h] && L[h] >= (u64)WB;
+            if constexpr (LIGHT) live[h] = win[h] = false;  // timing: offsets only, no header reads
             const uintptr_t wa = win[h] ? in + start[h] : (uintptr_t)aw;  // readable filler (>= 256 B)
 #pragma unroll
             for (int k = 0; k < WB / 16; ++k) {
@@ -190,13 +214,13 @@ __device__ void parser(const DecodeParams& p, u64* aw, u64 ntiles, u32 epoch, u3
                     }
                 }
             }
-            if (t0 + h < ntiles) {
+            if (th[h] < ntiles) {
 #pragma unroll
                 for (int f = 0; f < NV; ++f) {
                     const u64 inc = wave_incl_scan_u32w_dpp((u32)flen[f]);
                     const u64 agg = (u64)__builtin_amdgcn_readlane((u32)inc, 63) |
                                     ((u64)__builtin_amdgcn_readlane((u32)(inc >> 32), 63) << 32);
-                    if (lane == f) store_word(&aw[(size_t)f * ntiles + t0 + h], make_word(epoch, kStAgg, agg));
+                    if (lane == f) store_word(&aw[(size_t)f * ntiles + th[h]], make_word(epoch, kStAgg, agg));
                 }
             }
         }
@@ -374,11 +398,16 @@ __device__ void lookback(const DecodeParams& p, u64* aw, u64* pw, u64 ntiles, u6
 // MODE 0: the pipeline.  MODE 1: copiers only, every prefix taken as 0 (timing of the data movement
 // alone; wrong output -- tools/kbench.py variant 402).  DIAG: per-tile phase timestamps into p.dbg
 // (8 u64 per tile, s_memrealtime at 100 MHz; tools/fused_timeline.py).
-template <int NF, int NV, bool MIX, int MODE = 0, int DIAG = 0, int SK = 4, int PR = 2>
+// STG: staged bytes per tile (LDS: 24.7 KB at kStage -> 6 copiers per CU; below ~21 KB -> 7).
+// EARLY: the prefix word is loaded when the tile starts, so its cross-XCD round trip overlaps the
+// stage instead of following the parse.  PACE, XCDP: see parser().
+template <int NF, int NV, bool MIX, int MODE = 0, int DIAG = 0, int SK = 4, int PR = 2, int STG = kStage,
+          bool EARLY = false, int PACE = 0, bool XCDP = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))) void decode_pipe_kernel(
     DecodeParams p, u64* flags, u32 epoch) {
     static_assert(NV == 1 || NV == 2, "decode handles one or two string columns");
-    __shared__ Lds<NV> S;
+    constexpr int kLoads = (STG / 16 + kThreads - 1) / kThreads;
+    __shared__ Lds<NV, STG> S;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const u64 n = p.n, ntiles = num_tiles(n);
     const uintptr_t in = (uintptr_t)p.in;
@@ -391,15 +420,17 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
 
     const u32 P = p.pipe_parsers;
     const bool forced = p.impl == kImplLookback;  // parsers and scanner idle: look-back only
-    if (MODE == 0 && blockIdx.x < P) {
-        if (!forced) parser<NF, NV, MIX, PR>(p, aw, ntiles, epoch, P);
+    // MODE 2 / 3 (timing): roles run, copiers never wait; 3: parsers read only the offsets
+    constexpr bool kRoles = MODE == 0 || MODE == 2 || MODE == 3;
+    if (kRoles && blockIdx.x < P) {
+        if (!forced) parser<NF, NV, MIX, PR, 32, MODE == 3, PACE, XCDP>(p, aw, pw, ntiles, epoch, P);
         return;
     }
-    if (MODE == 0 && blockIdx.x == P) {
+    if (kRoles && blockIdx.x == P) {
         if (!forced) scanner<NV, SK>(aw, pw, ntiles, epoch, S);
         return;
     }
-    const u64 tile = MODE == 0 ? blockIdx.x - P - 1 : blockIdx.x;
+    const u64 tile = kRoles ? blockIdx.x - P - 1 : blockIdx.x;
     if (tile >= ntiles) return;
     auto stamp = [&](int slot) {
         if constexpr (DIAG)
@@ -411,23 +442,24 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
     const u64 s0 = p.rec_off[r0], s1 = p.rec_off[r0 + cnt];
     const uintptr_t base = (in + s0) & ~(uintptr_t)15;
     const uintptr_t stop = min((in + s1 + 15) & ~(uintptr_t)15, in_end16);
-    const int nst = (int)min((u64)kStage, (u64)(stop > base ? stop - base : 0));  // multiple of 16
+    const int nst = (int)min((u64)STG, (u64)(stop > base ? stop - base : 0));  // multiple of 16
 
-    // ---- 1. stage (and wave 0's record offsets) ----
-    u64 start = 0, endv = 0;
+    // ---- 1. stage (and wave 0's record offsets, and with EARLY its prefix words) ----
+    u64 start = 0, endv = 0, wv_early = 0;
     if (wave == 0) {
         start = p.rec_off[r0 + min(lane, cnt)];
         endv = p.rec_off[r0 + min(lane + 1, cnt)];
+        if (EARLY && MODE == 0 && lane < NV) wv_early = load_word(&pw[(size_t)lane * ntiles + tile]);
     }
     {
-        u32x4 sv[kStageLoads];
+        u32x4 sv[kLoads];
 #pragma unroll
-        for (int k = 0; k < kStageLoads; ++k) {  // unconditional loads: all in flight together
+        for (int k = 0; k < kLoads; ++k) {  // unconditional loads: all in flight together
             const int c = tid + kThreads * k;
             sv[k] = ld16u(16 * c < nst ? base + 16 * (uintptr_t)c : safe);
         }
 #pragma unroll
-        for (int k = 0; k < kStageLoads; ++k) {
+        for (int k = 0; k < kLoads; ++k) {
             const int c = tid + kThreads * k;
             if (16 * c < nst) *(u32x4*)&S.stage[16 * c] = sv[k];
         }
@@ -519,7 +551,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
                 // this tile's aggregate (a parser may have published the same value), then its prefix
                 store_word(&aw[(size_t)lane * ntiles + tile], make_word(epoch, kStAgg, lane == 0 ? agg[0] : agg[NV - 1]));
                 u64* a = &pw[(size_t)lane * ntiles + tile];
-                wv = load_word(a);
+                wv = EARLY && tagged(wv_early, epoch) ? wv_early : load_word(a);
                 if (!forced) {
                     for (const u64 t0 = now_ticks(); !tagged(wv, epoch) && now_ticks() - t0 <= kFallbackTicks;) {
                         __builtin_amdgcn_s_sleep(2);
@@ -538,6 +570,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
                 if constexpr (NV == 2) pre[1] = (i64)((u64)__shfl((long long)wv, 1, 64) & kValMask);
             }
         } else {  // timing only: spread the tiles over the columns in proportion to their stream offset
+            if ((MODE == 2 || MODE == 3) && lane < NV)
+                store_word(&aw[(size_t)lane * ntiles + tile], make_word(epoch, kStAgg, lane == 0 ? agg[0] : agg[NV - 1]));
             const double frac = (double)(s0 - p.rec_off[0]) / (double)(p.rec_off[n] - p.rec_off[0] + 1);
 #pragma unroll
             for (int f = 0; f < NV; ++f) pre[f] = (i64)(frac * (double)p.cap[f]);
@@ -639,7 +673,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
         if (tid == 0) p.dbg[tile * 8 + 5] = blockIdx.x;
 }
 
-template <int NF, int NV, bool MIX, int MODE, int DIAG, int SK = 4, int PR = 2>
+template <int NF, int NV, bool MIX, int MODE, int DIAG, int SK = 4, int PR = 2, int STG = kStage, bool EARLY = false,
+          int PACE = 0, bool XCDP = false>
 hipError_t launch(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stream, int pnum = 1, int pden = 1) {
     if (DIAG && !p.dbg) return hipErrorInvalidValue;  // timestamps need SYMHIP_DEBUG_PTR (tuning builds)
     static int cus[16] = {0};
@@ -649,12 +684,13 @@ hipError_t launch(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stre
     int& ncu = cus[dev & 15];
     if (ncu == 0 && (e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
     const u64 nt = num_tiles(p.n);
-    u64 P = MODE == 0 ? (u64)ncu * pnum / pden : 0;  // parser workgroups: pnum / pden per CU
+    constexpr bool kRoles = MODE == 0 || MODE == 2 || MODE == 3;
+    u64 P = kRoles ? (u64)ncu * pnum / pden : 0;  // parser workgroups: pnum / pden per CU
     if (P > (nt + 3) / 4) P = (nt + 3) / 4;
     DecodeParams q = p;
     q.pipe_parsers = (unsigned)P;
-    const u64 grid = MODE == 0 ? P + 1 + nt : nt;
-    hipLaunchKernelGGL((decode_pipe_kernel<NF, NV, MIX, MODE, DIAG, SK, PR>), dim3((unsigned)grid), dim3(kThreads), 0,
+    const u64 grid = kRoles ? P + 1 + nt : nt;
+    hipLaunchKernelGGL((decode_pipe_kernel<NF, NV, MIX, MODE, DIAG, SK, PR, STG, EARLY, PACE, XCDP>), dim3((unsigned)grid), dim3(kThreads), 0,
                        stream, q, flags, epoch);
     return hipGetLastError();
 }
@@ -663,17 +699,18 @@ constexpr int kScanPer = 2;      // scanner tiles per thread per step (512-tile 
 constexpr int kParsersNum = 3;   // parser workgroups = #CUs * 3/4
 constexpr int kParsersDen = 4;
 
-template <int MODE, int DIAG, int SK = kScanPer, int PR = 2>
+template <int MODE, int DIAG, int SK = kScanPer, int PR = 2, int STG = kStage, bool EARLY = false, int PACE = 0,
+          bool XCDP = false>
 hipError_t launch_layout(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stream, int pnum = kParsersNum,
                          int pden = kParsersDen) {
-    if (p.type) {  // mixed kv batch: GetRequest / SetRequest per record
-        if (p.lay.nfixed == 0 && p.lay.nvar == 2)
-            return launch<0, 2, true, MODE, DIAG, SK, PR>(p, flags, epoch, stream, pnum, pden);
-        return hipErrorInvalidValue;
-    }
-    if (p.lay.nfixed == 0 && p.lay.nvar == 1) return launch<0, 1, false, MODE, DIAG, SK, PR>(p, flags, epoch, stream, pnum, pden);
-    if (p.lay.nfixed == 0 && p.lay.nvar == 2) return launch<0, 2, false, MODE, DIAG, SK, PR>(p, flags, epoch, stream, pnum, pden);
-    if (p.lay.nfixed == 2 && p.lay.nvar == 2) return launch<2, 2, false, MODE, DIAG, SK, PR>(p, flags, epoch, stream, pnum, pden);
+#define SYMHIP_PIPE_LAUNCH(NF, NV, MIX) \
+    launch<NF, NV, MIX, MODE, DIAG, SK, PR, STG, EARLY, PACE, XCDP>(p, flags, epoch, stream, pnum, pden)
+    if (p.type)  // mixed kv batch: GetRequest / SetRequest per record
+        return p.lay.nfixed == 0 && p.lay.nvar == 2 ? SYMHIP_PIPE_LAUNCH(0, 2, true) : hipErrorInvalidValue;
+    if (p.lay.nfixed == 0 && p.lay.nvar == 1) return SYMHIP_PIPE_LAUNCH(0, 1, false);
+    if (p.lay.nfixed == 0 && p.lay.nvar == 2) return SYMHIP_PIPE_LAUNCH(0, 2, false);
+    if (p.lay.nfixed == 2 && p.lay.nvar == 2) return SYMHIP_PIPE_LAUNCH(2, 2, false);
+#undef SYMHIP_PIPE_LAUNCH
     return hipErrorInvalidValue;
 }
 
@@ -705,6 +742,30 @@ hipError_t launch_decode_pipe(const DecodeParams& p, void* flags, unsigned epoch
         case 449: return pipe::launch_layout<0, 0, 2>(p, fl, epoch, stream, 11, 16);
         case 460: return pipe::launch_layout<0, 0, 2, 1>(p, fl, epoch, stream);
         case 461: return pipe::launch_layout<0, 0, 2, 4>(p, fl, epoch, stream);
+        // round 2: early prefix load, 7 copiers per CU (20992-byte stage), both
+        case 470: return pipe::launch_layout<0, 0, 2, 2, pipe::kStage, true>(p, fl, epoch, stream);
+        case 471: return pipe::launch_layout<0, 0, 2, 2, 20992, false>(p, fl, epoch, stream);
+        case 472: return pipe::launch_layout<0, 0, 2, 2, 20992, true>(p, fl, epoch, stream);
+        case 473: return pipe::launch_layout<0, 0, 2, 2, 20992, true>(p, fl, epoch, stream, 1, 2);
+        case 474: return pipe::launch_layout<0, 0, 2, 2, 20992, true>(p, fl, epoch, stream, 1, 1);
+        case 475: return pipe::launch_layout<1, 0, 2, 2, 20992, false>(p, fl, epoch, stream);
+        case 476: return pipe::launch_layout<2, 0>(p, fl, epoch, stream);  // roles run, no waits (WRONG output)
+        case 477: return pipe::launch_layout<0, 0>(p, fl, epoch, stream, 0, 1);  // no parsers
+        case 478: return pipe::launch_layout<0, 0>(p, fl, epoch, stream, 1, 8);
+        case 479: return pipe::launch_layout<0, 0>(p, fl, epoch, stream, 1, 4);
+        case 480: return pipe::launch_layout<0, 0>(p, fl, epoch, stream, 1, 2);
+        case 481: return pipe::launch_layout<0, 0, 2, 1>(p, fl, epoch, stream);
+        case 482: return pipe::launch_layout<2, 0>(p, fl, epoch, stream, 0, 1);  // scanner only, no waits
+        case 483: return pipe::launch_layout<3, 0>(p, fl, epoch, stream);  // parsers read offsets only, no waits
+        case 484: return pipe::launch_layout<0, 0, 2, 2, pipe::kStage, false, 2048>(p, fl, epoch, stream);
+        case 485: return pipe::launch_layout<0, 0, 2, 2, pipe::kStage, false, 4096>(p, fl, epoch, stream);
+        case 486: return pipe::launch_layout<0, 0, 2, 2, pipe::kStage, false, 8192>(p, fl, epoch, stream);
+        case 487: return pipe::launch_layout<0, 0, 2, 2, pipe::kStage, false, 4096>(p, fl, epoch, stream, 1, 2);
+        case 488: return pipe::launch_layout<0, 0, 2, 2, pipe::kStage, false, 0, true>(p, fl, epoch, stream);
+        case 489: return pipe::launch_layout<0, 0, 2, 2, pipe::kStage, false, 512, true>(p, fl, epoch, stream);
+        case 490: return pipe::launch_layout<0, 0, 2, 2, pipe::kStage, false, 1024, true>(p, fl, epoch, stream);
+        case 491: return pipe::launch_layout<0, 0, 2, 2, pipe::kStage, false, 2048, true>(p, fl, epoch, stream);
+        case 492: return pipe::launch_layout<2, 0, 2, 2, pipe::kStage, false, 0, true>(p, fl, epoch, stream);
         default: break;
     }
 #endif

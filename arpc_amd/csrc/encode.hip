@@ -30,6 +30,7 @@ namespace symhip {
 
 constexpr int kWaveRecs = 64;  // records per wave tile
 constexpr int kWaves = 4;      // wave tiles per 256-thread workgroup
+constexpr int kGroupShift = 4; // mixed batches: 2^kGroupShift tiles per size-pass group (1024 records)
 
 // Header slot for H0 header bytes: a 16-byte window starting at any b < H0 stays in the slot,
 // and one starting up to 15 bytes before a slot reads only the previous slot's zero tail.
@@ -86,7 +87,7 @@ __global__ __launch_bounds__(256) void encode_kernel(EncodeParams p) {
             size = (i64)(22 + L[0] + (isset ? 8 + L[1] : 0));
         }
         const u64 tile = r0 / kWaveRecs;
-        const i64 tp = uniform_i64((i64)(p.group_pre[tile >> 6] + p.tile_loc[tile]));
+        const i64 tp = uniform_i64((i64)(p.group_pre[tile >> kGroupShift] + p.tile_loc[tile]));
         o = tp + (i64)(wave_incl_scan_u64((u64)size, lane) - (u64)size);
         if (lane < cnt) {
             const u64 r = r0 + lane;
@@ -348,9 +349,10 @@ hipError_t launch_encode(const EncodeParams& p, hipStream_t stream) {
 // type bytes and the value offsets (Σ over Sets of 8 + V; keys contribute 22 + K per record, taken
 // from the key offsets at tile edges) and writes, per 64-record tile, its exclusive size prefix
 // inside its group of kGroupTiles tiles, and per group its total.  The last workgroup to finish
-// (ticket) scans the group totals.  The encode kernel starts tile t at group_pre[t/64] + tile_loc[t].
-constexpr int kGroupTiles = 64;                 // tiles per size-pass workgroup (4096 records)
-constexpr int kTilesPerWave = kGroupTiles / 4;  // 16
+// (ticket) scans the group totals.  The encode kernel starts tile t at group_pre[t >> kGroupShift] +
+// tile_loc[t].
+constexpr int kGroupTiles = 1 << kGroupShift;   // tiles per size-pass workgroup (1024 records)
+constexpr int kTilesPerWave = kGroupTiles / 4;  // 4
 
 struct MixedWs {
     u64* group_pre;
@@ -375,36 +377,35 @@ __global__ __launch_bounds__(256) void mixed_size_kernel(EncodeParams p, MixedWs
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const u64 n = p.n, ntiles = mixed_ntiles(n), g = blockIdx.x;
     const u64 t0 = g * kGroupTiles + (u64)wave * kTilesPerWave;  // this wave's first tile
-    // every load of the wave's 16 tiles in flight before any is used (clamped, unconditional)
+    // every load of the wave's tiles in flight before any is used (clamped, unconditional); lane 0
+    // also loads the key offsets at the tiles' edges
     uint8_t ty[kTilesPerWave];
-    u64 v0[kTilesPerWave], v1[kTilesPerWave];
+    u64 v0[kTilesPerWave], v1[kTilesPerWave], ka[kTilesPerWave], kb[kTilesPerWave];
 #pragma unroll
     for (int k = 0; k < kTilesPerWave; ++k) {
-        const u64 r = min((t0 + k) * kWaveRecs + lane, n - 1);
+        const u64 a = min((t0 + k) * kWaveRecs, n), b = min(a + kWaveRecs, n);
+        const u64 r = min(a + lane, n - 1);
         ty[k] = p.type[r];
         v0[k] = p.offs[1][r];
         v1[k] = p.offs[1][r + 1];
+        ka[k] = p.offs[0][lane == 0 ? a : b];
+        kb[k] = p.offs[0][b];
     }
 #pragma unroll
     for (int k = 0; k < kTilesPerWave; ++k) {
-        const u64 t = t0 + k, r = t * kWaveRecs + lane;
-        const u64 extra = r < n && ty[k] != 0 ? 8 + (v1[k] - v0[k]) : 0;
-        const u64 sum = wave_sum_u64(extra);
-        if (lane == 0) {
-            u64 agg = 0;
-            if (t < ntiles) {
-                const u64 a = t * kWaveRecs, b = min(a + kWaveRecs, n);
-                agg = 22 * (b - a) + (p.offs[0][b] - p.offs[0][a]) + sum;
-            }
-            s_agg[wave * kTilesPerWave + k] = agg;
-        }
+        const u64 t = t0 + k, a = t * kWaveRecs, r = a + lane;
+        const u32 extra = r < n && ty[k] != 0 ? (u32)(8 + (v1[k] - v0[k])) : 0u;  // < 2^32 (u32 lengths)
+        const u64 inc = wave_incl_scan_u32w_dpp(extra);
+        const u64 sum = (u64)__builtin_amdgcn_readlane((u32)inc, 63) | ((u64)__builtin_amdgcn_readlane((u32)(inc >> 32), 63) << 32);
+        if (lane == 0)
+            s_agg[wave * kTilesPerWave + k] = t < ntiles ? 22 * (min(a + kWaveRecs, n) - a) + (kb[k] - ka[k]) + sum : 0;
     }
     __syncthreads();
-    if (wave == 0) {
-        const u64 v = s_agg[lane];
+    if (wave == 0) {  // the group's tiles: exclusive prefixes inside the group, and its total
+        const u64 v = lane < kGroupTiles ? s_agg[lane] : 0;
         const u64 inc = wave_incl_scan_u64(v, lane);
         const u64 t = g * kGroupTiles + lane;
-        if (t < ntiles) w.tile_loc[t] = inc - v;
+        if (lane < kGroupTiles && t < ntiles) w.tile_loc[t] = inc - v;
         if (lane == 63) __hip_atomic_store(&w.group_tot[g], inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();

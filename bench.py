@@ -6,15 +6,19 @@ encoded batch (BASELINE.json configs[1]: 2^20 kv-store SetRequest records, 64 B 
 buffer sets rotate so the 256 MiB Infinity Cache cannot serve a step from a previous
 one: step s encodes set s%4 and decodes the stream encoded two steps earlier.
 
-  python bench.py [--gpus N --steps K --warmup W] [--config 2|3] [--records R]
+  python bench.py [--gpus N --steps K --warmup W] [--config 2|3|4] [--records R]
   torchrun --nproc-per-node N bench.py --gpus N ...   (weak scaling, no data-path collective)
 
 Prints ONE JSON line on rank 0.  `value` = algorithmic GB/s over all ranks (SURVEY.md
 section 8d: 694 B encode + 695 B decode per 64/256 record), timed with a barrier +
 device sync on both sides, max over ranks.  `roofline` reports the dominant single kernel
 (encode_kernel, or the one-launch decode_pipe_kernel) from HIP events on the stream the kernels
-run on; `cpu_baseline` times the C oracle (a restatement of the Go codec,
-single thread) on a bounded sample on this host.
+run on; `cpu_baseline` times the C restatement of the Go codec (oracle/) on a bounded sample on
+this host, at 1 thread and at the host's core share, plus config 1's echo record.
+--config 4 is SURVEY 8d config 4: 2^23 SetRequests per GPU (seed 0x5EED0003 + rank), the shards
+of a 2^26-record batch on 8 GPUs.  Legs beside the headline (outside the timed region): the mixed
+Get/Set batch at the trace ratio (BASELINE config 2 as written), config 3, the host-inclusive
+rate through sym_encode_host / sym_decode_host, and the SURVEY 8f rows.
 """
 from __future__ import annotations
 
@@ -81,36 +85,82 @@ def max_over_ranks(x: float, world: int, dev) -> float:
 
 
 def workload(args, world, rank):
-    base = dict(datagen.CONFIG2 if args.config == 2 else datagen.CONFIG3)
+    if args.config == 4:  # shard `rank` of the 2^26-record batch
+        base = datagen.config4_shard(rank)
+    else:
+        base = dict(datagen.CONFIG2 if args.config == 2 else datagen.CONFIG3)
+        if world > 1:  # one seeded shard per GPU
+            base["seed"] = 0x5EED0003 + rank if args.config == 2 else base["seed"] + 0x100 * rank
     if args.records:
         base["n"] = args.records
-    if world > 1:  # config 4 sharding: one seeded contiguous shard per GPU
-        base["seed"] = 0x5EED0003 + rank if args.config == 2 else base["seed"] + 0x100 * rank
     return base
 
 
+def host_cpu_info() -> dict:
+    """nproc, the CPU model (lscpu's "Model name", from /proc/cpuinfo) and this process's core share."""
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    share = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    return {"nproc": os.cpu_count(), "affinity": share, "model": model}
+
+
 def cpu_baseline(kw: dict, seconds: float) -> dict:
-    """Time the CPU oracle (C restatement of the Go codec, 1 thread) on a bounded sample."""
+    """The C restatement of the Go codec (oracle/symphony_oracle.c; no Go toolchain exists here or
+    on the GPU box) on a bounded sample of the same workload: encode+decode at 1 thread and
+    record-sharded over the host's core share (at most 16 threads: the box's CPU share per GPU;
+    ctypes releases the GIL, so the shards run in parallel), plus config 1's echo record
+    (ns per MarshalSymphony / UnmarshalSymphony, one record per call)."""
+    from concurrent.futures import ThreadPoolExecutor
+
     from oracle import oracle
+    info = host_cpu_info()
     sample = dict(kw, n=min(kw["n"], 1 << 16))
     b = datagen.make_batch(**sample)
     s = b.schema
     stream, off = oracle.encode_batch(b.fixed, b.var)  # warm
     var_total = sum(int(o[-1] - o[0]) for _, o in b.var)
     enc_b, dec_b = alg_bytes(b.n, s.nvar, var_total, int(off[-1]))
-    reps, t0 = 0, time.perf_counter()
-    while True:
-        oracle.encode_batch(b.fixed, b.var)
-        oracle.decode_batch(s.nfixed, s.nvar, stream, off)
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    return {"value": round((enc_b + dec_b) * reps / el / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
-            "mrecords_per_s": round(2 * b.n * reps / el / 1e6, 4),
+
+    def run(budget: float) -> tuple[int, float]:
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            oracle.encode_batch(b.fixed, b.var)
+            oracle.decode_batch(s.nfixed, s.nvar, stream, off)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= budget:
+                return reps, el
+
+    reps1, el1 = run(seconds / 2)
+    threads = max(1, min(16, info["affinity"]))
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        res = list(ex.map(run, [seconds / 2] * threads))
+    elN = time.perf_counter() - t0
+    repsN = sum(r for r, _ in res)
+    m_ns, u_ns = oracle.bench_echo(2_000_000)
+    gb = lambda reps, el: round((enc_b + dec_b) * reps / el / 1e9, 4)
+    return {"value": gb(reps1, el1), "unit": "GB/s", "cores": 1, "kind": "port",
+            "mrecords_per_s": round(2 * b.n * reps1 / el1 / 1e6, 4),
+            "all_cores": {"value": gb(repsN, elN), "cores": threads,
+                          "mrecords_per_s": round(2 * b.n * repsN / elN / 1e6, 4)},
+            "host": info,
+            "config1_echo": {"marshal_ns": round(m_ns, 2), "unmarshal_ns": round(u_ns, 2),
+                             "records_per_s": round(1e9 / (m_ns + u_ns), 1),
+                             "gbps": round(54 * 2 / (m_ns + u_ns), 4),
+                             "note": "EchoRequest{42, 300, alice, hello world} (54 B), marshal then unmarshal, "
+                                     "one record per call with Go's allocations (oracle/bench_oracle.c, "
+                                     "testcases/simple/main.go:248-420 methodology), 1 thread"},
             "sample": f"{b.n} {s.go_type} records of the same workload (seed {sample['seed']:#x}), "
-                      f"encode+decode x{reps} in {el:.1f} s by oracle/symphony_oracle.c (-O2, 1 thread): "
-                      "C restatement of the Go codec, not Go (no Go toolchain)"}
+                      f"encode+decode x{reps1} in {el1:.1f} s on 1 thread and x{repsN} in {elN:.1f} s on "
+                      f"{threads} threads by oracle/symphony_oracle.c (-O2): C restatement of the Go codec, "
+                      "not Go (no Go toolchain)"}
 
 
 def load_traffic(kernel: str):
@@ -360,50 +410,202 @@ def flat_leg(codec: Codec, dev, reps: int) -> dict:
 
 
 def host_inclusive(codec: Codec, kw: dict, dev, steps: int) -> dict:
-    """Pinned host -> H2D -> encode -> D2H, then H2D -> decode -> D2H (serial, one stream)."""
+    """Host memory in, host memory out, through the C ABI's host entry points (what a cgo Serializer
+    adapter calls): sym_encode_host then sym_decode_host on the same workload, each call chunked over
+    three streams with H2D / kernel / D2H overlapped (arpc_amd/csrc/host.cpp).  Timed with the host
+    clock around the synchronous calls.  Two caller-memory kinds: pinned (DMA in place) and pageable
+    (staged through the ctx's pinned buffers).  For comparison, the same work serially on one stream
+    (pinned H2D, kernel, D2H, no chunking)."""
+    import ctypes
+
+    from arpc_amd import _native
+    L, ctx = codec._lib, codec._ctx
     b = datagen.make_batch(**kw)
     s = b.schema
+    n = b.n
     var_total = sum(int(o[-1] - o[0]) for _, o in b.var)
     total = b.encoded_size()
-    h_var = [(torch.from_numpy(by).pin_memory(), torch.from_numpy(o.view(np.int64)).pin_memory()) for by, o in b.var]
-    h_out = torch.empty(total, dtype=torch.uint8).pin_memory()
-    h_off = torch.empty(b.n + 1, dtype=torch.int64).pin_memory()
-    d_var = [(torch.empty_like(x, device=dev), torch.empty_like(o, device=dev)) for x, o in h_var]
-    d_out = torch.empty(total, dtype=torch.uint8, device=dev)
-    d_off = torch.empty(b.n + 1, dtype=torch.int64, device=dev)
-    h_dec = [(torch.empty(int(o[-1]), dtype=torch.uint8).pin_memory(), torch.empty(b.n + 1, dtype=torch.int64).pin_memory())
-             for _, o in b.var]
-    dec = DecodedBatch(fixed=[], var=[(torch.empty(int(o[-1]), dtype=torch.uint8, device=dev),
-                                       torch.empty(b.n + 1, dtype=torch.int64, device=dev)) for _, o in b.var],
-                       status=torch.empty(b.n, dtype=torch.uint8, device=dev))
-    h_status = torch.empty(b.n, dtype=torch.uint8).pin_memory()
+    enc_b, dec_b = alg_bytes(n, s.nvar, var_total, total)
 
-    def one():
-        for (hx, ho), (dx, do) in zip(h_var, d_var):
-            dx.copy_(hx, non_blocking=True)
-            do.copy_(ho, non_blocking=True)
-        codec.encode(s, [], d_var, out=d_out, out_off=d_off)
-        h_out.copy_(d_out, non_blocking=True)
-        h_off.copy_(d_off, non_blocking=True)
-        d_out.copy_(h_out, non_blocking=True)
-        d_off.copy_(h_off, non_blocking=True)
-        codec.decode(s, d_out, d_off, outputs=dec)
-        for (hx, ho), (dx, do) in zip(h_dec, dec.var):
-            hx.copy_(dx, non_blocking=True)
-            ho.copy_(do, non_blocking=True)
-        h_status.copy_(dec.status, non_blocking=True)
+    def cols(pinned: bool):
+        mk = (lambda a: torch.from_numpy(a).pin_memory()) if pinned else (lambda a: torch.from_numpy(a.copy()))
+        var = [(mk(by), mk(o.view(np.int64))) for by, o in b.var]
+        out = torch.empty(total + 16, dtype=torch.uint8, pin_memory=pinned)
+        off = torch.empty(n + 1, dtype=torch.int64, pin_memory=pinned)
+        dec = [(torch.empty(int(o[-1] - o[0]) + 16, dtype=torch.uint8, pin_memory=pinned),
+                torch.empty(n + 1, dtype=torch.int64, pin_memory=pinned)) for _, o in b.var]
+        st = torch.empty(n, dtype=torch.uint8, pin_memory=pinned)
+        return var, out, off, dec, st
 
-    one()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
+    def run(pinned: bool) -> dict:
+        var, out, off, dec, st = cols(pinned)
+        bp = _native.ptr_array([x.data_ptr() for x, _ in var])
+        op = _native.ptr_array([o.data_ptr() for _, o in var])
+        dbp = _native.ptr_array([x.data_ptr() for x, _ in dec])
+        dop = _native.ptr_array([o.data_ptr() for _, o in dec])
+        caps = _native.u64_array([x.numel() for x, _ in dec])
+
+        def enc():
+            _native.check(L.sym_encode_host(ctx, s.schema_id, n, None, bp, op, 0, 0, out.data_ptr(), off.data_ptr()),
+                          "sym_encode_host")
+
+        def dcd():
+            _native.check(L.sym_decode_host(ctx, s.schema_id, n, out.data_ptr(), off.data_ptr(), None, dbp, caps, dop,
+                                            st.data_ptr()), "sym_decode_host")
+        enc()
+        dcd()  # warm (allocates the slots)
+        ok = bool((st == 0).all()) and all(torch.equal(d[0][:x.numel()], x) for d, (x, _) in zip(dec, var))
+        te = td = 0.0
+        for _ in range(steps):
+            t0 = time.perf_counter()
+            enc()
+            t1 = time.perf_counter()
+            dcd()
+            te += t1 - t0
+            td += time.perf_counter() - t1
+        return {"encode_gbps": round(enc_b * steps / te / 1e9, 2), "decode_gbps": round(dec_b * steps / td / 1e9, 2),
+                "gbps_algorithmic": round((enc_b + dec_b) * steps / (te + td) / 1e9, 2),
+                "ms_per_step": round((te + td) / steps * 1e3, 3), "round_trip_ok": ok}
+
+    def serial() -> dict:
+        var, out, off, dec, st = cols(True)
+        d_var = [(torch.empty_like(x, device=dev), torch.empty_like(o, device=dev)) for x, o in var]
+        d_out = torch.empty(total + 16, dtype=torch.uint8, device=dev)
+        d_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        dd = DecodedBatch(fixed=[], var=[(torch.empty_like(x, device=dev), torch.empty_like(o, device=dev))
+                                         for x, o in dec], status=torch.empty(n, dtype=torch.uint8, device=dev))
+
+        def one():
+            for (hx, ho), (dx, do) in zip(var, d_var):
+                dx.copy_(hx, non_blocking=True)
+                do.copy_(ho, non_blocking=True)
+            codec.encode(s, [], d_var, out=d_out, out_off=d_off)
+            out.copy_(d_out, non_blocking=True)
+            off.copy_(d_off, non_blocking=True)
+            d_out.copy_(out, non_blocking=True)
+            d_off.copy_(off, non_blocking=True)
+            codec.decode(s, d_out, d_off, outputs=dd)
+            for (hx, ho), (dx, do) in zip(dec, dd.var):
+                hx.copy_(dx, non_blocking=True)
+                ho.copy_(do, non_blocking=True)
+            st.copy_(dd.status, non_blocking=True)
         one()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            one()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        return {"gbps_algorithmic": round((enc_b + dec_b) * steps / el / 1e9, 2), "ms_per_step": round(el / steps * 1e3, 3)}
+
+    return {"pinned": run(True), "pageable": run(False), "serial_one_stream": serial(),
+            "note": "sym_encode_host + sym_decode_host (chunked, 3 streams, H2D/kernel/D2H overlapped), host clock; "
+                    "algorithmic bytes as the headline; serial_one_stream: the same work unchunked on one stream"}
+
+
+def mixed_leg(codec: Codec, dev, reps: int) -> dict:
+    """BASELINE config 2 as written ("1 M kv-store-symphony Get/Set records"): 2^20 requests at the
+    trace's 36.9 % SetRequest share (datagen.CONFIG2_MIXED), K=64, V=256, encoded with
+    sym_encode_kv_mixed (size pass + encode) and decoded with sym_decode_kv_mixed, device-resident,
+    HIP events, two rotating buffer sets.  Algorithmic bytes -- encode: type n + keys + key offsets
+    8(n+1) + Set values + value offsets 8(n+1) read, stream + 8(n+1) offsets written; decode: stream +
+    8(n+1) + type n read, keys + values + 2 x 8(n+1) offsets + n status written."""
+    b = datagen.make_mixed_batch(**datagen.CONFIG2_MIXED)
+    n = b.n
+    total = b.encoded_size()
+    kb, vb = int(b.key[1][-1]), int(b.val[1][-1])
+    sets = []
+    for k in range(2):
+        t = torch.from_numpy(b.type).to(dev)
+        key = (torch.from_numpy(b.key[0]).to(dev) ^ (0x3B * k), torch.from_numpy(b.key[1].view(np.int64)).to(dev))
+        val = (torch.from_numpy(b.val[0]).to(dev) ^ (0x3B * k), torch.from_numpy(b.val[1].view(np.int64)).to(dev))
+        out = (torch.empty(total + 16, dtype=torch.uint8, device=dev), torch.empty(n + 1, dtype=torch.int64, device=dev))
+        dec = DecodedBatch(fixed=[], var=[(torch.empty(kb + 16, dtype=torch.uint8, device=dev),
+                                           torch.empty(n + 1, dtype=torch.int64, device=dev)),
+                                          (torch.empty(vb + 16, dtype=torch.uint8, device=dev),
+                                           torch.empty(n + 1, dtype=torch.int64, device=dev))],
+                           status=torch.empty(n, dtype=torch.uint8, device=dev))
+        sets.append((t, key, val, out, dec))
+    for t, key, val, out, dec in sets:
+        codec.encode_kv_mixed(t, key, val, 1, 1, 2, out=out[0], out_off=out[1])
+        codec.decode_kv_mixed(out[0], out[1], t, outputs=dec)
+    codec.check()
+    ok = all(bool((dec.status == 0).all()) and torch.equal(dec.var[1][0][:vb], val[0]) and
+             torch.equal(dec.var[0][0][:kb], key[0]) for t, key, val, out, dec in sets)
+    ev_e, ev_d = [], []
+    for i in range(reps):
+        t, key, val, out, dec = sets[i % 2]
+        e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+        e0.record()
+        codec.encode_kv_mixed(t, key, val, 1, 1, 2, out=out[0], out_off=out[1])
+        e1.record()
+        _, _, _, out2, dec2 = sets[(i + 1) % 2]
+        codec.decode_kv_mixed(out2[0], out2[1], sets[(i + 1) % 2][0], outputs=dec2)
+        e2.record()
+        ev_e.append((e0, e1))
+        ev_d.append((e1, e2))
     torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    enc_b, dec_b = alg_bytes(b.n, s.nvar, var_total, total)
-    return {"gbps_algorithmic": round((enc_b + dec_b) * steps / el / 1e9, 2),
-            "ms_per_step": round(el / steps * 1e3, 3),
-            "note": "pinned H2D + encode + D2H + H2D + decode + D2H, serial on one stream"}
+    codec.check()
+    enc_ms = float(np.mean([a.elapsed_time(c) for a, c in ev_e]))
+    dec_ms = float(np.mean([a.elapsed_time(c) for a, c in ev_d]))
+    enc_alg = n + kb + 8 * (n + 1) + vb + 8 * (n + 1) + total + 8 * (n + 1)
+    dec_alg = total + 8 * (n + 1) + n + kb + vb + 16 * (n + 1) + n
+    nset = int(b.type.sum())
+    return {"records": n, "set_records": nset, "set_fraction": round(nset / n, 4), "stream_bytes": total,
+            "round_trip_ok": ok, "encode_ms": round(enc_ms, 4), "encode_gbps": round(enc_alg / enc_ms / 1e6, 1),
+            "decode_ms": round(dec_ms, 4), "decode_gbps": round(dec_alg / dec_ms / 1e6, 1),
+            "gbps_algorithmic": round((enc_alg + dec_alg) / (enc_ms + dec_ms) / 1e6, 1),
+            "mrecords_per_s": round(2 * n / (enc_ms + dec_ms) / 1e3, 1),
+            "note": "Get/Set mix at the trace_large.req ratio (9,267 SET / 25,125); encode = size pass + encode "
+                    "kernel (two launches); client IDs: service 1, Get 1, Set 2"}
+
+
+def config3_leg(codec: Codec, dev, reps: int) -> dict:
+    """2^20 SetRequests, K=64, V log-uniform 16-4096 B (mean ~736 B, 774 MB stream:
+    no set fits the Infinity Cache), encode + decode device-resident, HIP events, two buffer sets."""
+    b = datagen.make_batch(**datagen.CONFIG3)
+    s = b.schema
+    n = b.n
+    var_total = sum(int(o[-1] - o[0]) for _, o in b.var)
+    total = b.encoded_size()
+    fixed0, var0 = to_device(b, dev)
+    del b
+    caps = [int(o[-1].item() - o[0].item()) for _, o in var0]
+    sets = []
+    for k in range(2):
+        var = [((x ^ (0x3B * k)) if k else x, o.clone()) for x, o in var0]
+        enc = (torch.empty(total + 16, dtype=torch.uint8, device=dev), torch.empty(n + 1, dtype=torch.int64, device=dev))
+        dec = DecodedBatch(fixed=[], var=[(torch.empty(c + 16, dtype=torch.uint8, device=dev),
+                                           torch.empty(n + 1, dtype=torch.int64, device=dev)) for c in caps],
+                           status=torch.empty(n, dtype=torch.uint8, device=dev))
+        codec.encode(s, [], var, out=enc[0], out_off=enc[1])
+        sets.append((var, enc, dec))
+    codec.check()
+    ev_e, ev_d = [], []
+    for i in range(reps):
+        var, enc, _ = sets[i % 2]
+        _, enc2, dec2 = sets[(i + 1) % 2]
+        e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+        e0.record()
+        codec.encode(s, [], var, out=enc[0], out_off=enc[1])
+        e1.record()
+        codec.decode(s, enc2[0], enc2[1], outputs=dec2)
+        e2.record()
+        ev_e.append((e0, e1))
+        ev_d.append((e1, e2))
+    torch.cuda.synchronize()
+    codec.check()
+    ok = all(bool((dec.status == 0).all()) and torch.equal(dec.var[1][0][:caps[1]], var[1][0])
+             for var, _, dec in sets)
+    enc_ms = float(np.mean([a.elapsed_time(c) for a, c in ev_e]))
+    dec_ms = float(np.mean([a.elapsed_time(c) for a, c in ev_d]))
+    enc_b, dec_b = alg_bytes(n, s.nvar, var_total, total)
+    return {"records": n, "stream_bytes": total, "round_trip_ok": ok,
+            "encode_ms": round(enc_ms, 4), "encode_gbps": round(enc_b / enc_ms / 1e6, 1),
+            "decode_ms": round(dec_ms, 4), "decode_gbps": round(dec_b / dec_ms / 1e6, 1),
+            "gbps_algorithmic": round((enc_b + dec_b) / (enc_ms + dec_ms) / 1e6, 1),
+            "kernels": {"encode": "encode_kernel<0, 2, 0, false>", "decode": "decode_pipe_kernel<0, 2, false, 0, 0, 2, 2>"},
+            "note": "config 3 (seed 0x5EED0002), the headline's algorithmic byte definition"}
 
 
 def main():
@@ -413,7 +615,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--overlap", type=int, default=0,
                     help="1: encode and decode of a step on two HIP streams (independent buffer sets), overlapped")
-    ap.add_argument("--config", type=int, default=2, choices=(2, 3))
+    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4))
     ap.add_argument("--records", type=int, default=0, help="records per GPU (default: the config's 2^20)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--host-steps", type=int, default=5, help="host-inclusive steps (0 = skip)")
@@ -422,6 +624,10 @@ def main():
     ap.add_argument("--reassembly-reps", type=int, default=5, help="reassembly leg repetitions (0 = skip)")
     ap.add_argument("--crypto-reps", type=int, default=3, help="segment cipher leg repetitions (0 = skip)")
     ap.add_argument("--flat-reps", type=int, default=5, help="flat-schema codec leg repetitions (0 = skip)")
+    ap.add_argument("--mixed-reps", type=int, default=10, help="mixed Get/Set leg repetitions (0 = skip)")
+    ap.add_argument("--config3-reps", type=int, default=6, help="config 3 leg repetitions (0 = skip)")
+    ap.add_argument("--ref-reps", type=int, default=-1,
+                    help="decode reference timings (three-kernel, look-back only); -1 = max(5, steps/2), 0 = skip")
     args = ap.parse_args()
 
     world, rank, local = dist_setup()
@@ -439,8 +645,8 @@ def main():
     fixed0, var0 = to_device(b, dev)
     del b
     sets = []
-    for k in range(NSETS):
-        var_k = [((x ^ (0x3B * k)) if k else x, o) for x, o in var0]
+    for k in range(NSETS):  # distinct bytes AND distinct offset tensors per set (nothing stays cache-hot)
+        var_k = [((x ^ (0x3B * k)) if k else x, o.clone() if k else o) for x, o in var0]
         sets.append(([f ^ k for f in fixed0], var_k))
     enc = [(torch.empty(total, dtype=torch.uint8, device=dev), torch.empty(n + 1, dtype=torch.int64, device=dev))
            for _ in range(NSETS)]
@@ -529,12 +735,12 @@ def main():
     dec_ms = float(np.mean([a.elapsed_time(b_) for a, b_ in ev["dec"]]))
     enc_b, dec_b = alg_bytes(n, s.nvar, var_total, total)
     value = world * (enc_b + dec_b) * args.steps / elapsed / 1e9
-    # Reference points for the decode, outside the timed region on the same buffers and stream:
-    # the three-kernel decode (variant 300) and the pipeline's data movement alone (variant 402:
-    # copiers only, prefixes taken as 0 -- wrong output, the bound the in-kernel scan costs against).
-    def time_variant(v: str, reps: int) -> float:
+    # Reference points for the decode, outside the timed region on the same buffers and stream: the
+    # three-kernel decode and the pipeline's forced look-back mode (its progress fallback), selected
+    # with sym_ctx_set_decode_impl.  Same results; timings only.
+    def time_impl(impl: int, reps: int) -> float:
         evs = []
-        os.environ["SYMHIP_DECODE_VARIANT"] = v
+        codec.set_decode_impl(impl)
         try:
             for i in range(reps):
                 d = (i + 2) % NSETS
@@ -544,19 +750,29 @@ def main():
                 e1.record()
                 evs.append((e0, e1))
         finally:
-            del os.environ["SYMHIP_DECODE_VARIANT"]
+            codec.set_decode_impl(0)
         torch.cuda.synchronize()
         return float(np.mean([a.elapsed_time(b_) for a, b_ in evs]))
 
-    reps = max(5, args.steps // 2)
-    three_ms = time_variant("300", reps)
-    move_ms = time_variant("402", reps)
+    reps = max(5, args.steps // 2) if args.ref_reps < 0 else args.ref_reps
+    refs = {}
+    if reps:
+        three_ms, lookback_ms = time_impl(1, reps), time_impl(2, reps)
+        refs = {"three_kernel_ms": round(three_ms, 4), "three_kernel_gbps": round(dec_b / three_ms / 1e6, 1),
+                "lookback_only_ms": round(lookback_ms, 4),
+                "lookback_note": "SYM_DECODE_LOOKBACK: parsers and scanner idle, every copier resolves its prefix "
+                                 "by look-back (the progress fallback)"}
     codec.check()
+    glob = None
+    if world > 1:  # the shards as one global stream: rebase by the exclusive scan of shard totals
+        from arpc_amd import shard
+        base, gtotal = shard.global_base(total)
+        glob = {"rank0_base": base, "global_stream_bytes": gtotal, "global_records": n * world}
     # roofline: the dominant single kernel by time (the default decode is one launch)
     if enc_ms >= dec_ms:
-        kname, dom_ms, dom_bytes = f"encode_kernel<{s.nfixed}, {s.nvar}, 0>", enc_ms, enc_b
+        kname, dom_ms, dom_bytes = f"encode_kernel<{s.nfixed}, {s.nvar}, 0, false>", enc_ms, enc_b
     else:
-        kname, dom_ms, dom_bytes = f"decode_pipe_kernel<{s.nfixed}, {s.nvar}, 0, 0, 2>", dec_ms, dec_b
+        kname, dom_ms, dom_bytes = f"decode_pipe_kernel<{s.nfixed}, {s.nvar}, false, 0, 0, 2, 2>", dec_ms, dec_b
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     traffic = load_traffic(kname)
 
@@ -576,8 +792,9 @@ def main():
         "dtype": "u8",
         "data": f"synthetic: splitmix64 bytes, seed {kw['seed']:#x}"
                 + (" + rank (config 4 shard seeds)" if world > 1 else "") + f"; {NSETS} rotating buffer sets",
-        "config": {"workload": ("config2: kv-store SetRequest K=64 B, V=256 B" if args.config == 2 else
-                                "config3: kv-store SetRequest K=64 B, V log-uniform 16-4096 B")
+        "config": {"workload": {2: "config2: kv-store SetRequest K=64 B, V=256 B",
+                                 3: "config3: kv-store SetRequest K=64 B, V log-uniform 16-4096 B",
+                                 4: "config4: kv-store SetRequest K=64 B, V=256 B, 2^23-record shard per GPU"}[args.config]
                    + ", device-resident encode+decode",
                    "records_per_gpu": n, "global_records": n * world, "parallelism": f"shard{world}", "streams": 2 if args.overlap else 1,
                    "bytes_per_record_algorithmic": round((enc_b + dec_b) / n, 3)},
@@ -587,15 +804,17 @@ def main():
                                "gbps": round(enc_b / enc_ms / 1e6, 1)},
                     "decode": {"avg_ms": round(dec_ms, 4), "alg_bytes": dec_b,
                                "gbps": round(dec_b / dec_ms / 1e6, 1),
-                               "kernel": f"decode_pipe_kernel<{s.nfixed}, {s.nvar}, 0, 0, 2>",
-                               "three_kernel_ms": round(three_ms, 4),
-                               "three_kernel_gbps": round(dec_b / three_ms / 1e6, 1),
-                               "movement_only_ms": round(move_ms, 4),
-                               "movement_only_note": "variant 402: copiers without the scan (wrong output); "
-                                                     "the data-movement bound of the pipeline"}},
+                               "kernel": f"decode_pipe_kernel<{s.nfixed}, {s.nvar}, false, 0, 0, 2, 2>", **refs}},
+        "per_gpu_gbps": round((enc_b + dec_b) * args.steps / elapsed / 1e9, 2),
         "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic},
     }
+    if glob:
+        line["config"]["global"] = glob
+    if world == 1 and args.mixed_reps > 0:
+        line["mixed"] = mixed_leg(codec, dev, args.mixed_reps)
+    if world == 1 and args.config3_reps > 0 and args.config == 2:
+        line["config3"] = config3_leg(codec, dev, args.config3_reps)
     if world == 1 and args.host_steps > 0:
         line["host_inclusive"] = host_inclusive(codec, kw, dev, args.host_steps)
     if world == 1 and args.packetize_reps > 0:

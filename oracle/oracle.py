@@ -129,6 +129,20 @@ def decode_batch(nfixed: int, nvar: int, data: np.ndarray, rec_off: np.ndarray):
     return ([f[:n] for f in fixed], [(cols[i][:int(offs[i][-1])], offs[i]) for i in range(nvar)], status[:n])
 
 
+def bench_echo(iters: int) -> tuple[float, float]:
+    """ns per MarshalSymphony and per UnmarshalSymphony of config 1's echo record, one record per
+    call with Go's allocation semantics (oracle/bench_oracle.c; testcases/simple/main.go:248-420)."""
+    L = lib()
+    if not getattr(L, "_bench_ready", False):
+        L.sym_oracle_bench_echo.restype = ctypes.c_uint64
+        L.sym_oracle_bench_echo.argtypes = [ctypes.c_uint64, ctypes.POINTER(ctypes.c_double),
+                                            ctypes.POINTER(ctypes.c_double)]
+        L._bench_ready = True
+    m, u = ctypes.c_double(), ctypes.c_double()
+    L.sym_oracle_bench_echo(iters, ctypes.byref(m), ctypes.byref(u))
+    return m.value, u.value
+
+
 # ---------------------------------------------------------------- mixed Get/Set batches
 def encode_kv_mixed(rtype, key, val, service_id: int = 0, get_method_id: int = 0, set_method_id: int = 0):
     """rtype: u8 [n] (0 GetRequest, else SetRequest); key / val: (u8 bytes, u64 offs [n+1]).
