@@ -70,6 +70,7 @@ SIGNATURES = {
     "sym_flat_encoded_size": (_u64, [_vp, _int, _u64, _u64]),
     "sym_flat_encode": (_int, [_ctx, _vp, _int, _u64, _vp, _vp, _u32, _u32, _u8p, _u64p, _vp]),
     "sym_flat_decode": (_int, [_ctx, _vp, _int, _u64, _u8p, _u64p, _vp, _vp, _vp, _u8p, _vp]),
+    "sym_raw_set": (_int, [_ctx, _vp, _int, _int, _u8p, _u64p, _u64, _vp, _u64p, _u8p, _u64, _u64p, _u8p, _vp]),
     "sym_encrypt": (_int, [_ctx, _u8p, _u64p, _u64, ctypes.c_char_p, ctypes.c_char_p, _u8p, _u8p, _u64p, _u8p, _vp]),
     "sym_decrypt": (_int, [_ctx, _u8p, _u64p, _u64, ctypes.c_char_p, ctypes.c_char_p, _u8p, _u64p, _u8p, _vp]),
 }
@@ -107,6 +108,14 @@ SYM_CRYPT_AUTH_PRIVATE = 4
 SYM_CRYPT_BAD_VERSION = 5
 SYM_GCM_OVERHEAD = 28
 
+
+SYM_SET_OK = 0
+SYM_SET_COMPLETE_BUFFER = 1
+SYM_SET_INVALID_BUFFER = 2
+SYM_SET_PUBLIC_ONLY = 3
+SYM_SET_TOO_SHORT = 4
+SYM_SET_UNMARSHAL = 5
+SYM_SET_BOUNDS = 6
 
 SYM_MAX_FLAT_FIELDS = 16
 SYM_FIELD_REPEATED = 0x80

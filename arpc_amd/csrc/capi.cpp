@@ -653,6 +653,25 @@ int sym_flat_decode(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t
     return e == hipSuccess ? SYM_OK : hip_fail(e, "flat decode launch");
 }
 
+int sym_raw_set(sym_ctx* ctx, const sym_field* fields, int nfields, int field, const uint8_t* d_in,
+                const uint64_t* d_rec_off, uint64_t n, const void* d_val, const uint64_t* d_val_off, uint8_t* d_out,
+                uint64_t out_cap, uint64_t* d_out_off, uint8_t* d_status, void* stream) {
+    if (!ctx) return fail(SYM_ERR_INVALID, "sym_raw_set: ctx is NULL");
+    int rc = flat_check("sym_raw_set", fields, nfields);
+    if (rc != SYM_OK) return rc;
+    if (field < 0 || field >= nfields) return fail(SYM_ERR_INVALID, "sym_raw_set: field %d of %d", field, nfields);
+    const bool scalar = flat_scalar(fields[field]);
+    if (!d_out_off || (n && (!d_in || !d_rec_off || !d_val || (!scalar && !d_val_off) || !d_out || !d_status)))
+        return fail(SYM_ERR_INVALID, "sym_raw_set: NULL argument");
+    DeviceGuard g(ctx->device);
+    if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
+    if (n && (rc = ensure_scratch(ctx, symhip::raw_set_ws_bytes(n), "raw setter")) != SYM_OK) return rc;
+    hipError_t e = symhip::launch_raw_set(fields, nfields, field, n, d_in, d_rec_off, (const uint8_t*)d_val,
+                                          scalar ? nullptr : d_val_off, d_out, out_cap, d_out_off, d_status, ctx->frag,
+                                          ctx->err, (hipStream_t)stream);
+    return e == hipSuccess ? SYM_OK : hip_fail(e, "raw setter launch");
+}
+
 static int crypt_call(bool enc, sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_off, uint64_t n,
                       const uint8_t* pub_key, const uint8_t* priv_key, const uint8_t* d_nonces, uint8_t* d_out,
                       uint64_t* d_out_off, uint8_t* d_status, void* stream) {

@@ -156,6 +156,12 @@ hipError_t launch_flat_decode(const sym_field* f, int nf, uint64_t n, const uint
                               void* const* cols, const uint64_t* caps, uint64_t* const* offs, uint8_t* status,
                               void* ws, unsigned* err, hipStream_t stream);
 
+// ---- batched Raw setters (setters.hip)
+size_t raw_set_ws_bytes(uint64_t n);
+hipError_t launch_raw_set(const sym_field* f, int nf, int k, uint64_t n, const uint8_t* in, const uint64_t* rec_off,
+                          const uint8_t* val, const uint64_t* val_off, uint8_t* out, uint64_t cap, uint64_t* out_off,
+                          uint8_t* status, void* ws, unsigned* err, hipStream_t stream);
+
 // ---- per-segment AES-256-GCM (crypto.hip)
 size_t crypt_tables_bytes();
 void crypt_build_tables(const uint8_t pub_key[32], const uint8_t priv_key[32], void* host_tables);

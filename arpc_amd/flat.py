@@ -161,3 +161,49 @@ def decode(codec: Codec, schema: FlatSchema, data: torch.Tensor, rec_off: torch.
                                             _native.ptr_array(offs), _dptr(st), _stream_handle(codec.device, stream)),
                   "sym_flat_decode")
     return [c[:n] if isinstance(c, torch.Tensor) else c for c in cols], st[:n]
+
+
+def _c_fields(fields):
+    """A FlatSchema, or [(segment 0 public / 1 private, width | SYM_FIELD_REPEATED)] pairs."""
+    if isinstance(fields, FlatSchema):
+        return fields.c_fields(), [(0 if f.public else 1, f.c_width) for f in fields.fields]
+    arr = (_native.SymField * max(1, len(fields)))()
+    for k, (seg, w) in enumerate(fields):
+        arr[k].segment, arr[k].width = seg, w
+    return arr, list(fields)
+
+
+def raw_set(codec: Codec, fields, k: int, data: torch.Tensor, rec_off: torch.Tensor, values, n: int | None = None,
+            out_cap: int | None = None, stream=None):
+    """XxxRaw.Set<field k>(values[i]) on buffer i (sym_raw_set; generator main.go:1038-1093, 1296-1336,
+    1567-1620, 1685-1740, 371-437).  values: a tensor of n values of the field's width (fixed field)
+    or (uint8 bytes, int64 offsets [n+1]) (string / bytes / repeated).  -> (out uint8, out_off int64
+    [n+1], status uint8 [n], SYM_SET_*).  out_cap defaults to the bound that always suffices (one
+    device sync to read the input span)."""
+    cf, pairs = _c_fields(fields)
+    _check_col(data, torch.uint8, "data", codec.device)
+    _check_col(rec_off, torch.int64, "rec_off", codec.device)
+    n = rec_off.numel() - 1 if n is None else n
+    seg, w = pairs[k]
+    scalar = w != 0 and not (w & _native.SYM_FIELD_REPEATED)
+    if scalar:
+        vb, vo = values, None
+        _check_col(vb, vb.dtype, "values", codec.device)
+        vbytes = vb.numel() * vb.element_size()
+    else:
+        vb, vo = values
+        _check_col(vb, torch.uint8, "values", codec.device)
+        _check_col(vo, torch.int64, "value offsets", codec.device)
+        vbytes = int(vo[-1].item() - vo[0].item()) if n else 0
+    if out_cap is None:
+        nv = sum(1 for _, wd in pairs if wd == 0 or wd & _native.SYM_FIELD_REPEATED)
+        g = 14 + sum(4 if (wd == 0 or wd & _native.SYM_FIELD_REPEATED) else wd for _, wd in pairs) + 4 * nv
+        span = int(rec_off[-1].item() - rec_off[0].item()) if n else 0
+        out_cap = (nv + 1) * span + n * g + vbytes + 16
+    out = torch.empty(max(1, out_cap), dtype=torch.uint8, device=codec.device)
+    off = torch.empty(n + 1, dtype=torch.int64, device=codec.device)
+    st = torch.empty(max(1, n), dtype=torch.uint8, device=codec.device)
+    _native.check(codec._lib.sym_raw_set(codec._ctx, cf, len(pairs), k, _dptr(data) or 1, _dptr(rec_off), n,
+                                         _dptr(vb) or 1, _dptr(vo) if vo is not None else 0, _dptr(out), out_cap,
+                                         _dptr(off), _dptr(st), _stream_handle(codec.device, stream)), "sym_raw_set")
+    return out, off, st[:n]

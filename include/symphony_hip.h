@@ -370,6 +370,32 @@ typedef struct sym_field {
 } sym_field;
 
 uint64_t sym_flat_encoded_size(const sym_field* fields, int nfields, uint64_t n, uint64_t var_total);
+
+/* ---- Batched Raw setters ----------------------------------------------------
+ * XxxRaw.SetF(v_i) on buffer i of a flat schema (generator main.go:1038-1093 assertions,
+ * :1296-1336 fixed, :1567-1620 string / bytes, :1685-1740 repeated fixed, :371-437 remarshal;
+ * e.g. GetRequestRaw.SetScore / SetUsername / SetKey, kv-store-symphony-element kv.syn.go:340-412).
+ * fields[field] is the field set.  Values: a fixed field takes n values of its width in d_val
+ * (d_val_off ignored); a string / bytes field takes d_val[d_val_off[i], d_val_off[i+1]); a repeated
+ * field takes its element bytes the same way.  Fixed fields and payloads that are not longer than the
+ * old ones are written in place (the old tail stays as slack); otherwise the message is
+ * remarshalled -- a public field through a fake private segment, keeping the public part and bytes
+ * [5:13]; a private field into a complete message whose [5:13] are 0, as MarshalSymphony writes them.
+ * Every buffer goes to d_out (sizes may change) with d_out_off[n+1]; a buffer whose setter would
+ * panic or fail is copied unchanged and d_status[i] says why.  d_out must hold the result: a bound
+ * is sum((nvar + 1) * len_i + G) + the new value bytes, G = 14 + tables + 4 * nvar (for well-formed
+ * buffers sum(len_i + G) + new bytes); past out_cap buffers are not written and sym_ctx_check
+ * reports SYM_ERR_CAPACITY. */
+#define SYM_SET_OK 0
+#define SYM_SET_COMPLETE_BUFFER 1 /* panic "public setter ... called on complete buffer" */
+#define SYM_SET_INVALID_BUFFER 2  /* panic "private setter ... called on invalid buffer" (len < 5) */
+#define SYM_SET_PUBLIC_ONLY 3     /* panic "private setter ... called on public-only buffer" */
+#define SYM_SET_TOO_SHORT 4       /* error "buffer too short" / "buffer too short for table entry" */
+#define SYM_SET_UNMARSHAL 5       /* error "failed to unmarshal: ..." (remarshal path) */
+#define SYM_SET_BOUNDS 6          /* Go panics with an index out of range (in-place write, fake segment) */
+int sym_raw_set(sym_ctx* ctx, const sym_field* fields, int nfields, int field, const uint8_t* d_in,
+                const uint64_t* d_rec_off, uint64_t n, const void* d_val, const uint64_t* d_val_off, uint8_t* d_out,
+                uint64_t out_cap, uint64_t* d_out_off, uint8_t* d_status, void* stream);
 int sym_flat_encode(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const void* const* d_cols,
                     const uint64_t* const* d_offs, uint32_t service_id, uint32_t method_id, uint8_t* d_out,
                     uint64_t* d_out_off, void* stream);

@@ -467,3 +467,43 @@ def flat_decode(fields, data, rec_off):
                              _ptr(st))
     cols = [o[:n] if isinstance(o, np.ndarray) else (o[0][:int(o[1][n])], o[1]) for o in outs]
     return cols, st[:n]
+
+
+SET_OK, SET_COMPLETE_BUFFER, SET_INVALID_BUFFER, SET_PUBLIC_ONLY, SET_TOO_SHORT, SET_UNMARSHAL, SET_BOUNDS = range(7)
+
+
+def raw_set_bound(fields, rec_off, val_bytes: int) -> int:
+    """Output bytes that always suffice for a batched setter: (nv + 1) len + G per record + new bytes."""
+    nv = sum(1 for _, w in fields if not w or w & REPEATED)
+    g = 14 + sum(4 if (not w or w & REPEATED) else w for _, w in fields) + 4 * nv
+    lens = np.diff(np.asarray(rec_off, np.uint64)).astype(np.int64)
+    return int(((nv + 1) * lens + g).sum()) + int(val_bytes) + 16
+
+
+def raw_set(fields, k: int, data, rec_off, values):
+    """XxxRaw.Set<field k>(value i) on buffer i (flat_oracle.c sym_oracle_raw_set).  values: u8 array
+    [n, width] (fixed field) or (bytes, offs [n+1]) (string / repeated: element bytes).
+    -> (out u8, out_off u64 [n+1], status u8 [n])."""
+    L = lib()
+    if not getattr(L, "_set_ready", False):
+        u64, i32, vp = ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p
+        L.sym_oracle_raw_set.restype = u64
+        L.sym_oracle_raw_set.argtypes = [i32, vp, i32, u64, vp, vp, vp, vp, vp, vp, vp]
+        L._set_ready = True
+    data, rec_off, n, dp = _batch_args(data, rec_off)
+    seg, w = fields[k]
+    if w and not w & REPEATED:
+        vb = np.ascontiguousarray(values, np.uint8).reshape(-1)
+        vo = None
+        nbytes = vb.size
+    else:
+        vb, vo = np.ascontiguousarray(values[0], np.uint8), np.ascontiguousarray(values[1], np.uint64)
+        nbytes = int(vo[-1] - vo[0])
+    cap = raw_set_bound(fields, rec_off, nbytes)
+    out = np.zeros(cap, np.uint8)
+    off = np.zeros(n + 1, np.uint64)
+    st = np.zeros(max(1, n), np.uint8)
+    f = _fields(fields)
+    total = L.sym_oracle_raw_set(len(fields), ctypes.addressof(f), k, n, dp, _ptr(rec_off), _ptr(vb) if vb.size else 0,
+                                 _ptr(vo) if vo is not None else 0, _ptr(out), _ptr(off), _ptr(st))
+    return out[:total], off, st[:n]
