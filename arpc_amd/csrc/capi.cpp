@@ -237,6 +237,8 @@ int symhip::capi::encode_call(sym_ctx* ctx, int schema, uint64_t n, const int32_
     p.err = ctx->err;
 #ifdef SYMHIP_TUNING
     p.variant = symhip::tuning_variant("SYMHIP_ENCODE_VARIANT");
+    if (const char* d = getenv("SYMHIP_DEBUG_PTR")) p.dbg = (uint64_t*)(uintptr_t)strtoull(d, nullptr, 16);
+    if ((p.variant == 6 || p.variant == 7 || p.variant == 10) && !p.dbg) return fail(SYM_ERR_INVALID, "encode timeline needs SYMHIP_DEBUG_PTR");
 #endif
     DeviceGuard g(ctx->device);
     if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
@@ -418,6 +420,9 @@ int sym_encode_kv_mixed(sym_ctx* ctx, const uint8_t* d_type, const uint8_t* d_ke
     p.out = d_out;
     p.out_off = d_out_off;
     p.err = ctx->err;
+#ifdef SYMHIP_TUNING
+    p.variant = symhip::tuning_variant("SYMHIP_ENCODE_VARIANT");
+#endif
     if (n) {
         const int rc = ensure_scratch(ctx, symhip::encode_mixed_ws_bytes(n), "mixed encode");
         if (rc != SYM_OK) return rc;

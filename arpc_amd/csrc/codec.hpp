@@ -38,6 +38,7 @@ struct EncodeParams {
     const uint64_t* tile_loc;
     uint32_t method_get;  // method id written into [9:13] of GetRequest records (mixed batches)
     uint64_t out_base;    // added to every out_off value written (chunked host staging), 0 otherwise
+    uint64_t* dbg;        // tuning builds only (tools/enc_timeline.py): per-tile timestamps, else null
     int variant;    // kernel tuning variant (tuning builds only, tuning_variant("SYMHIP_ENCODE_VARIANT"))
 };
 

@@ -188,8 +188,16 @@ __device__ __forceinline__ i64 uniform_i64(i64 x) {
     return (i64)(((u64)hi << 32) | lo);
 }
 
-// Order LDS traffic between lanes of ONE wave (no workgroup barrier).
+// Order LDS traffic between lanes of ONE wave (no workgroup barrier).  The fences name the
+// local address space only: a wavefront fence over all address spaces makes the compiler wait for
+// every global load in flight (s_waitcnt vmcnt(0)), which serialises software-pipelined loops.
 __device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+}
+// The same for global memory as well (a global read by every lane before one lane's write).
+__device__ __forceinline__ void wave_sync_global() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");

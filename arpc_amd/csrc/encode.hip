@@ -44,34 +44,59 @@ struct EncWaveLds {
     int o[kWaveRecs + 1];              // record start relative to the tile start; [cnt] = span
     u32 len[NV][kWaveRecs];
     u64 delta[NV][kWaveRecs];          // payload byte address = delta + chunk position
-    uint8_t flags[64];                 // record-start marks of one phase-2 step
     uint8_t h0[kWaveRecs];             // mixed batches: the record's bytes before field 0's payload
+    i64 t0;                            // the tile's stream start
+    int span, ok;                      // its length; 0 if it is too long for 32-bit positions
+    int safe;                          // no payload window of the tile reaches past a column end
 };
 
 // MIXED: a kv batch of GetRequests (type 0: 22 + K bytes, kv.syn.go:74-132) and SetRequests (else:
 // 30 + K + V bytes, :611-678); the layout constants below are the SetRequest's, and every per-record
 // difference (header image, table, where the key payload starts, no value) is taken per record.
-template <int NF, int NV, int kVariant, bool MIXED = false>
+// WPT (waves per tile): 1 = each wave owns a tile; kWaves = the workgroup owns one tile, wave 0
+// builds it and the waves take its output steps round-robin (4x shorter-lived workgroups, so a
+// 2^20-record launch runs ~8 rounds of workgroups instead of ~2 and its tail is short).
+template <int NF, int NV, int kVariant, bool MIXED = false, int WPT = 1, bool DIAG = false>
 __global__ __launch_bounds__(256) void encode_kernel(EncodeParams p) {
-    static_assert(!MIXED || (NF == 0 && NV == 2 && kVariant == 0), "mixed batches are kv Get/Set");
+    static_assert(!MIXED || (NF == 0 && NV == 2 && kVariant <= 1), "mixed batches are kv Get/Set");
+    static_assert(WPT == 1 || (WPT == kWaves && kVariant <= 1), "whole-workgroup tiles take one step per wave");
     constexpr int NT = NF + NV;
     constexpr int H0 = 14 + 4 * NT + 4;        // bytes before field 0's payload (the largest, in mixed batches)
     constexpr i64 OVH = 14 + 4 * NT + 4 * NV;  // fixed bytes per record
     constexpr int SLOT = slot_bytes(H0);
     static_assert(SLOT - 16 >= H0 && OVH >= 16, "layout assumptions");
 
-    __shared__ EncWaveLds<NV, SLOT> lds_all[kWaves];
+    __shared__ EncWaveLds<NV, SLOT> lds_all[kWaves / WPT];
+    __shared__ uint8_t flags_all[kWaves][64];  // record-start marks of one phase-2 step, per wave
     __shared__ MaskTable masks;
     mask_table_init(masks, threadIdx.x);
-    __syncthreads();  // the only workgroup barrier
+    __syncthreads();
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    EncWaveLds<NV, SLOT>& S = lds_all[wave];
-    const u64 r0 = ((u64)blockIdx.x * kWaves + wave) * kWaveRecs;
-    if (r0 >= p.n) return;  // wave-uniform
+    EncWaveLds<NV, SLOT>& S = lds_all[WPT == 1 ? wave : 0];
+    uint8_t* const flg = flags_all[wave];
+    const u64 r0 = (WPT == 1 ? (u64)blockIdx.x * kWaves + wave : (u64)blockIdx.x) * kWaveRecs;
+    if (r0 >= p.n) return;  // wave-uniform (workgroup-uniform when WPT > 1)
     const int cnt = (int)min((u64)kWaveRecs, p.n - r0);
+    flg[lane] = 0;
+    u64* const stamp = DIAG ? p.dbg + (r0 / kWaveRecs) * 8 : nullptr;  // tools/enc_timeline.py
+    if (DIAG && lane == 0 && (WPT == 1 || wave == 0)) {
+        stamp[0] = __builtin_amdgcn_s_memrealtime();
+        stamp[6] = blockIdx.x;
+    }
 
     // ---------------- phase 1: per-record offsets and header image ----------------
+    if (WPT == 1 || wave == 0) {
+    // A payload window reads up to 15 bytes beyond its field; that stays inside the column
+    // unless the tile's fields sit within 16 bytes of the column's ends (batch edges).  Scalar
+    // loads, issued with the per-record ones.
+    bool tile_safe = true;
+#pragma unroll
+    for (int f = 0; f < NV; ++f) {
+        const u64 c0 = p.offs[f][0], c1 = p.offs[f][p.n];
+        const u64 t0 = p.offs[f][r0], t1 = p.offs[f][r0 + cnt];
+        tile_safe = tile_safe && t0 >= c0 + 16 && t1 + 16 <= c1;
+    }
     i64 o = 0, size = 0;
     u64 L[NV];
     bool isset = true;  // mixed batches: SetRequest (else GetRequest)
@@ -114,11 +139,15 @@ __global__ __launch_bounds__(256) void encode_kernel(EncodeParams p) {
     // wave-uniform: readfirstlane keeps them (and the phase-2 loop bounds) in SGPRs
     const i64 T0 = uniform_i64((i64)__shfl((long long)o, 0, 64));
     const i64 T1 = uniform_i64((i64)__shfl((long long)(o + size), cnt - 1, 64));
-    if (T1 - T0 >= (i64)1 << 31) {  // positions are 32-bit inside a tile
-        if (lane == 0) atomicOr(p.err, kErrTooLarge);
-        return;
+    const bool ok = T1 - T0 < (i64)1 << 31;  // positions are 32-bit inside a tile
+    if (lane == 0) {
+        S.t0 = T0;
+        S.span = (int)(T1 - T0);
+        S.ok = ok;
+        S.safe = tile_safe;
+        if (!ok) atomicOr(p.err, kErrTooLarge);
     }
-    if (lane < cnt) {
+    if (ok && lane < cnt) {
         const u64 r = r0 + lane;
         const int orel = (int)(o - T0);
         S.o[lane] = orel;
@@ -157,24 +186,20 @@ __global__ __launch_bounds__(256) void encode_kernel(EncodeParams p) {
         for (int k = 0; k < SLOT / 8; ++k) slot[k] = make_uint2(h[2 * k], h[2 * k + 1]);
     }
     if (lane < SLOT / 4) ((u32*)S.hdr)[lane] = 0;
-    S.flags[lane] = 0;
-    wave_sync();
+    }
+    if constexpr (WPT == 1) wave_sync();
+    else __syncthreads();
+    if (!S.ok) return;  // uniform
+    if (DIAG && lane == 0 && (WPT == 1 || wave == 0)) stamp[1] = __builtin_amdgcn_s_memrealtime();
 
     // ---------------- phase 2: natural-order output chunks ----------------
-    const int span = (int)(T1 - T0);
+    const i64 T0 = uniform_i64(S.t0);
+    const int span = __builtin_amdgcn_readfirstlane(S.span);
     const i64 mis = (i64)((uintptr_t)p.out & 15);
     const int first = (int)(((T0 + mis) & ~(i64)15) - mis - T0);  // in (-16, 0]
     uint8_t* const out_t = p.out + T0;
     const uintptr_t dummy = (uintptr_t)p.out & ~(uintptr_t)15;  // readable; its bytes get masked off
-    // A payload window reads up to 15 bytes beyond its field; that stays inside the column
-    // unless the tile's fields sit within 16 bytes of the column's ends (batch edges).
-    bool tile_safe = true;
-#pragma unroll
-    for (int f = 0; f < NV; ++f) {
-        const u64 c0 = p.offs[f][0], c1 = p.offs[f][p.n];
-        const u64 t0 = p.offs[f][r0], t1 = p.offs[f][r0 + cnt];
-        tile_safe = tile_safe && t0 >= c0 + 16 && t1 + 16 <= c1;
-    }
+    const bool tile_safe = S.safe != 0;
     const i64 my_o = lane < cnt ? (i64)S.o[lane] : ((i64)1 << 40);  // record-role register
 
     // Chunk -> record without searching: records are >= 22 bytes, so at most one record starts
@@ -183,60 +208,70 @@ __global__ __launch_bounds__(256) void encode_kernel(EncodeParams p) {
     auto locate = [&](int B) -> int {
         const i64 ck = (my_o - B + 15) >> 4;
         const u64 before = __ballot(ck <= 0);
-        if (ck >= 1 && ck <= 63) S.flags[ck] = 1;
+        if (ck >= 1 && ck <= 63) flg[ck] = 1;
         wave_sync();
-        const bool mine = S.flags[lane] != 0;
+        const bool mine = flg[lane] != 0;
         const u64 m = __ballot(mine);
-        if (mine) S.flags[lane] = 0;  // clean for the next step (each lane its own byte)
+        if (mine) flg[lane] = 0;  // clean for the next step (each lane its own byte)
         const int below = (int)__builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u));
         // (int) casts matter: __popcll is unsigned and max(unsigned, int) picks the double overload
         const int counted = (int)__popcll(before) + below + (mine ? 1 : 0);
         return counted > 0 ? counted - 1 : 0;  // 0 only for the chunk straddling the tile start
     };
 
-    auto chunk = [&](int P, int j, bool careful) {
-        const int oj = S.o[j];
-        const int b = P - oj;  // chunk start relative to record j (> -16)
-        const int h0j = MIXED ? (int)S.h0[j] : H0;
-        int t = h0j - b;       // chunk offset where field 0's payload starts
-        int Lf[NV];
-        uintptr_t X[NV];
-        bool need[NV], fast[NV];
-        u32x4 w[NV];
+    // fetch: the chunk's payload windows (loads only); assemble: header | payloads | prefixes ->
+    // one store.  Split so a pipelined loop can issue step s+1's loads before step s's store.
+    auto fetch = [&](int P, int j, bool careful, u32x4 (&w)[NV]) {
+        const int b = P - S.o[j];  // chunk start relative to record j (> -16)
+        int t = (MIXED ? (int)S.h0[j] : H0) - b;  // chunk offset where field 0's payload starts
 #pragma unroll
         for (int f = 0; f < NV; ++f) {
-            Lf[f] = (int)S.len[f][j];
-            X[f] = (uintptr_t)(S.delta[f][j] + (u64)(i64)P);
-            need[f] = t < 16 && t + Lf[f] > 0 && (!MIXED || Lf[f] > 0);  // a GetRequest has no value
-            fast[f] = need[f];
+            const int Lf = (int)S.len[f][j];
+            const uintptr_t X = (uintptr_t)(S.delta[f][j] + (u64)(i64)P);
+            bool fast = P < span && t < 16 && t + Lf > 0 && (!MIXED || Lf > 0);  // a GetRequest has no value
             if (careful) {  // the 16-byte window must lie inside the column's 16-byte-rounded extent
                 const uintptr_t c0 = (uintptr_t)(p.bytes[f] + p.offs[f][0]) & ~(uintptr_t)15;
                 const uintptr_t c1 = ((uintptr_t)(p.bytes[f] + p.offs[f][p.n]) + 15) & ~(uintptr_t)15;
-                fast[f] = need[f] && X[f] >= c0 && X[f] + 16 <= c1;
+                fast = fast && X >= c0 && X + 16 <= c1;
             }
-            w[f] = ld16u(fast[f] ? X[f] : dummy);  // unconditional: both loads issue together
-            t += Lf[f] + 4;
+            w[f] = ld16u(fast ? X : dummy);  // unconditional: the loads issue together
+            t += Lf + 4;
         }
+    };
+    auto assemble = [&](int P, int j, bool careful, const u32x4 (&w)[NV]) {
+        const int b = P - S.o[j];
+        const int h0j = MIXED ? (int)S.h0[j] : H0;
         u32x4 r = {0, 0, 0, 0};
         if (b < H0) r = lds16u(S.hdr, (j + 1) * SLOT + b);  // a GetRequest's slot is zero past its 22 bytes
-        t = h0j - b;
+        int t = h0j - b;
 #pragma unroll
         for (int f = 0; f < NV; ++f) {
+            const int Lf = (int)S.len[f][j];
             if (f > 0 && t > 0 && t < 20) {  // inner length prefix of field f at [t-4, t)
                 u32 tmp[4] = {r.x, r.y, r.z, r.w};
-                or_u32_at((u32)Lf[f], t - 4, tmp);
+                or_u32_at((u32)Lf, t - 4, tmp);
                 r = u32x4{tmp[0], tmp[1], tmp[2], tmp[3]};
             }
-            if (need[f]) {
+            if (!careful) {
+                // unconditional use of the load (the mask is zero where the field is absent): a use
+                // inside a skippable branch would leave the load pending on that path, and the
+                // pipelined loop would wait for it at the loop head
+                r |= w[f] & range_mask(masks, t, t + Lf);
+            } else if (t < 16 && t + Lf > 0 && (!MIXED || Lf > 0)) {
                 u32x4 v = w[f];
-                if (careful && !fast[f]) {  // batch edges: aligned blocks holding valid bytes only
-                    u32 tmp[4] = {0, 0, 0, 0};
-                    or_window_global(X[f], max(t, 0), min(t + Lf[f], 16), tmp);
-                    v = u32x4{tmp[0], tmp[1], tmp[2], tmp[3]};
+                {  // batch edges: windows reaching outside the column are read blockwise
+                    const uintptr_t X = (uintptr_t)(S.delta[f][j] + (u64)(i64)P);
+                    const uintptr_t c0 = (uintptr_t)(p.bytes[f] + p.offs[f][0]) & ~(uintptr_t)15;
+                    const uintptr_t c1 = ((uintptr_t)(p.bytes[f] + p.offs[f][p.n]) + 15) & ~(uintptr_t)15;
+                    if (!(X >= c0 && X + 16 <= c1)) {  // aligned blocks holding valid bytes only
+                        u32 tmp[4] = {0, 0, 0, 0};
+                        or_window_global(X, max(t, 0), min(t + Lf, 16), tmp);
+                        v = u32x4{tmp[0], tmp[1], tmp[2], tmp[3]};
+                    }
                 }
-                r |= v & range_mask(masks, t, t + Lf[f]);
+                r |= v & range_mask(masks, t, t + Lf);
             }
-            t += Lf[f] + 4;
+            t += Lf + 4;
         }
         if (j + 1 < cnt) {  // the next record's header may start inside this chunk
             const int nb = P - S.o[j + 1];
@@ -245,13 +280,68 @@ __global__ __launch_bounds__(256) void encode_kernel(EncodeParams p) {
         const u32 rr[4] = {r.x, r.y, r.z, r.w};
         store_chunk(out_t, P, 0, span, rr);
     };
+    auto chunk = [&](int P, int j, bool careful) {
+        u32x4 w[NV];
+        fetch(P, j, careful, w);
+        assemble(P, j, careful, w);
+    };
 
+    if constexpr (kVariant == 1) {  // pipelined: step s+1's loads are in flight across step s's store
+        if (!tile_safe) {
+            for (int B = first + 16 * 64 * (WPT == 1 ? 0 : wave); B < span; B += 16 * 64 * WPT) {
+                const int j = locate(B);
+                const int P = B + 16 * lane;
+                if (P < span) chunk(P, j, true);
+            }
+            return;
+        }
+        // Straight-line software pipeline over the first kPipe steps (ping-pong registers): step
+        // s+1's loads are issued before step s is assembled and stored.  Every path that fetches
+        // a register set also consumes it and no value of a pending load reaches a join or a loop
+        // head (the compiler would copy it there, waiting for every load in flight); steps past
+        // kPipe run in a plain loop (the last pipelined fetch is then simply not used).
+        constexpr int kStep = 16 * 64 * WPT, kPipe = 8;
+        int B = first + 16 * 64 * (WPT == 1 ? 0 : wave);  // the next step to store
+        if (B < span) {
+            u32x4 wa[NV], wb[NV];
+            int ja = locate(B);
+            fetch(B + 16 * lane, ja, false, wa);
+#pragma unroll
+            for (int st = 0; st < kPipe; st += 2) {
+                if (B + kStep >= span) {
+                    assemble(B + 16 * lane, ja, false, wa);  // lanes past the span store nothing
+                    B = span;
+                    break;
+                }
+                const int jb = locate(B + kStep);
+                fetch(B + kStep + 16 * lane, jb, false, wb);
+                assemble(B + 16 * lane, ja, false, wa);
+                B += kStep;
+                if (B + kStep >= span) {
+                    assemble(B + 16 * lane, jb, false, wb);
+                    B = span;
+                    break;
+                }
+                ja = locate(B + kStep);
+                fetch(B + kStep + 16 * lane, ja, false, wa);
+                assemble(B + 16 * lane, jb, false, wb);
+                B += kStep;
+            }
+        }
+        for (; B < span; B += kStep) {  // wave-uniform loop
+            const int j = locate(B);
+            if (B + 16 * lane < span) chunk(B + 16 * lane, j, false);
+        }
+        if (DIAG && lane == 0) stamp[2 + (WPT == 1 ? 0 : wave)] = __builtin_amdgcn_s_memrealtime();
+        return;
+    }
     if constexpr (kVariant == 0) {
-        for (int B = first; B < span; B += 16 * 64) {  // wave-uniform loop
+        for (int B = first + 16 * 64 * (WPT == 1 ? 0 : wave); B < span; B += 16 * 64 * WPT) {  // wave-uniform loop
             const int j = locate(B);
             const int P = B + 16 * lane;
             if (P < span) chunk(P, j, !tile_safe);
         }
+        if (DIAG && lane == 0) stamp[2 + (WPT == 1 ? 0 : wave)] = __builtin_amdgcn_s_memrealtime();
         return;
     }
     if (!tile_safe) {  // batch-edge tiles (two per batch): the careful one-step path
@@ -314,31 +404,45 @@ __global__ __launch_bounds__(256) void encode_kernel(EncodeParams p) {
     }
 }
 
+static dim3 encode_grid(u64 n, int wpt) {
+    const u64 tiles = (n + kWaveRecs - 1) / kWaveRecs;
+    return dim3((unsigned)(wpt == 1 ? (tiles + kWaves - 1) / kWaves : tiles));
+}
+
 template <int NF, int NV>
-static void launch_layout(const EncodeParams& p, dim3 grid, dim3 block, hipStream_t stream) {
+static void launch_layout(const EncodeParams& p, hipStream_t stream) {
+    const dim3 block(64 * kWaves);
 #ifdef SYMHIP_TUNING
     // variants 2/4: that many steps' loads in flight per wave (measured no faster on MI355X: the
-    // one-step loop already runs at ~92 % of a plain 350 MB copy, tools/ubench_copy.hip)
+    // one-step loop already runs at ~92 % of a plain 350 MB copy, tools/ubench_copy.hip);
+    // 5: one tile per wave (the round-1 layout)
     switch (p.variant) {
-        case 2: hipLaunchKernelGGL((encode_kernel<NF, NV, 2>), grid, block, 0, stream, p); return;
-        case 4: hipLaunchKernelGGL((encode_kernel<NF, NV, 4>), grid, block, 0, stream, p); return;
+        case 2: hipLaunchKernelGGL((encode_kernel<NF, NV, 2>), encode_grid(p.n, 1), block, 0, stream, p); return;
+        case 4: hipLaunchKernelGGL((encode_kernel<NF, NV, 4>), encode_grid(p.n, 1), block, 0, stream, p); return;
+        case 5: hipLaunchKernelGGL((encode_kernel<NF, NV, 0>), encode_grid(p.n, 1), block, 0, stream, p); return;
+        // 6/7: per-tile timestamps into p.dbg (tools/enc_timeline.py), workgroup tiles / wave tiles
+        case 6: hipLaunchKernelGGL((encode_kernel<NF, NV, 0, false, kWaves, true>), encode_grid(p.n, kWaves), block, 0, stream, p); return;
+        case 7: hipLaunchKernelGGL((encode_kernel<NF, NV, 0, false, 1, true>), encode_grid(p.n, 1), block, 0, stream, p); return;
+        // 8/9: pipelined steps, workgroup tiles / wave tiles; 10: 8 with timestamps
+        case 8: hipLaunchKernelGGL((encode_kernel<NF, NV, 1, false, kWaves>), encode_grid(p.n, kWaves), block, 0, stream, p); return;
+        case 9: hipLaunchKernelGGL((encode_kernel<NF, NV, 1, false, 1>), encode_grid(p.n, 1), block, 0, stream, p); return;
+        case 10: hipLaunchKernelGGL((encode_kernel<NF, NV, 1, false, kWaves, true>), encode_grid(p.n, kWaves), block, 0, stream, p); return;
+        // 15: workgroup tiles, one step at a time (no software pipeline)
+        case 15: hipLaunchKernelGGL((encode_kernel<NF, NV, 0, false, kWaves>), encode_grid(p.n, kWaves), block, 0, stream, p); return;
         default: break;
     }
 #endif
-    hipLaunchKernelGGL((encode_kernel<NF, NV, 0>), grid, block, 0, stream, p);
+    hipLaunchKernelGGL((encode_kernel<NF, NV, 1, false, kWaves>), encode_grid(p.n, kWaves), block, 0, stream, p);
 }
 
 hipError_t launch_encode(const EncodeParams& p, hipStream_t stream) {
     if (p.n == 0) return hipMemsetAsync(p.out_off, 0, sizeof(uint64_t), stream);
-    const u64 tiles = (p.n + kWaveRecs - 1) / kWaveRecs;
-    const dim3 grid((unsigned)((tiles + kWaves - 1) / kWaves));
-    const dim3 block(64 * kWaves);
     if (p.lay.nfixed == 0 && p.lay.nvar == 1)
-        launch_layout<0, 1>(p, grid, block, stream);
+        launch_layout<0, 1>(p, stream);
     else if (p.lay.nfixed == 0 && p.lay.nvar == 2)
-        launch_layout<0, 2>(p, grid, block, stream);
+        launch_layout<0, 2>(p, stream);
     else if (p.lay.nfixed == 2 && p.lay.nvar == 2)
-        launch_layout<2, 2>(p, grid, block, stream);
+        launch_layout<2, 2>(p, stream);
     else
         return hipErrorInvalidValue;
     return hipGetLastError();
@@ -456,9 +560,14 @@ hipError_t launch_encode_mixed(EncodeParams p, void* ws, unsigned* ticket, hipSt
     hipLaunchKernelGGL(mixed_size_kernel, dim3((unsigned)mixed_ngroups(p.n)), dim3(256), 0, stream, p, w, ticket);
     p.group_pre = w.group_pre;
     p.tile_loc = w.tile_loc;
-    const u64 tiles = mixed_ntiles(p.n);
-    hipLaunchKernelGGL((encode_kernel<0, 2, 0, true>), dim3((unsigned)((tiles + kWaves - 1) / kWaves)), dim3(64 * kWaves),
-                       0, stream, p);
+#ifdef SYMHIP_TUNING
+    if (p.variant == 5 || p.variant == 15) {
+        if (p.variant == 5) hipLaunchKernelGGL((encode_kernel<0, 2, 0, true>), encode_grid(p.n, 1), dim3(64 * kWaves), 0, stream, p);
+        else hipLaunchKernelGGL((encode_kernel<0, 2, 0, true, kWaves>), encode_grid(p.n, kWaves), dim3(64 * kWaves), 0, stream, p);
+        return hipGetLastError();
+    }
+#endif
+    hipLaunchKernelGGL((encode_kernel<0, 2, 1, true, kWaves>), encode_grid(p.n, kWaves), dim3(64 * kWaves), 0, stream, p);
     return hipGetLastError();
 }
 

@@ -246,7 +246,7 @@ __global__ __launch_bounds__(256) void write_kernel(SetArgs a) {
         const Plan p = plan_one(a, i, v, fx, src, len);  // every lane: the same (wave-uniform) plan
         const u64 size = p.st ? v.L : p.size;
         const u64 at = a.pre[i / kTile].bytes + a.out_off[i];
-        wave_sync();  // every lane has read its tile-relative offset
+        wave_sync_global();  // every lane has read its tile-relative offset
         if (lane == 0) {
             a.out_off[i] = at;
             if (i == a.n - 1) a.out_off[a.n] = at + size;

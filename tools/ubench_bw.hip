@@ -66,6 +66,17 @@ __global__ __launch_bounds__(256) void copy_k(const unsigned char* src, unsigned
     for (; c < nchunks; c += stride) *(g_u4*)(dst + 16 * c) = *(gc_u4*)(src + 16 * c);
 }
 
+// each workgroup copies K consecutive 4 KiB blocks (its own contiguous K*4 KiB span), one per step
+template <int K>
+__global__ __launch_bounds__(256) void copy_blocks_k(const unsigned char* src, unsigned char* dst, size_t nchunks) {
+    const size_t c0 = (size_t)blockIdx.x * 256 * K + threadIdx.x;
+#pragma unroll 1
+    for (int k = 0; k < K; ++k) {
+        const size_t c = c0 + (size_t)k * 256;
+        if (c < nchunks) *(g_u4*)(dst + 16 * c) = *(gc_u4*)(src + 16 * c);
+    }
+}
+
 int main() {
     int ncu = 0;
     CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
@@ -74,7 +85,7 @@ int main() {
     CHECK(hipEventCreate(&e1));
     u32* sink;
     CHECK(hipMalloc(&sink, 64));
-    const size_t sizes[2] = {(size_t)350 << 20, (size_t)2 << 30};
+    const size_t sizes[3] = {(size_t)350 << 20, (size_t)700 << 20, (size_t)2800 << 20};
     for (size_t bytes : sizes) {
         const int nsets = bytes < ((size_t)1 << 30) ? 4 : 1;
         unsigned char *src[4], *dst[4];
@@ -104,6 +115,9 @@ int main() {
             {"copy   grid-stride x4 nt, 8 WG/CU", 2, 2, (unsigned)ncu * 8},
             {"copy   grid-stride x4, 32 WG/CU", 2, 2, (unsigned)ncu * 32},
             {"copy   one chunk per thread", 2, 2, full},
+            {"copy   4 KiB x4 per WG", 2, 2, (full + 3) / 4},
+            {"copy   4 KiB x16 per WG", 2, 2, (full + 15) / 16},
+            {"copy   4 KiB x64 per WG", 2, 2, (full + 63) / 64},
         };
         printf("--- %zu MiB per buffer, %d rotating set(s)\n", bytes >> 20, nsets);
         for (int ci = 0; ci < (int)(sizeof(cases) / sizeof(cases[0])); ++ci) {
@@ -122,6 +136,9 @@ int main() {
                     case 8: hipLaunchKernelGGL((copy_k<4, 1>), g, b, 0, 0, src[k], dst[k], nch); break;
                     case 9: hipLaunchKernelGGL((copy_k<4, 0>), g, b, 0, 0, src[k], dst[k], nch); break;
                     case 10: hipLaunchKernelGGL((copy_k<1, 0>), g, b, 0, 0, src[k], dst[k], nch); break;
+                    case 11: hipLaunchKernelGGL((copy_blocks_k<4>), g, b, 0, 0, src[k], dst[k], nch); break;
+                    case 12: hipLaunchKernelGGL((copy_blocks_k<16>), g, b, 0, 0, src[k], dst[k], nch); break;
+                    case 13: hipLaunchKernelGGL((copy_blocks_k<64>), g, b, 0, 0, src[k], dst[k], nch); break;
                 }
             };
             for (int k = 0; k < nsets; ++k) launch(k);
