@@ -70,6 +70,10 @@ SIGNATURES = {
     "sym_flat_encoded_size": (_u64, [_vp, _int, _u64, _u64]),
     "sym_flat_encode": (_int, [_ctx, _vp, _int, _u64, _vp, _vp, _u32, _u32, _u8p, _u64p, _vp]),
     "sym_flat_decode": (_int, [_ctx, _vp, _int, _u64, _u8p, _u64p, _vp, _vp, _vp, _u8p, _vp]),
+    "sym_flat_encoded_size_ex": (_u64, [_vp, _int, _u64, _vp, _vp]),
+    "sym_flat_encode_ex": (_int, [_ctx, _vp, _int, _u64, _vp, _vp, _vp, _u32, _u32, _u8p, _u64p, _vp]),
+    "sym_flat_decode_ex": (_int, [_ctx, _vp, _int, _u64, _u8p, _u64p, _vp, _vp, _vp, _vp, _vp, _u8p, _u8p, _vp]),
+    "sym_flat_nested_status": (_int, [_ctx, _vp, _int, _int, _u64, _u64p, _u8p, _u8p, _u8p, _vp]),
     "sym_raw_set": (_int, [_ctx, _vp, _int, _int, _u8p, _u64p, _u64, _vp, _u64p, _u8p, _u64, _u64p, _u8p, _vp]),
     "sym_encrypt": (_int, [_ctx, _u8p, _u64p, _u64, ctypes.c_char_p, ctypes.c_char_p, _u8p, _u8p, _u64p, _u8p, _vp]),
     "sym_decrypt": (_int, [_ctx, _u8p, _u64p, _u64, ctypes.c_char_p, ctypes.c_char_p, _u8p, _u64p, _u8p, _vp]),
@@ -119,6 +123,8 @@ SYM_SET_BOUNDS = 6
 
 SYM_MAX_FLAT_FIELDS = 16
 SYM_FIELD_REPEATED = 0x80
+SYM_FIELD_MESSAGE = 0x40
+SYM_STATUS_NESTED = 5
 
 
 class SymField(ctypes.Structure):

@@ -15,6 +15,7 @@
 #include "../../include/symphony_hip.h"
 #include "codec.hpp"
 #include "ctx.hpp"
+#include "flat_schema.hpp"
 
 using symhip::DecodeParams;
 using symhip::EncodeParams;
@@ -171,6 +172,9 @@ int sym_ctx_check(sym_ctx* ctx, void* stream) {
     if (bits & symhip::kErrTimeout) return fail(SYM_ERR_DEVICE, "decode look-back timed out (device error bits 0x%x)", bits);
     if (bits & symhip::kErrTooLarge)
         return fail(SYM_ERR_INVALID, "64 consecutive records span >= 2 GiB; split the batch (device error bits 0x%x)", bits);
+    if (bits & symhip::kErrBadNested)
+        return fail(SYM_ERR_INVALID, "a nested (non-repeated) message field was given more than one item for a record "
+                    "(device error bits 0x%x)", bits);
     if (bits & symhip::kErrBadLength)
         return fail(SYM_ERR_INVALID, "a repeated field's byte length is not a multiple of its element width "
                     "(device error bits 0x%x)", bits);
@@ -583,20 +587,26 @@ int sym_reassemble(sym_ctx* ctx, const uint8_t* d_wire, const uint64_t* d_dg_off
     return e == hipSuccess ? SYM_OK : hip_fail(e, "reassembly launch");
 }
 
-static int flat_check(const char* what, const sym_field* fields, int nf) {
+// lists: accept the list-like widths (repeated string / bytes, nested and repeated messages)
+static int flat_check(const char* what, const sym_field* fields, int nf, bool lists) {
     if (nf < 0 || nf > SYM_MAX_FLAT_FIELDS || (nf && !fields))
         return fail(SYM_ERR_INVALID, "%s: %d fields (0..%d)", what, nf, SYM_MAX_FLAT_FIELDS);
     for (int k = 0; k < nf; ++k) {
         if (fields[k].segment > 1) return fail(SYM_ERR_INVALID, "%s: field %d segment %u", what, k, fields[k].segment);
-        const unsigned w = fields[k].width & ~SYM_FIELD_REPEATED, rep = fields[k].width & SYM_FIELD_REPEATED;
-        if ((w != 0 && w != 1 && w != 4 && w != 8) || (rep && w == 0))
-            return fail(SYM_ERR_INVALID, "%s: field %d width 0x%x", what, k, fields[k].width);
+        const unsigned wd = fields[k].width;
+        const unsigned w = wd & ~(SYM_FIELD_REPEATED | SYM_FIELD_MESSAGE), rep = wd & SYM_FIELD_REPEATED;
+        const bool list = symhip::flat::list_kind(fields[k]) != symhip::flat::kListNone;
+        if ((w != 0 && w != 1 && w != 4 && w != 8) || ((wd & SYM_FIELD_MESSAGE) && w != 0) || (list && !lists) ||
+            (rep && w == 0 && !lists))
+            return fail(SYM_ERR_INVALID, "%s: field %d width 0x%x%s", what, k, wd,
+                        list && !lists ? " (list-like fields need the _ex entry points)" : "");
     }
     return SYM_OK;
 }
 
 // scalar fixed-width field (a value column, no offsets); else string or repeated (bytes + offsets)
-static bool flat_scalar(const sym_field& f) { return f.width != 0 && !(f.width & SYM_FIELD_REPEATED); }
+static bool flat_scalar(const sym_field& f) { return !symhip::flat::is_payload(f); }
+static bool flat_list(const sym_field& f) { return symhip::flat::list_kind(f) != symhip::flat::kListNone; }
 
 uint64_t sym_flat_encoded_size(const sym_field* fields, int nfields, uint64_t n, uint64_t var_total) {
     if (nfields == 0) return 14 * n;
@@ -606,16 +616,31 @@ uint64_t sym_flat_encoded_size(const sym_field* fields, int nfields, uint64_t n,
     return per * n + var_total;
 }
 
-int sym_flat_encode(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const void* const* d_cols,
-                    const uint64_t* const* d_offs, uint32_t service_id, uint32_t method_id, uint8_t* d_out,
-                    uint64_t* d_out_off, void* stream) {
+uint64_t sym_flat_encoded_size_ex(const sym_field* fields, int nfields, uint64_t n, const uint64_t* bytes,
+                                  const uint64_t* items) {
+    if (nfields == 0) return 14 * n;
+    uint64_t t = 14 * n;
+    for (int k = 0; k < nfields; ++k) {
+        const sym_field& f = fields[k];
+        const uint64_t b = bytes ? bytes[k] : 0, m = items ? items[k] : 0;
+        if (flat_scalar(f)) t += (uint64_t)f.width * n;
+        else if (!flat_list(f)) t += 8 * n + b;  // entry + prefix + payload
+        else if (f.width & SYM_FIELD_REPEATED) t += 8 * n + 4 * m + b;  // entry + count + items
+        else t += 4 * n + 4 * m + b;  // nested: entry, and [len] + message when present
+    }
+    return t;
+}
+
+int sym_flat_encode_ex(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const void* const* d_cols,
+                       const uint64_t* const* d_offs, const uint64_t* const* d_items, uint32_t service_id,
+                       uint32_t method_id, uint8_t* d_out, uint64_t* d_out_off, void* stream) {
     if (!ctx) return fail(SYM_ERR_INVALID, "sym_flat_encode: ctx is NULL");
-    int rc = flat_check("sym_flat_encode", fields, nfields);
+    int rc = flat_check("sym_flat_encode", fields, nfields, d_items != nullptr);
     if (rc != SYM_OK) return rc;
     if (!d_out_off || (n && (!d_out || (nfields && (!d_cols || !d_offs)))))
         return fail(SYM_ERR_INVALID, "sym_flat_encode: NULL argument");
     for (int k = 0; k < nfields && n; ++k) {
-        if (!d_cols[k] || (!flat_scalar(fields[k]) && !d_offs[k]))
+        if (!d_cols[k] || (!flat_scalar(fields[k]) && !d_offs[k]) || (flat_list(fields[k]) && !d_items[k]))
             return fail(SYM_ERR_INVALID, "sym_flat_encode: field %d has no column", k);
         if (flat_scalar(fields[k]) && (uintptr_t)d_cols[k] % fields[k].width)
             return fail(SYM_ERR_INVALID, "sym_flat_encode: field %d column not %u-byte aligned", k, fields[k].width);
@@ -626,43 +651,84 @@ int sym_flat_encode(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t
         hipError_t e = hipMemsetAsync(d_out_off, 0, sizeof(uint64_t), (hipStream_t)stream);
         return e == hipSuccess ? SYM_OK : hip_fail(e, "hipMemsetAsync");
     }
-    hipError_t e = symhip::launch_flat_encode(fields, nfields, n, d_cols, d_offs, service_id, method_id, d_out,
-                                              d_out_off, ctx->err, (hipStream_t)stream);
+    hipError_t e = symhip::launch_flat_encode(fields, nfields, n, d_cols, d_offs, d_items, service_id, method_id,
+                                              d_out, d_out_off, ctx->err, (hipStream_t)stream);
     return e == hipSuccess ? SYM_OK : hip_fail(e, "flat encode launch");
+}
+
+int sym_flat_encode(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const void* const* d_cols,
+                    const uint64_t* const* d_offs, uint32_t service_id, uint32_t method_id, uint8_t* d_out,
+                    uint64_t* d_out_off, void* stream) {
+    return sym_flat_encode_ex(ctx, fields, nfields, n, d_cols, d_offs, nullptr, service_id, method_id, d_out,
+                              d_out_off, stream);
+}
+
+int sym_flat_decode_ex(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const uint8_t* d_in,
+                       const uint64_t* d_rec_off, void* const* d_cols, const uint64_t* caps, uint64_t* const* d_offs,
+                       uint64_t* const* d_items, const uint64_t* item_caps, uint8_t* d_status, uint8_t* d_fail,
+                       void* stream) {
+    if (!ctx) return fail(SYM_ERR_INVALID, "sym_flat_decode: ctx is NULL");
+    const bool lists = d_items != nullptr;
+    int rc = flat_check("sym_flat_decode", fields, nfields, lists);
+    if (rc != SYM_OK) return rc;
+    if (n && (!d_in || !d_rec_off || !d_status || (nfields && (!d_cols || !caps || !d_offs))))
+        return fail(SYM_ERR_INVALID, "sym_flat_decode: NULL argument");
+    for (int k = 0; k < nfields; ++k) {
+        if ((n && !d_cols[k] && (flat_scalar(fields[k]) || caps[k])) || (!flat_scalar(fields[k]) && !d_offs[k]))
+            return fail(SYM_ERR_INVALID, "sym_flat_decode: field %d has no column", k);
+        if (flat_list(fields[k]) && (!item_caps || !d_items[k]))
+            return fail(SYM_ERR_INVALID, "sym_flat_decode: list-like field %d needs d_items and item_caps", k);
+    }
+    DeviceGuard g(ctx->device);
+    if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
+    if (n == 0) {
+        for (int k = 0; k < nfields; ++k) {
+            hipError_t e = hipSuccess;
+            if (!flat_scalar(fields[k])) e = hipMemsetAsync(d_offs[k], 0, sizeof(uint64_t), (hipStream_t)stream);
+            if (e == hipSuccess && flat_list(fields[k]))
+                e = hipMemsetAsync(d_items[k], 0, sizeof(uint64_t), (hipStream_t)stream);
+            if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync");
+        }
+        return SYM_OK;
+    }
+    if ((rc = ensure_scratch(ctx, symhip::flat_ws_bytes(fields, nfields, n, item_caps), "flat decode")) != SYM_OK)
+        return rc;
+    hipError_t e = symhip::launch_flat_decode(fields, nfields, n, d_in, d_rec_off, d_cols, caps, d_offs, d_items,
+                                              item_caps, d_status, d_fail, ctx->frag, ctx->err, (hipStream_t)stream);
+    return e == hipSuccess ? SYM_OK : hip_fail(e, "flat decode launch");
 }
 
 int sym_flat_decode(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const uint8_t* d_in,
                     const uint64_t* d_rec_off, void* const* d_cols, const uint64_t* caps, uint64_t* const* d_offs,
                     uint8_t* d_status, void* stream) {
-    if (!ctx) return fail(SYM_ERR_INVALID, "sym_flat_decode: ctx is NULL");
-    int rc = flat_check("sym_flat_decode", fields, nfields);
+    return sym_flat_decode_ex(ctx, fields, nfields, n, d_in, d_rec_off, d_cols, caps, d_offs, nullptr, nullptr,
+                              d_status, nullptr, stream);
+}
+
+int sym_flat_nested_status(sym_ctx* ctx, const sym_field* fields, int nfields, int field, uint64_t n,
+                           const uint64_t* d_rec_items, const uint8_t* d_item_status, uint8_t* d_status,
+                           uint8_t* d_fail, void* stream) {
+    if (!ctx) return fail(SYM_ERR_INVALID, "sym_flat_nested_status: ctx is NULL");
+    int rc = flat_check("sym_flat_nested_status", fields, nfields, true);
     if (rc != SYM_OK) return rc;
-    if (n && (!d_in || !d_rec_off || !d_status || (nfields && (!d_cols || !caps || !d_offs))))
-        return fail(SYM_ERR_INVALID, "sym_flat_decode: NULL argument");
+    if (field < 0 || field >= nfields || !(fields[field].width & SYM_FIELD_MESSAGE))
+        return fail(SYM_ERR_INVALID, "sym_flat_nested_status: field %d is not a message field", field);
+    if (n && (!d_rec_items || !d_item_status || !d_status || !d_fail))
+        return fail(SYM_ERR_INVALID, "sym_flat_nested_status: NULL argument");
+    uint32_t pos = 0;  // the field's position in unmarshal order: public fields, then private
     for (int k = 0; k < nfields; ++k)
-        if ((n && !d_cols[k] && (flat_scalar(fields[k]) || caps[k])) || (!flat_scalar(fields[k]) && !d_offs[k]))
-            return fail(SYM_ERR_INVALID, "sym_flat_decode: field %d has no column", k);
+        if (fields[k].segment < fields[field].segment || (fields[k].segment == fields[field].segment && k < field)) ++pos;
     DeviceGuard g(ctx->device);
     if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
-    if (n == 0) {
-        for (int k = 0; k < nfields; ++k)
-            if (!flat_scalar(fields[k])) {
-                hipError_t e = hipMemsetAsync(d_offs[k], 0, sizeof(uint64_t), (hipStream_t)stream);
-                if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync");
-            }
-        return SYM_OK;
-    }
-    if ((rc = ensure_scratch(ctx, symhip::flat_ws_bytes(fields, nfields, n), "flat decode")) != SYM_OK) return rc;
-    hipError_t e = symhip::launch_flat_decode(fields, nfields, n, d_in, d_rec_off, d_cols, caps, d_offs, d_status,
-                                              ctx->frag, ctx->err, (hipStream_t)stream);
-    return e == hipSuccess ? SYM_OK : hip_fail(e, "flat decode launch");
+    hipError_t e = symhip::launch_nested_status(n, pos, d_rec_items, d_item_status, d_status, d_fail, (hipStream_t)stream);
+    return e == hipSuccess ? SYM_OK : hip_fail(e, "nested status launch");
 }
 
 int sym_raw_set(sym_ctx* ctx, const sym_field* fields, int nfields, int field, const uint8_t* d_in,
                 const uint64_t* d_rec_off, uint64_t n, const void* d_val, const uint64_t* d_val_off, uint8_t* d_out,
                 uint64_t out_cap, uint64_t* d_out_off, uint8_t* d_status, void* stream) {
     if (!ctx) return fail(SYM_ERR_INVALID, "sym_raw_set: ctx is NULL");
-    int rc = flat_check("sym_raw_set", fields, nfields);
+    int rc = flat_check("sym_raw_set", fields, nfields, false);
     if (rc != SYM_OK) return rc;
     if (field < 0 || field >= nfields) return fail(SYM_ERR_INVALID, "sym_raw_set: field %d of %d", field, nfields);
     const bool scalar = flat_scalar(fields[field]);

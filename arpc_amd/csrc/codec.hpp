@@ -78,6 +78,7 @@ struct DecodeWsHeader {
 constexpr unsigned kErrCapacity = 1u;
 constexpr unsigned kErrTimeout = 2u;   // a bounded device-side wait gave up (no kernel sets it today)
 constexpr unsigned kErrTooLarge = 4u;  // 64 consecutive records spanning >= 2 GiB
+constexpr unsigned kErrBadNested = 16u;  // flat encode: a (non-repeated) nested field given more than one item
 constexpr unsigned kErrBadLength = 8u;  // flat encode: a repeated field's byte length is not a multiple of its width
 
 size_t decode_workspace_bytes(int nvar, uint64_t n);
@@ -149,13 +150,16 @@ hipError_t launch_segment_gather(const raw::GatherArgs& a, hipStream_t stream);
 }  // namespace symhip
 struct sym_field;
 namespace symhip {
-size_t flat_ws_bytes(const sym_field* f, int nf, uint64_t n);
+size_t flat_ws_bytes(const sym_field* f, int nf, uint64_t n, const uint64_t* item_caps);
 hipError_t launch_flat_encode(const sym_field* f, int nf, uint64_t n, const void* const* cols,
-                              const uint64_t* const* offs, uint32_t sid, uint32_t mid, uint8_t* out,
-                              uint64_t* out_off, unsigned* err, hipStream_t stream);
+                              const uint64_t* const* offs, const uint64_t* const* items, uint32_t sid, uint32_t mid,
+                              uint8_t* out, uint64_t* out_off, unsigned* err, hipStream_t stream);
 hipError_t launch_flat_decode(const sym_field* f, int nf, uint64_t n, const uint8_t* in, const uint64_t* rec_off,
-                              void* const* cols, const uint64_t* caps, uint64_t* const* offs, uint8_t* status,
-                              void* ws, unsigned* err, hipStream_t stream);
+                              void* const* cols, const uint64_t* caps, uint64_t* const* offs, uint64_t* const* items,
+                              const uint64_t* item_caps, uint8_t* status, uint8_t* fail, void* ws, unsigned* err,
+                              hipStream_t stream);
+hipError_t launch_nested_status(uint64_t n, uint32_t pos, const uint64_t* rec_items, const uint8_t* item_status,
+                                uint8_t* status, uint8_t* fail, hipStream_t stream);
 
 // ---- batched Raw setters (setters.hip)
 size_t raw_set_ws_bytes(uint64_t n);

@@ -229,3 +229,40 @@ def make_element_batch(n: int, lens: tuple, seed: int, score_range=(0, 100)) -> 
         strings.append((random_bytes(seed + 0x100000000 * (f + 1), int(offs[-1])), offs))
     data, rec_off = element_records(score, strings)
     return ElementBatch(score, strings, data, rec_off)
+
+
+# ---- online-boutique messages (benchmark/serialization/online-boutique/proto/onlineboutique.proto):
+# synthetic PlaceOrderResponse batches as column trees for arpc_amd.flat (numpy, host side).
+# A tree node is: a numpy array (scalar column), (bytes, offsets) (string), ("list", bytes,
+# item_off, rec) (repeated string), or ("msg", [child nodes], rec) (message / repeated message).
+def _strings(rng, n: int, lo: int, hi: int):
+    ln = rng.integers(lo, hi + 1, size=n, dtype=np.int64)
+    off = np.zeros(n + 1, np.int64)
+    np.cumsum(ln, out=off[1:])
+    return rng.integers(32, 127, size=int(off[-1]), dtype=np.uint8), off
+
+
+def _present(n: int):
+    return np.arange(n + 1, dtype=np.int64)
+
+
+def _money(rng, n: int):
+    return ("msg", [_strings(rng, n, 3, 3), rng.integers(0, 10_000, size=n, dtype=np.int64),
+                    rng.integers(0, 999_999_999, size=n, dtype=np.int32)], _present(n))
+
+
+def ob_place_order(n: int, seed: int = 0x5EED0B00, items=(1, 5)) -> tuple:
+    """n PlaceOrderResponse{OrderResult{order id, tracking id, Money, Address, 1..5 OrderItem{CartItem,
+    Money}}} as a column tree (see above); the message sizes are those of the demo's checkout."""
+    rng = np.random.default_rng(seed)
+    cnt = rng.integers(items[0], items[1] + 1, size=n, dtype=np.int64)
+    rec_items = np.zeros(n + 1, np.int64)
+    np.cumsum(cnt, out=rec_items[1:])
+    m = int(rec_items[-1])
+    cart = ("msg", [_strings(rng, m, 10, 10), rng.integers(1, 10, size=m, dtype=np.int32)], _present(m))
+    order_item = ("msg", [cart, _money(rng, m)], rec_items)
+    address = ("msg", [_strings(rng, n, 12, 30), _strings(rng, n, 5, 15), _strings(rng, n, 2, 2),
+                       _strings(rng, n, 6, 20), rng.integers(10000, 99999, size=n, dtype=np.int32)], _present(n))
+    order = ("msg", [_strings(rng, n, 36, 36), _strings(rng, n, 18, 18), _money(rng, n), address, order_item],
+             _present(n))
+    return ("msg", [order], None)

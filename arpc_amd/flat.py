@@ -1,20 +1,33 @@
-"""Any flat Symphony schema on the GPU (the flat part).
+"""Any Symphony schema on the GPU: flat, repeated and nested.
 
 Reference: the protoc-gen-symphony generator emits, per message, MarshalSymphony / UnmarshalSymphony
 whose layout follows the fields' kinds and `is_public` flags
-(cmd/symphony-gen-arpc/protoc-gen-symphony/main.go:196-368 marshal, :622-800 unmarshal; field
-classification :1172-1239).  Here the message is described at run time -- `FlatSchema` lists the
-fields in declaration order -- and one pair of kernels serves every flat schema (arpc_amd/csrc/
-flat.hip, `sym_flat_encode` / `sym_flat_decode`).  Repeated fixed-width fields are covered;
-repeated string and nested fields are not.
+(cmd/symphony-gen-arpc/protoc-gen-symphony/main.go:196-368 marshal, :622-800 unmarshal, :493-620 and
+:843-947 repeated / nested; field classification :1172-1239).  Here the message is described at run
+time -- `FlatSchema` lists the fields in declaration order -- and one set of kernels serves every
+schema (arpc_amd/csrc/flat.hip, `sym_flat_encode_ex` / `sym_flat_decode_ex`).  A message-typed
+field is one level of that codec: `encode` / `decode` below walk the message tree, encoding inner
+messages first (their bytes become the outer field's items) and decoding outer records first (their
+items become the inner records), folding inner statuses back with `sym_flat_nested_status`.
 
 Kinds (protobuf scalar -> table width): bool 1; int32, uint32, float, enum 4; int64, uint64,
-double 8; string, bytes 0 (a 4-byte payload offset in the table, then length + bytes).
+double 8; string, bytes 0 (a 4-byte payload offset in the table, then length + bytes); message
+(a 4-byte offset, then length + the inner message, or a 0 offset when nil).
+
+Columns (per field, n records):
+  scalar                  tensor of n values
+  string / bytes          (uint8 bytes, int64 offsets [n+1])
+  repeated scalar         (uint8 element bytes, int64 byte offsets [n+1])
+  repeated string / bytes ListColumn(bytes, item_off [m+1], rec [n+1]: record i has items rec[i]..rec[i+1])
+  message                 MessageColumn(cols of the inner schema over m present messages, rec [n+1], at
+                          most one per record; none = nil)
+  repeated message        MessageColumn(cols over m items, rec [n+1])
 """
 from __future__ import annotations
 
-from dataclasses import dataclass
+from dataclasses import dataclass, field as dc_field
 
+import numpy as np
 import torch
 
 from . import _native
@@ -30,24 +43,52 @@ DTYPE = {"bool": torch.uint8, "int32": torch.int32, "uint32": torch.int32, "floa
 class FlatField:
     """One field; `repeated` with a fixed-width kind is `repeated int32 xs` etc. (payload: u32
     count + elements, main.go:493-535, :795-841), carried like a string column: (element bytes,
-    int64 byte offsets [n+1])."""
+    int64 byte offsets [n+1]).  kind "message" takes the inner schema in `message`."""
     name: str
     kind: str
     public: bool = False
     repeated: bool = False
+    message: "FlatSchema | None" = None
 
     def __post_init__(self):
-        if self.repeated and not WIDTH[self.kind]:
-            raise ValueError(f"{self.name}: repeated {self.kind} fields are not covered")
+        if (self.kind == "message") != (self.message is not None):
+            raise ValueError(f"{self.name}: a message field names its schema (and only it does)")
+        if self.kind != "message" and self.kind not in WIDTH:
+            raise ValueError(f"{self.name}: unknown kind {self.kind}")
+
+    @property
+    def list_like(self) -> bool:
+        """Repeated string / bytes, nested and repeated messages: item lists on the C-ABI."""
+        return self.kind == "message" or (self.repeated and not WIDTH[self.kind])
 
     @property
     def width(self) -> int:
-        """Scalar width of a fixed field's value column; 0 for string and repeated fields."""
-        return 0 if self.repeated else WIDTH[self.kind]
+        """Scalar width of a fixed field's value column; 0 for payload fields."""
+        return 0 if self.repeated or self.kind == "message" else WIDTH[self.kind]
 
     @property
     def c_width(self) -> int:
+        if self.kind == "message":
+            return _native.SYM_FIELD_MESSAGE | (_native.SYM_FIELD_REPEATED if self.repeated else 0)
         return (_native.SYM_FIELD_REPEATED | WIDTH[self.kind]) if self.repeated else WIDTH[self.kind]
+
+
+@dataclass
+class ListColumn:
+    """Items of a list-like field: bytes, item byte offsets [m+1], record item ranges [n+1]."""
+    bytes: torch.Tensor
+    item_off: torch.Tensor
+    rec: torch.Tensor
+
+
+@dataclass
+class MessageColumn:
+    """Inner messages of a message field: the inner schema's columns over its m items, the record
+    item ranges [n+1], and (decode) the items' statuses."""
+    cols: list
+    rec: torch.Tensor
+    status: torch.Tensor | None = None
+    n_items: int = 0
 
 
 @dataclass(frozen=True)
@@ -61,6 +102,10 @@ class FlatSchema:
             arr[k].segment = _native.SYM_SEGMENT_PUBLIC if f.public else _native.SYM_SEGMENT_PRIVATE
             arr[k].width = f.c_width
         return arr
+
+    @property
+    def has_lists(self) -> bool:
+        return any(f.list_like for f in self.fields)
 
 
 # benchmark/kv-store-symphony-element/symphony/kv.proto:18-41 (score and username public)
@@ -79,32 +124,59 @@ TEST_FIXED = FlatSchema("Fixed", (FlatField("FInt32", "int32", True), FlatField(
 
 def encode(codec: Codec, schema: FlatSchema, cols: list, service_id: int = 0, method_id: int = 0,
            stream=None, n: int | None = None, out=None):
-    """cols[k]: tensor of n values (fixed field; any dtype of the field's width) or (uint8 bytes,
-    int64 offsets [n+1]) (string field).  -> (stream uint8, offsets int64 [n+1]).  `n` is needed
+    """cols[k] per the module docstring.  -> (stream uint8, offsets int64 [n+1]).  `n` is needed
     only for a schema without fields (n empty messages).  out=(uint8 buffer, int64 [n+1]) skips
-    the size query (a device sync): the buffer must hold encoded_size bytes."""
+    the size query (a device sync): the buffer must hold the encoded size.  Message fields are
+    encoded first (their own message fields first), with service / method ids 0 as
+    MarshalSymphony writes for nested messages."""
     if len(cols) != len(schema.fields):
         raise ValueError(f"{schema.name}: {len(schema.fields)} columns expected")
     if not schema.fields and n is None:
         raise ValueError(f"{schema.name}: a schema without fields needs the record count n")
-    var_total, ptrs, offs, n_arg = 0, [], [], n
+    ptrs, offs, items, nbytes, nitems, n_arg = [], [], [], [], [], n
+    keep = []  # inner streams must outlive the launch
     n = None if schema.fields else n
     for f, c in zip(schema.fields, cols):
-        if f.width:
+        if f.kind == "message":
+            if not isinstance(c, MessageColumn):
+                raise ValueError(f"{f.name}: a MessageColumn expected")
+            m_in = int(c.rec[-1].item() - c.rec[0].item()) if c.rec.numel() > 1 else 0
+            ib, io = encode(codec, f.message, c.cols, stream=stream, n=m_in if not c.cols else None)
+            c = ListColumn(ib, io, c.rec)
+            keep.append(c)
+        if f.list_like:
+            _check_col(c.bytes, torch.uint8, f.name, codec.device)
+            _check_col(c.item_off, torch.int64, f.name + " item offsets", codec.device)
+            _check_col(c.rec, torch.int64, f.name + " record items", codec.device)
+            m = c.rec.numel() - 1
+            ptrs.append(_dptr(c.bytes) or 1)
+            offs.append(_dptr(c.rec))
+            items.append(_dptr(c.item_off))
+            if out is None:
+                j0, j1 = (int(x) for x in c.rec[[0, -1]].tolist()) if m else (0, 0)
+                o = c.item_off[[j0, j1]].tolist() if c.item_off.numel() else [0, 0]
+                nbytes.append(int(o[1] - o[0]))
+                nitems.append(j1 - j0)
+        elif f.width:
             if c.element_size() != f.width or c.device != codec.device or not c.is_contiguous():
                 raise ValueError(f"{f.name}: a contiguous {f.width}-byte column on {codec.device} expected")
             m = c.numel()
             ptrs.append(_dptr(c) or 1)
             offs.append(0)
+            items.append(0)
+            nbytes.append(0)
+            nitems.append(0)
         else:
             b, o = c
             _check_col(b, torch.uint8, f.name, codec.device)
             _check_col(o, torch.int64, f.name + " offsets", codec.device)
             m = o.numel() - 1
             if out is None:
-                var_total += int(o[-1].item() - o[0].item()) if m else 0
+                nbytes.append(int(o[-1].item() - o[0].item()) if m else 0)
+            nitems.append(0)
             ptrs.append(_dptr(b) or 1)
             offs.append(_dptr(o))
+            items.append(0)
         if n is not None and m != n:
             raise ValueError("columns disagree on the record count")
         n = m
@@ -113,7 +185,8 @@ def encode(codec: Codec, schema: FlatSchema, cols: list, service_id: int = 0, me
     n = n or 0
     cf = schema.c_fields()
     if out is None:
-        size = codec._lib.sym_flat_encoded_size(cf, len(schema.fields), n, var_total)
+        size = codec._lib.sym_flat_encoded_size_ex(cf, len(schema.fields), n, _native.u64_array(nbytes or [0]),
+                                                   _native.u64_array(nitems or [0]))
         out = torch.empty(max(1, size), dtype=torch.uint8, device=codec.device)
         off = torch.empty(n + 1, dtype=torch.int64, device=codec.device)
     else:
@@ -123,23 +196,27 @@ def encode(codec: Codec, schema: FlatSchema, cols: list, service_id: int = 0, me
         if off.numel() != n + 1:
             raise ValueError("out offsets: n + 1 entries expected")
         size = out.numel()
-    _native.check(codec._lib.sym_flat_encode(codec._ctx, cf, len(schema.fields), n, _native.ptr_array(ptrs),
-                                            _native.ptr_array(offs), service_id, method_id, _dptr(out), _dptr(off),
-                                            _stream_handle(codec.device, stream)), "sym_flat_encode")
+    lists = schema.has_lists
+    _native.check(codec._lib.sym_flat_encode_ex(codec._ctx, cf, len(schema.fields), n, _native.ptr_array(ptrs),
+                                               _native.ptr_array(offs), _native.ptr_array(items) if lists else None,
+                                               service_id, method_id, _dptr(out), _dptr(off),
+                                               _stream_handle(codec.device, stream)), "sym_flat_encode_ex")
+    del keep
     return out[:size], off
 
 
 def decode(codec: Codec, schema: FlatSchema, data: torch.Tensor, rec_off: torch.Tensor, stream=None,
-           span: int | None = None):
-    """UnmarshalSymphony into fresh structs -> (cols, status); cols[k] a tensor of n values (fixed,
-    dtype of its kind) or (uint8 bytes, int64 offsets [n+1]) (string).  span = rec_off[n] -
-    rec_off[0] when the caller knows it (skips a device sync)."""
+           span: int | None = None, with_fail: bool = False):
+    """UnmarshalSymphony into fresh structs -> (cols, status) (with_fail: (cols, status, fail)); cols
+    per the module docstring, message fields decoded recursively with their items' statuses folded
+    into `status` (SYM_STATUS_NESTED).  span = rec_off[n] - rec_off[0] when the caller knows it
+    (skips a device sync)."""
     _check_col(data, torch.uint8, "data", codec.device)
     _check_col(rec_off, torch.int64, "rec_off", codec.device)
     n = rec_off.numel() - 1
     if span is None:
         span = int(rec_off[-1].item() - rec_off[0].item()) if n else 0
-    cols, ptrs, caps, offs = [], [], [], []
+    cols, ptrs, caps, offs, items, icaps = [], [], [], [], [], []
     for f in schema.fields:
         if f.width:
             c = torch.empty(max(1, n), dtype=DTYPE[f.kind], device=codec.device)
@@ -147,6 +224,19 @@ def decode(codec: Codec, schema: FlatSchema, data: torch.Tensor, rec_off: torch.
             ptrs.append(_dptr(c))
             caps.append(0)
             offs.append(0)
+            items.append(0)
+            icaps.append(0)
+        elif f.list_like:
+            icap = n if (f.kind == "message" and not f.repeated) else span // 4 + 1  # items hold a [u32 len] each
+            b = torch.empty(max(1, span), dtype=torch.uint8, device=codec.device)
+            io = torch.empty(icap + 1, dtype=torch.int64, device=codec.device)
+            rec = torch.empty(n + 1, dtype=torch.int64, device=codec.device)
+            cols.append(ListColumn(b, io, rec))
+            ptrs.append(_dptr(b))
+            caps.append(span)
+            offs.append(_dptr(rec))
+            items.append(_dptr(io))
+            icaps.append(icap)
         else:
             b = torch.empty(max(1, span), dtype=torch.uint8, device=codec.device)
             o = torch.empty(n + 1, dtype=torch.int64, device=codec.device)
@@ -154,13 +244,35 @@ def decode(codec: Codec, schema: FlatSchema, data: torch.Tensor, rec_off: torch.
             ptrs.append(_dptr(b))
             caps.append(span)
             offs.append(_dptr(o))
+            items.append(0)
+            icaps.append(0)
     st = torch.empty(max(1, n), dtype=torch.uint8, device=codec.device)
+    fail = torch.empty(max(1, n), dtype=torch.uint8, device=codec.device)
     cf = schema.c_fields()
-    _native.check(codec._lib.sym_flat_decode(codec._ctx, cf, len(schema.fields), n, _dptr(data) or 1, _dptr(rec_off),
-                                            _native.ptr_array(ptrs), _native.u64_array(caps),
-                                            _native.ptr_array(offs), _dptr(st), _stream_handle(codec.device, stream)),
-                  "sym_flat_decode")
-    return [c[:n] if isinstance(c, torch.Tensor) else c for c in cols], st[:n]
+    lists = schema.has_lists
+    hs = _stream_handle(codec.device, stream)
+    _native.check(codec._lib.sym_flat_decode_ex(codec._ctx, cf, len(schema.fields), n, _dptr(data) or 1,
+                                               _dptr(rec_off), _native.ptr_array(ptrs), _native.u64_array(caps),
+                                               _native.ptr_array(offs), _native.ptr_array(items) if lists else None,
+                                               _native.u64_array(icaps) if lists else None, _dptr(st), _dptr(fail),
+                                               hs), "sym_flat_decode_ex")
+    for k, f in enumerate(schema.fields):
+        if not f.list_like:
+            continue
+        lc = cols[k]
+        m = int(lc.rec[n].item() - lc.rec[0].item()) if n else 0
+        lc.item_off = lc.item_off[:m + 1]
+        lc.bytes = lc.bytes[:int(lc.item_off[-1].item()) if m else 0]
+        if f.kind == "message":
+            # the items are the inner records (item_off[0] == 0): decode them, fold their statuses in
+            inner_cols, inner_st = decode(codec, f.message, lc.bytes, lc.item_off, stream=stream)
+            if n:
+                _native.check(codec._lib.sym_flat_nested_status(codec._ctx, cf, len(schema.fields), k, n,
+                                                                 _dptr(lc.rec), _dptr(inner_st) or 1, _dptr(st),
+                                                                 _dptr(fail), hs), "sym_flat_nested_status")
+            cols[k] = MessageColumn(inner_cols, lc.rec, inner_st, m)
+    out = [c[:n] if isinstance(c, torch.Tensor) else c for c in cols]
+    return (out, st[:n], fail[:n]) if with_fail else (out, st[:n])
 
 
 def _c_fields(fields):
@@ -207,3 +319,46 @@ def raw_set(codec: Codec, fields, k: int, data: torch.Tensor, rec_off: torch.Ten
                                          _dptr(vb) or 1, _dptr(vo) if vo is not None else 0, _dptr(out), out_cap,
                                          _dptr(off), _dptr(st), _stream_handle(codec.device, stream)), "sym_raw_set")
     return out, off, st[:n]
+
+
+# benchmark/serialization/online-boutique/proto/onlineboutique.proto (every field private: the
+# file sets no is_public option); the messages of the PlaceOrder and ListProducts responses
+OB_MONEY = FlatSchema("Money", (FlatField("CurrencyCode", "string"), FlatField("Units", "int64"),
+                                FlatField("Nanos", "int32")))
+OB_CART_ITEM = FlatSchema("CartItem", (FlatField("ProductId", "string"), FlatField("Quantity", "int32")))
+OB_ADDRESS = FlatSchema("Address", (FlatField("StreetAddress", "string"), FlatField("City", "string"),
+                                    FlatField("State", "string"), FlatField("Country", "string"),
+                                    FlatField("ZipCode", "int32")))
+OB_ORDER_ITEM = FlatSchema("OrderItem", (FlatField("Item", "message", message=OB_CART_ITEM),
+                                         FlatField("Cost", "message", message=OB_MONEY)))
+OB_ORDER_RESULT = FlatSchema("OrderResult", (FlatField("OrderId", "string"), FlatField("ShippingTrackingId", "string"),
+                                             FlatField("ShippingCost", "message", message=OB_MONEY),
+                                             FlatField("ShippingAddress", "message", message=OB_ADDRESS),
+                                             FlatField("Items", "message", repeated=True, message=OB_ORDER_ITEM)))
+OB_PLACE_ORDER_RESPONSE = FlatSchema("PlaceOrderResponse", (FlatField("Order", "message", message=OB_ORDER_RESULT),))
+OB_PRODUCT = FlatSchema("Product", (FlatField("Id", "string"), FlatField("Name", "string"),
+                                    FlatField("Description", "string"), FlatField("Picture", "string"),
+                                    FlatField("PriceUsd", "message", message=OB_MONEY),
+                                    FlatField("Categories", "string", repeated=True)))
+OB_LIST_PRODUCTS_RESPONSE = FlatSchema("ListProductsResponse",
+                                       (FlatField("Products", "message", repeated=True, message=OB_PRODUCT),))
+
+
+def columns_from_tree(schema: FlatSchema, nodes: list, device) -> list:
+    """Host column trees (arpc_amd.datagen.ob_place_order) -> device columns for `encode`."""
+    def dev(a):
+        return torch.from_numpy(np.ascontiguousarray(a)).to(device)
+    cols = []
+    for f, nd in zip(schema.fields, nodes):
+        if f.kind == "message":
+            _, children, rec = nd
+            cols.append(MessageColumn(columns_from_tree(f.message, children, device), dev(rec)))
+        elif f.list_like:
+            _, b, io, rec = nd
+            cols.append(ListColumn(dev(b), dev(io), dev(rec)))
+        elif f.width:
+            cols.append(dev(nd))
+        else:
+            b, o = nd
+            cols.append((dev(b), dev(o)))
+    return cols

@@ -69,6 +69,7 @@ extern "C" {
 #define SYM_STATUS_BAD_VERSION 2      /* "invalid data: wrong public version" */
 #define SYM_STATUS_NO_PRIVATE 3       /* "missing private segment"           */
 #define SYM_STATUS_FIELD_TOO_SHORT 4  /* "invalid data: too short for field" (int32 fields) */
+#define SYM_STATUS_NESTED 5           /* "failed to unmarshal nested message" (sym_flat_nested_status) */
 
 /* Flat schemas on the hot path: nfixed int32 fields followed by nvar string fields. */
 #define SYM_SCHEMA_KV_GET_REQUEST 0  /* GetRequest{Key}        kv.syn.go:74-185   (0 fixed, 1 var) */
@@ -348,7 +349,7 @@ int sym_decrypt(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_off, ui
  * 4 (int32 / uint32 / float / enum), 8 (int64 / uint64 / double) or 0 (string / bytes), or
  * SYM_FIELD_REPEATED | 1 / 4 / 8 for a repeated fixed-width field (`repeated int32 xs`: a 4-byte
  * table entry, then a u32 element count and the elements, main.go:493-535 / :795-841).
- * Repeated string and nested fields are not covered.  Columns are indexed by field: d_cols[k] is n
+ * Repeated string / bytes and nested messages: the _ex entry points below.  Columns are indexed by field: d_cols[k] is n
  * little-endian values of `width` bytes (fixed, `width`-aligned) or the packed bytes (string and
  * repeated fixed, with d_offs[k] its n+1 BYTE offsets; a repeated field's record lengths must be
  * multiples of its element width -- the count written is length / width; d_offs[k] is ignored
@@ -363,6 +364,7 @@ int sym_decrypt(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_off, ui
  *                    with d_offs[k][n+1]; d_status[n] SYM_STATUS_*. */
 #define SYM_MAX_FLAT_FIELDS 16
 #define SYM_FIELD_REPEATED 0x80 /* or'ed into sym_field.width: repeated fixed-width field */
+#define SYM_FIELD_MESSAGE 0x40  /* nested message; | SYM_FIELD_REPEATED: repeated message (sym_flat_*_ex) */
 
 typedef struct sym_field {
     uint8_t segment; /* SYM_SEGMENT_PUBLIC / SYM_SEGMENT_PRIVATE */
@@ -370,6 +372,50 @@ typedef struct sym_field {
 } sym_field;
 
 uint64_t sym_flat_encoded_size(const sym_field* fields, int nfields, uint64_t n, uint64_t var_total);
+
+/* ---- Repeated string / bytes and nested messages (the rest) -----------------
+ * List-like fields (generator main.go:537-620 marshal, :843-947 unmarshal):
+ *   width SYM_FIELD_REPEATED            repeated string / bytes: [u32 count] then per item [u32 len][bytes]
+ *   width SYM_FIELD_MESSAGE             nested message: [u32 len][inner MarshalSymphony] when set, and a
+ *                                       0 table entry with no payload when nil
+ *   width SYM_FIELD_REPEATED | SYM_FIELD_MESSAGE   repeated message: as repeated bytes, the items being
+ *                                       inner MarshalSymphony outputs
+ * A message field is one level: its items are the inner messages' bytes, produced (encode) or
+ * consumed (decode) by calls on the inner schema -- the caller walks the message tree
+ * (arpc_amd/flat.py does).  For a list-like field k, d_cols[k] holds the items' bytes,
+ * d_items[k] their byte offsets (m_k + 1 entries, into d_cols[k]) and d_offs[k] each record's item
+ * range (n + 1 item indices: record i has items [d_offs[k][i], d_offs[k][i+1])).  A nested
+ * (non-repeated) field has at most one item per record: none = nil.  Other fields as above.
+ *   sym_flat_encoded_size_ex  exact output size: bytes[k] = payload bytes of field k (strings and
+ *                    repeated fixed: their column bytes; list-like: item bytes), items[k] = items of a
+ *                    list-like field (nested: records where it is set).
+ *   sym_flat_encode_ex  as sym_flat_encode; list bodies are written by a second kernel into the
+ *                    holes the record kernel leaves.  More than one item for a nested field is
+ *                    SYM_ERR_INVALID from sym_ctx_check.
+ *   sym_flat_decode_ex  as sym_flat_decode; list-like field k: item bytes into d_cols[k] (caps[k]),
+ *                    item offsets into d_items[k] (item_caps[k] + 1 entries) and record item ranges
+ *                    into d_offs[k] (n + 1).  A list keeps the items that fit in the record, in order
+ *                    (Go's loop stops making progress at the first that does not).  d_fail (n bytes,
+ *                    nullable): the unmarshal position (public fields in order, then private) of
+ *                    the field where decoding stopped, nfields when it did not.
+ *   sym_flat_nested_status  after decoding field `field`'s items with the inner schema (their
+ *                    statuses d_item_status), marks the records that reached the field and have a
+ *                    failed item SYM_STATUS_NESTED (Go returns "failed to unmarshal nested message"
+ *                    there); d_fail is updated, so fields can be folded in in any order.  Field
+ *                    values of a record with a non-OK status are unspecified beyond the fields
+ *                    before the failing one (Go callers discard the struct on error). */
+uint64_t sym_flat_encoded_size_ex(const sym_field* fields, int nfields, uint64_t n, const uint64_t* bytes,
+                                  const uint64_t* items);
+int sym_flat_encode_ex(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const void* const* d_cols,
+                       const uint64_t* const* d_offs, const uint64_t* const* d_items, uint32_t service_id,
+                       uint32_t method_id, uint8_t* d_out, uint64_t* d_out_off, void* stream);
+int sym_flat_decode_ex(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const uint8_t* d_in,
+                       const uint64_t* d_rec_off, void* const* d_cols, const uint64_t* caps, uint64_t* const* d_offs,
+                       uint64_t* const* d_items, const uint64_t* item_caps, uint8_t* d_status, uint8_t* d_fail,
+                       void* stream);
+int sym_flat_nested_status(sym_ctx* ctx, const sym_field* fields, int nfields, int field, uint64_t n,
+                           const uint64_t* d_rec_items, const uint8_t* d_item_status, uint8_t* d_status,
+                           uint8_t* d_fail, void* stream);
 
 /* ---- Batched Raw setters ----------------------------------------------------
  * XxxRaw.SetF(v_i) on buffer i of a flat schema (generator main.go:1038-1093 assertions,
