@@ -409,6 +409,53 @@ def flat_leg(codec: Codec, dev, reps: int) -> dict:
                     "columns (caching allocator)"}
 
 
+def boutique_leg(codec: Codec, dev, reps: int, n: int = 1 << 18) -> dict:
+    """SURVEY.md 8f N5 (nested / repeated): online-boutique PlaceOrderResponse messages
+    (onlineboutique.proto: OrderResult{ids, Money, Address, 1..5 OrderItem{CartItem, Money}}),
+    synthetic (datagen.ob_place_order), the whole message tree encoded and decoded by
+    arpc_amd.flat (one launch set per message level; the host reads the item totals between
+    levels).  Host clock around each full call.  The reference README's numbers are Go, one message
+    per call, on its 99,848-message trace (Xeon 6142): Symphony Write 2079 ns/op, Read 2939 ns/op."""
+    import time
+
+    from arpc_amd import datagen, flat
+    sch = flat.OB_PLACE_ORDER_RESPONSE
+    tree = datagen.ob_place_order(n)
+    cols = flat.columns_from_tree(sch, tree[1], dev)
+    data, off = flat.encode(codec, sch, cols)
+    dcols, st = flat.decode(codec, sch, data, off)
+    data2, off2 = flat.encode(codec, sch, dcols)
+    torch.cuda.synchronize()
+    codec.check()
+    ok = bool(torch.equal(data, data2)) and bool(torch.equal(off, off2)) and bool((st == 0).all().item())
+    inner = int(tree[1][0][1][4][2][-1])  # OrderItems
+
+    def timed(fn) -> float:
+        ts = []
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        codec.check()
+        return float(np.median(ts)) * 1e3
+
+    enc_ms = timed(lambda: flat.encode(codec, sch, cols))
+    dec_ms = timed(lambda: flat.decode(codec, sch, data, off))
+    sb = int(off[-1].item())
+    msgs = 4 * n + 3 * inner  # PlaceOrderResponse, OrderResult, Money, Address; per item OrderItem, CartItem, Money
+    return {"schema": sch.name, "records": n, "order_items": inner, "messages_per_batch": msgs, "stream_bytes": sb,
+            "round_trip_ok": ok, "encode_ms": round(enc_ms, 3), "decode_ms": round(dec_ms, 3),
+            "encode_records_per_s": round(n / (enc_ms * 1e-3)), "decode_records_per_s": round(n / (dec_ms * 1e-3)),
+            "encode_ns_per_record": round(enc_ms * 1e6 / n, 2), "decode_ns_per_record": round(dec_ms * 1e6 / n, 2),
+            "stream_gbps_encode": round(sb / (enc_ms * 1e-3) / 1e9, 1),
+            "stream_gbps_decode": round(sb / (dec_ms * 1e-3) / 1e9, 1),
+            "reference_readme_ns_per_op": {"write": 2079, "read": 2939},
+            "note": "host clock around the whole tree call (several launches per level plus the host "
+                    "reads of item totals); synthetic payloads, not the reference's trace"}
+
+
 def host_inclusive(codec: Codec, kw: dict, dev, steps: int) -> dict:
     """Host memory in, host memory out, through the C ABI's host entry points (what a cgo Serializer
     adapter calls): sym_encode_host then sym_decode_host on the same workload, each call chunked over
@@ -624,6 +671,7 @@ def main():
     ap.add_argument("--reassembly-reps", type=int, default=5, help="reassembly leg repetitions (0 = skip)")
     ap.add_argument("--crypto-reps", type=int, default=3, help="segment cipher leg repetitions (0 = skip)")
     ap.add_argument("--flat-reps", type=int, default=5, help="flat-schema codec leg repetitions (0 = skip)")
+    ap.add_argument("--boutique-reps", type=int, default=3, help="online-boutique nested leg repetitions (0 = skip)")
     ap.add_argument("--mixed-reps", type=int, default=10, help="mixed Get/Set leg repetitions (0 = skip)")
     ap.add_argument("--config3-reps", type=int, default=6, help="config 3 leg repetitions (0 = skip)")
     ap.add_argument("--ref-reps", type=int, default=-1,
@@ -827,6 +875,8 @@ def main():
         line["proxy"] = proxy_leg(codec, dev, args.proxy_reps)
     if world == 1 and args.flat_reps > 0:
         line["flat"] = flat_leg(codec, dev, args.flat_reps)
+    if world == 1 and args.boutique_reps > 0:
+        line["boutique"] = boutique_leg(codec, dev, args.boutique_reps)
     if world == 1 and args.cpu_seconds > 0:
         line["cpu_baseline"] = cpu_baseline(kw, args.cpu_seconds)
     print(json.dumps(line), flush=True)
