@@ -82,6 +82,7 @@ struct Args {
     SeqState* state;
     uint8_t* status;
     Pair* cnt;             // per arrival (n+1): (message bytes, segments << 32 | messages)
+    Pair* agg;             // its tile totals (simple batches: written by parse_kernel)
     const Pair* pre;       // its exclusive scan
     u64* msg_off;
     u64* msg_rpc;
@@ -90,50 +91,133 @@ struct Args {
     u64* seg_len;
 };
 
-// ---- 1. parse + group key (transport.go:266-283, builtin_packets.go:118-161)
-__global__ __launch_bounds__(256) void parse_kernel(Args a) {
+__device__ inline void block_scan_pair(Pair v, Pair& excl, Pair& tile_total);
+
+// ---- 1. parse (transport.go:266-283, builtin_packets.go:118-161): status, RPCID, meta, payload
+// length, and whether the batch is "simple" -- every DataPacket a whole message in one datagram
+// (TotalPackets 1, sequence 0, fragment 0, last).  Then each DataPacket completes its own message on
+// arrival whatever else the batch holds (no RPCID ever keeps state), so the messages are the
+// DataPackets in arrival order: cnt[i] = (payload bytes, one segment, one message) is already the
+// per-arrival triple the general path computes.
+__global__ __launch_bounds__(256) void parse_kernel(Args a, unsigned* complex_flag) {
     const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
-    if (i > a.n) return;
-    a.cnt[i] = Pair{0, 0};
-    if (i == a.n) return;
-    const u64 s = a.dg_off[i], L = a.dg_off[i + 1] - s;
-    const uintptr_t p = (uintptr_t)(a.wire + s);
-    uint8_t st = SYM_RX_PENDING;
-    u32 g = kNoSlot;  // table slot
-    if (L < 1) {
-        st = SYM_RX_TOO_SHORT;                       // "data too short to read packet type"
-    } else if (const u32 t = ld_u8(p); t != 1 && t != 2) {
-        st = SYM_RX_NOT_DATA;                        // Error packet, or no codec for the type
-    } else if (L < kHdr) {
-        st = SYM_RX_TOO_SHORT;                       // "data too short for DataPacket header"
-    } else {
-        const u32 pl = ld_u32(p + 27);
-        if (L < (u64)kHdr + pl) {
-            st = SYM_RX_BAD_LENGTH;                  // "too short for declared payload length"
-        } else {
-            const u64 r = (u64)ld_u32(p + 1) | ((u64)ld_u32(p + 5) << 32);
-            a.rpc[i] = r;
-            a.meta[i] = (u64)(ld_u32(p + 11) & 0xffff) | ((u64)(ld_u32(p + 9) & 0xffff) << 16) |
-                        ((u64)(ld_u8(p + 13) != 0) << 32) | ((u64)ld_u8(p + 14) << 40);
-            a.plen[i] = pl;
-            if (r == kEmpty) {
-                g = a.special;
-            } else {  // open addressing; the table has >= 2n slots, so a free slot is always found
-                u64 h = mix64(r) & a.tmask;
-                for (;;) {
-                    const u64 prev = atomicCAS((unsigned long long*)&a.table[h], (unsigned long long)kEmpty,
-                                               (unsigned long long)r);
-                    if (prev == kEmpty || prev == r) break;
-                    h = (h + 1) & a.tmask;
-                }
-                g = (u32)h;
+    Pair c = {0, 0};  // entries past the datagrams (entry n included) are zero
+    bool simple = true;
+    if (i < a.n) {
+        const u64 s = a.dg_off[i], L = a.dg_off[i + 1] - s;
+        const uintptr_t p = (uintptr_t)(a.wire + s);
+        uint8_t st = SYM_RX_PENDING;
+        u32 pl = 0;
+        if (L >= kHdr && s + 32 <= a.dg_off[a.n]) {
+            // the whole header in two byte-unaligned 16-byte loads, issued together (the common case)
+            const u32x4 w0 = ld16u(p), w1 = ld16u(p + 16);
+            const u32 w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+            auto u32_at = [&](int q) {  // q is a constant: the shifts fold
+                return q % 4 == 0 ? w[q / 4] : (w[q / 4] >> (8 * (q % 4))) | (w[q / 4 + 1] << (32 - 8 * (q % 4)));
+            };
+            const u32 t = w[0] & 0xff;
+            pl = u32_at(27);
+            if (t != 1 && t != 2) {
+                st = SYM_RX_NOT_DATA;                    // Error packet, or no codec for the type
+            } else if (L < (u64)kHdr + pl) {
+                st = SYM_RX_BAD_LENGTH;                  // "too short for declared payload length"
+            } else {
+                const u64 r = (u64)u32_at(1) | ((u64)u32_at(5) << 32);
+                const u64 m = (u64)(u32_at(11) & 0xffff) | ((u64)(u32_at(9) & 0xffff) << 16) |
+                              ((u64)(((w[3] >> 8) & 0xff) != 0) << 32) | ((u64)((w[3] >> 16) & 0xff) << 40);
+                a.rpc[i] = r;
+                a.meta[i] = m;
+                a.plen[i] = pl;
+                simple = m_total(m) == 1 && m_seq(m) == 0 && m_fidx(m) == 0 && !m_more(m);
+            }
+        } else if (L < 1) {
+            st = SYM_RX_TOO_SHORT;                       // "data too short to read packet type"
+        } else if (const u32 t = ld_u8(p); t != 1 && t != 2) {
+            st = SYM_RX_NOT_DATA;
+        } else if (L < kHdr) {
+            st = SYM_RX_TOO_SHORT;                       // "data too short for DataPacket header"
+        } else {  // a header within 32 bytes of the batch end: byte loads
+            pl = ld_u32(p + 27);
+            if (L < (u64)kHdr + pl) {
+                st = SYM_RX_BAD_LENGTH;
+            } else {
+                const u64 r = (u64)ld_u32(p + 1) | ((u64)ld_u32(p + 5) << 32);
+                const u64 m = (u64)(ld_u32(p + 11) & 0xffff) | ((u64)(ld_u32(p + 9) & 0xffff) << 16) |
+                              ((u64)(ld_u8(p + 13) != 0) << 32) | ((u64)ld_u8(p + 14) << 40);
+                a.rpc[i] = r;
+                a.meta[i] = m;
+                a.plen[i] = pl;
+                simple = m_total(m) == 1 && m_seq(m) == 0 && m_fidx(m) == 0 && !m_more(m);
             }
         }
+        a.status[i] = st;
+        if (st == SYM_RX_PENDING) c = Pair{pl, ((u64)1 << 32) | 1u};
     }
-    a.status[i] = st;
+    if (i <= a.n) a.cnt[i] = c;
+    if (__ballot(!simple) && (threadIdx.x & 63) == 0) atomicOr(complex_flag, 1u);
+    Pair e, t;  // this tile's totals, for the scan of the triples (simple batches)
+    block_scan_pair(c, e, t);
+    if (threadIdx.x == 0) a.agg[blockIdx.x] = t;
+}
+
+// ---- 1a. general path: the RPCID into an open-addressing hash table (agent-scope CAS) that
+// also keeps each RPCID's first arrival (atomicMin); that first arrival index is the group key,
+// so groups sort in order of first appearance and an in-order stream keeps its arrival order
+// through every later pass (coalesced).  The per-arrival triples are recomputed by group pass 0.
+__global__ __launch_bounds__(256) void hash_kernel(Args a) {
+    const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.n) return;
+    a.cnt[i] = Pair{0, 0};
+    u32 g = kNoSlot;  // table slot
+    if (a.status[i] == SYM_RX_PENDING) {
+        const u64 r = a.rpc[i];
+        if (r == kEmpty) {
+            g = a.special;
+        } else {  // open addressing; the table has >= 2n slots, so a free slot is always found
+            u64 h = mix64(r) & a.tmask;
+            for (;;) {
+                const u64 prev = atomicCAS((unsigned long long*)&a.table[h], (unsigned long long)kEmpty,
+                                           (unsigned long long)r);
+                if (prev == kEmpty || prev == r) break;
+                h = (h + 1) & a.tmask;
+            }
+            g = (u32)h;
+        }
+    }
     a.slot[i] = g;
     if (g != kNoSlot) atomicMin(&a.first[g], (u32)i);
     a.idx[i] = (u32)i;
+}
+
+// ---- simple batches: each DataPacket is message number (its rank among the DataPackets).  The
+// kernel is queued before the host knows the batch kind and does nothing for other batches
+// (except zeroing the segment count, so the speculative gather after it is empty too).
+__global__ __launch_bounds__(256) void emit_simple_kernel(Args a, const Pair* tpre, const unsigned* complex_flag,
+                                                          u64* nmsg, u64* nseg) {
+    const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
+    if (*complex_flag) {
+        if (i == 0) *nseg = 0;
+        return;
+    }
+    const bool data = i < a.n && a.status[i] == SYM_RX_PENDING;
+    const u32 pl = data ? a.plen[i] : 0u;
+    Pair e, t;
+    block_scan_pair(data ? Pair{pl, ((u64)1 << 32) | 1u} : Pair{0, 0}, e, t);
+    const Pair b = tpre[blockIdx.x];
+    const u64 bytes = b.bytes + e.bytes, mi = (b.count + e.count) & 0xffffffffull;
+    if (data) {
+        a.msg_off[mi] = bytes;
+        a.msg_rpc[mi] = a.rpc[i];
+        a.msg_dg[mi] = i;
+        a.seg_src[mi] = a.dg_off[i] + kHdr;
+        a.seg_len[mi] = pl;
+        a.status[i] = SYM_RX_CONSUMED;
+    }
+    if (i == a.n) {  // entry n: the totals
+        *nmsg = mi;
+        a.msg_off[mi] = bytes;
+        *nseg = mi;
+    }
 }
 
 // ---- 1b. group key = the RPCID's first arrival: groups sort in order of first appearance, so an
@@ -311,7 +395,7 @@ inline unsigned key_bits(u64 n) { return log2u(n + 1) + 1; }  // keys in [0, n]
 
 struct Layout {
     size_t table, first, slot, rpc, meta, plen, gid, idx, gs, is, state, cnt, pre, agg, tpre, seg_src, seg_len, agg2,
-        pre2, nseg, temp, total;
+        pre2, nseg, flag, temp, total;
     size_t temp_bytes;
 };
 
@@ -344,6 +428,7 @@ inline Layout layout(u64 n) {
     L.agg2 = take((tiles(n) + 1) * sizeof(Pair));
     L.pre2 = take((tiles(n) + 1) * sizeof(Pair));
     L.nseg = take(8);
+    L.flag = take(4);
     size_t tb = 0;
     (void)rocprim::radix_sort_pairs(nullptr, tb, (const u32*)nullptr, (u32*)nullptr, (const u32*)nullptr,
                                     (u32*)nullptr, (size_t)n, 0u, key_bits(n));
@@ -391,55 +476,78 @@ hipError_t launch_reassemble(const uint8_t* wire, const u64* dg_off, u64 n, uint
     a.seg_src = (u64*)(w + L.seg_src);
     a.seg_len = (u64*)(w + L.seg_len);
     const dim3 b256(256);
-    hipError_t e = hipMemsetAsync(a.table, 0xff, TS * 8, stream);
-    if (e == hipSuccess) e = hipMemsetAsync(a.first, 0xff, (TS + 1) * 4, stream);
+    unsigned* flag = (unsigned*)(w + L.flag);
+    const dim3 gq((unsigned)rx::tiles(n));
+    const u64 nt = rx::tiles(n + 1), ns = rx::tiles(n);
+    Pair* agg = (Pair*)(w + L.agg);
+    Pair* tpre = (Pair*)(w + L.tpre);
+    u64* nseg = (u64*)(w + L.nseg);
+    a.agg = agg;
+    auto seg_tail = [&]() -> hipError_t {  // the payload segments' tile prefixes, then the gather
+        Pair* agg2 = (Pair*)(w + L.agg2);
+        Pair* pre2 = (Pair*)(w + L.pre2);
+        hipLaunchKernelGGL(rx::seg_tile_total_kernel, dim3((unsigned)ns), b256, 0, stream, (const u64*)a.seg_len,
+                           (const u64*)nseg, agg2);
+        hipError_t r = hipGetLastError();
+        if (r == hipSuccess) r = launch_tile_scan(agg2, pre2, ns, stream);
+        if (r != hipSuccess) return r;
+        raw::GatherArgs ga{};
+        ga.in = wire;
+        ga.n = n;
+        ga.n_ptr = nseg;
+        ga.lo_ptr = dg_off;
+        ga.hi_ptr = dg_off + n;
+        ga.pre = pre2;
+        ga.seg_src = a.seg_src;
+        ga.seg_len = a.seg_len;
+        ga.out = msg;
+        ga.cap = msg_cap;
+        ga.err = err;
+        return launch_segment_gather(ga, stream);
+    };
+    // Simple batches (every DataPacket one whole message) complete on the device without a host
+    // decision: parse (with the tile totals of the per-arrival triples), their scan, the messages,
+    // the gather.  Queued for every batch; for the others the emit writes no message and zero
+    // segments, so the gather after it is empty.
+    hipError_t e = hipMemsetAsync(flag, 0, sizeof(unsigned), stream);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(rx::parse_kernel, dim3((unsigned)rx::tiles(n + 1)), b256, 0, stream, a);
+    hipLaunchKernelGGL(rx::parse_kernel, dim3((unsigned)nt), b256, 0, stream, a, flag);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(rx::key_kernel, dim3((unsigned)rx::tiles(n)), b256, 0, stream, a);
+    if ((e = launch_tile_scan(agg, tpre, nt, stream)) != hipSuccess) return e;
+    hipLaunchKernelGGL(rx::emit_simple_kernel, dim3((unsigned)nt), b256, 0, stream, a, (const Pair*)tpre,
+                       (const unsigned*)flag, nmsg, nseg);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = seg_tail()) != hipSuccess) return e;
+    // the one host read of the call: whether the general path has to run
+    unsigned complex_batch = 1;
+    if ((e = hipMemcpyAsync(&complex_batch, flag, sizeof(unsigned), hipMemcpyDeviceToHost, stream)) != hipSuccess)
+        return e;
+    if ((e = hipStreamSynchronize(stream)) != hipSuccess) return e;
+    if (!complex_batch) return hipSuccess;
+    if ((e = hipMemsetAsync(a.table, 0xff, TS * 8, stream)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(a.first, 0xff, (TS + 1) * 4, stream)) != hipSuccess) return e;
+    hipLaunchKernelGGL(rx::hash_kernel, gq, b256, 0, stream, a);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(rx::key_kernel, gq, b256, 0, stream, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     size_t tb = L.temp_bytes;
     e = rocprim::radix_sort_pairs(w + L.temp, tb, (const u32*)a.gid, (u32*)(w + L.gs), (const u32*)a.idx,
                                   (u32*)(w + L.is), (size_t)n, 0u, rx::key_bits(n), stream);
     if (e != hipSuccess) return e;
-    const dim3 gq((unsigned)rx::tiles(n));
     hipLaunchKernelGGL(rx::group_kernel<0>, gq, b256, 0, stream, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    const u64 nt = rx::tiles(n + 1);
-    Pair* agg = (Pair*)(w + L.agg);
-    Pair* tpre = (Pair*)(w + L.tpre);
     hipLaunchKernelGGL(rx::pair_tile_total_kernel, dim3((unsigned)nt), b256, 0, stream, (const Pair*)a.cnt, n + 1, agg);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = launch_tile_scan(agg, tpre, nt, stream)) != hipSuccess) return e;
     hipLaunchKernelGGL(rx::pair_scan_apply_kernel, dim3((unsigned)nt), b256, 0, stream, (const Pair*)a.cnt, n + 1,
                        (const Pair*)tpre, (Pair*)(w + L.pre));
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    u64* nseg = (u64*)(w + L.nseg);
     hipLaunchKernelGGL(rx::finalize_kernel, dim3(1), dim3(1), 0, stream, (const Pair*)(w + L.pre) + n, msg_off, nmsg,
                        nseg);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(rx::group_kernel<1>, gq, b256, 0, stream, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    const u64 ns = rx::tiles(n);
-    Pair* agg2 = (Pair*)(w + L.agg2);
-    Pair* pre2 = (Pair*)(w + L.pre2);
-    hipLaunchKernelGGL(rx::seg_tile_total_kernel, dim3((unsigned)ns), b256, 0, stream, (const u64*)a.seg_len,
-                       (const u64*)nseg, agg2);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    if ((e = launch_tile_scan(agg2, pre2, ns, stream)) != hipSuccess) return e;
-    raw::GatherArgs ga{};
-    ga.in = wire;
-    ga.n = n;
-    ga.n_ptr = nseg;
-    ga.lo_ptr = dg_off;
-    ga.hi_ptr = dg_off + n;
-    ga.pre = pre2;
-    ga.seg_src = a.seg_src;
-    ga.seg_len = a.seg_len;
-    ga.out = msg;
-    ga.cap = msg_cap;
-    ga.err = err;
-    return launch_segment_gather(ga, stream);
+    return seg_tail();
 }
 
 }  // namespace symhip
