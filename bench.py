@@ -651,7 +651,8 @@ def config3_leg(codec: Codec, dev, reps: int) -> dict:
             "encode_ms": round(enc_ms, 4), "encode_gbps": round(enc_b / enc_ms / 1e6, 1),
             "decode_ms": round(dec_ms, 4), "decode_gbps": round(dec_b / dec_ms / 1e6, 1),
             "gbps_algorithmic": round((enc_b + dec_b) / (enc_ms + dec_ms) / 1e6, 1),
-            "kernels": {"encode": "encode_kernel<0, 2, 0, false>", "decode": "decode_pipe_kernel<0, 2, false, 0, 0, 2, 2>"},
+            "kernels": {"encode": "encode_kernel<0, 2, 1, false, 4, false>",
+                        "decode": "decode_pipe_kernel<0, 2, false, 0, 0, 2, 2, 22528, false, 0, false>"},
             "note": "config 3 (seed 0x5EED0002), the headline's algorithmic byte definition"}
 
 
@@ -818,9 +819,10 @@ def main():
         glob = {"rank0_base": base, "global_stream_bytes": gtotal, "global_records": n * world}
     # roofline: the dominant single kernel by time (the default decode is one launch)
     if enc_ms >= dec_ms:
-        kname, dom_ms, dom_bytes = f"encode_kernel<{s.nfixed}, {s.nvar}, 0, false>", enc_ms, enc_b
+        kname, dom_ms, dom_bytes = f"encode_kernel<{s.nfixed}, {s.nvar}, 1, false, 4, false>", enc_ms, enc_b
     else:
-        kname, dom_ms, dom_bytes = f"decode_pipe_kernel<{s.nfixed}, {s.nvar}, false, 0, 0, 2, 2>", dec_ms, dec_b
+        kname, dom_ms, dom_bytes = (f"decode_pipe_kernel<{s.nfixed}, {s.nvar}, false, 0, 0, 2, 2, 22528, false, 0, false>",
+                                     dec_ms, dec_b)
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     traffic = load_traffic(kname)
 
@@ -852,7 +854,8 @@ def main():
                                "gbps": round(enc_b / enc_ms / 1e6, 1)},
                     "decode": {"avg_ms": round(dec_ms, 4), "alg_bytes": dec_b,
                                "gbps": round(dec_b / dec_ms / 1e6, 1),
-                               "kernel": f"decode_pipe_kernel<{s.nfixed}, {s.nvar}, false, 0, 0, 2, 2>", **refs}},
+                               "kernel": f"decode_pipe_kernel<{s.nfixed}, {s.nvar}, false, 0, 0, 2, 2, 22528, false, 0, false>",
+                               **refs}},
         "per_gpu_gbps": round((enc_b + dec_b) * args.steps / elapsed / 1e9, 2),
         "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic},
