@@ -149,3 +149,84 @@ def test_encode_host_small_batch(codec):
     assert off.tolist() == [0, 23, 46, 69]
     want, _ = oracle.encode_batch([], [(kb, ko)], 1, 1)
     np.testing.assert_array_equal(out[:69], want)
+
+
+def _pinned(L, ctx, nbytes, dtype, keep):
+    """A numpy view of sym_host_alloc memory (freed by the caller via `keep`)."""
+    import ctypes
+    p = ctypes.c_void_p()
+    assert L.sym_host_alloc(ctx, max(1, nbytes), ctypes.byref(p)) == 0, _native.last_error()
+    keep.append(p.value)
+    buf = (ctypes.c_uint8 * max(1, nbytes)).from_address(p.value)
+    return np.frombuffer(buf, np.uint8)[:nbytes].view(dtype)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("memory", ["pageable", "pinned"])
+@pytest.mark.parametrize("schema,lens", [("kv_set_request", (64, ("loguniform", 1, 4096))),
+                                         ("echo_request", (("uniform", 0, 300), ("uniform", 0, 600)))])
+def test_host_entry_points_many_chunks(codec, memory, schema, lens):
+    """sym_encode_host / sym_decode_host over a batch of ~5 chunks (kChunkBytes = 8 MiB): outputs of
+    every chunk land in place, bit-exact against the oracle; a corrupted record's status and the
+    record after it come back exactly as the oracle decodes them."""
+    L, ctx = codec._lib, codec._ctx
+    sid = datagen.schemas.BY_NAME[schema].schema_id
+    n = 64000 if schema == "kv_set_request" else 110000
+    b = datagen.make_batch(schema, n, lens, seed=0x5EEDC0DE)
+    want, want_off = oracle.encode_batch(b.fixed, b.var, 3, 4)
+    assert int(want_off[-1]) > 4 * (8 << 20)
+    keep = []
+    try:
+        if memory == "pinned":
+            def mk(a):
+                v = _pinned(L, ctx, a.nbytes, a.dtype, keep)
+                v[:] = a
+                return v
+            fixed = [mk(f) for f in b.fixed]
+            var = [(mk(x), mk(o)) for x, o in b.var]
+            out = _pinned(L, ctx, int(want_off[-1]), np.uint8, keep)
+            off = _pinned(L, ctx, 8 * (n + 1), np.uint64, keep)
+        else:
+            fixed, var = b.fixed, b.var
+            out = np.zeros(int(want_off[-1]), np.uint8)
+            off = np.zeros(n + 1, np.uint64)
+        rc = L.sym_encode_host(ctx, sid, n, _native.ptr_array([f.ctypes.data for f in fixed]) if fixed else None,
+                               _native.ptr_array([x.ctypes.data for x, _ in var]),
+                               _native.ptr_array([o.ctypes.data for _, o in var]), 3, 4, out.ctypes.data,
+                               off.ctypes.data)
+        assert rc == 0, _native.last_error()
+        np.testing.assert_array_equal(off, want_off)
+        np.testing.assert_array_equal(out, want)
+
+        # decode the stream with two records damaged in different chunks
+        data = np.array(want)
+        for r in (n // 3, (3 * n) // 4):
+            data[int(want_off[r])] = 2  # version byte
+        wf, wv, wst = oracle.decode_batch(b.schema.nfixed, b.schema.nvar, data, want_off)
+        if memory == "pinned":
+            d_in = _pinned(L, ctx, data.nbytes, np.uint8, keep)
+            d_in[:] = data
+            roff = _pinned(L, ctx, want_off.nbytes, np.uint64, keep)
+            roff[:] = want_off
+        else:
+            d_in, roff = data, want_off
+        caps = np.array([int(o[-1]) for _, o in wv], np.uint64)
+        dfix = [np.zeros(n, np.int32) for _ in range(b.schema.nfixed)]
+        dbytes = [np.zeros(max(1, int(c)), np.uint8) for c in caps]
+        doffs = [np.zeros(n + 1, np.uint64) for _ in range(b.schema.nvar)]
+        st = np.zeros(n, np.uint8)
+        rc = L.sym_decode_host(ctx, sid, n, d_in.ctypes.data, roff.ctypes.data,
+                               _native.ptr_array([f.ctypes.data for f in dfix]) if dfix else None,
+                               _native.ptr_array([x.ctypes.data for x in dbytes]), caps.ctypes.data,
+                               _native.ptr_array([o.ctypes.data for o in doffs]), st.ctypes.data)
+        assert rc == 0, _native.last_error()
+        np.testing.assert_array_equal(st, wst)
+        assert (st != 0).sum() == 2
+        for f in range(b.schema.nfixed):
+            np.testing.assert_array_equal(dfix[f], wf[f])
+        for f in range(b.schema.nvar):
+            np.testing.assert_array_equal(doffs[f], wv[f][1])
+            np.testing.assert_array_equal(dbytes[f][:int(caps[f])], wv[f][0])
+    finally:
+        for p in keep:
+            L.sym_host_free(ctx, p)

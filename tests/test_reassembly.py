@@ -225,3 +225,32 @@ def test_reassembly_round_trip_gpu(gcodec, gdev, cfg, mtu):
     perm = np.random.default_rng(7).permutation(len(dg_off) - 1)
     want = _gpu_vs_oracle(gcodec, gdev, *shuffled(wire, dg_off, perm))
     assert len(want[2]) == 20000 and (want[4] == C).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 63, 64, 257, 5000])
+def test_reassembly_simple_batch_gpu(gcodec, gdev, n):
+    """Batches of complete single-datagram messages take the device fast path (no grouping): parse
+    errors and reused RPC IDs in between, with every misalignment of the wire buffer."""
+    rng = np.random.default_rng(100 + n)
+    bad = [b"", b"\x03" * 40, b"\x01" * 12, dgram(1, 1, 0, b"x", plen=77), dgram(2, 1, 0, b"e", ptype=3)]
+    dgs = []
+    for k in range(n):
+        if rng.random() < 0.1:
+            dgs.append(bad[int(rng.integers(0, len(bad)))])
+        else:
+            dgs.append(dgram(int(rng.integers(0, 50)), 1, 0, bytes(rng.integers(0, 256, int(rng.integers(0, 90)),
+                                                                               dtype=np.uint8))))
+    want = _gpu_vs_oracle(gcodec, gdev, *batch(dgs), misalign=n % 7)
+    assert len(want[2]) == sum(1 for s in want[4] if s == C)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("where", ["first", "middle", "last"])
+def test_reassembly_one_fragment_makes_batch_general_gpu(gcodec, gdev, where):
+    """One two-fragment message among single-datagram ones sends the batch down the general path."""
+    singles = [dgram(k, 1, 0, bytes([k & 255]) * (k % 40)) for k in range(300)]
+    pos = {"first": 0, "middle": 150, "last": 300}[where]
+    dgs = singles[:pos] + [dgram(999, 2, 1, b"tail"), dgram(999, 2, 0, b"head")] + singles[pos:]
+    want = _gpu_vs_oracle(gcodec, gdev, *batch(dgs))
+    assert len(want[2]) == 301
