@@ -659,8 +659,12 @@ def config3_leg(codec: Codec, dev, reps: int) -> dict:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--prewarm-ms", type=float, default=200.0,
+                    help="untimed steps for this much wall time before the warmup steps (GPU clock ramp)")
+    ap.add_argument("--kernel-events", type=int, default=1,
+                    help="0: no per-kernel HIP events inside the timed region (experiment)")
     ap.add_argument("--overlap", type=int, default=0,
                     help="1: encode and decode of a step on two HIP streams (independent buffer sets), overlapped")
     ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4))
@@ -741,20 +745,27 @@ def main():
             ev["enc"].append((e0, e1))
             ev["dec"].append((e2, e3))
 
+    last_ev = [None]  # a step's closing event opens the next step's encode (2 markers per step, not 3)
+
     def step(i: int, timed: bool):
         if args.overlap:
             return step_overlap(i, timed)
+        timed = timed and args.kernel_events
         a, d = i % NSETS, (i + 2) % NSETS
         fx, vr = sets[a]
         if timed:
-            e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
-            e0.record()
+            e0 = last_ev[0]
+            if e0 is None:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e0.record()
+            e1, e2 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         codec.encode(s, fx, vr, out=enc[a][0], out_off=enc[a][1])
         if timed:
             e1.record()
         codec.decode(s, enc[d][0], enc[d][1], outputs=dec[d])
         if timed:
             e2.record()
+            last_ev[0] = e2
             ev["enc"].append((e0, e1))
             ev["dec"].append((e1, e2))
 
@@ -762,8 +773,17 @@ def main():
         fx, vr = sets[k]
         codec.encode(s, fx, vr, out=enc[k][0], out_off=enc[k][1])
     torch.cuda.synchronize()
+    # Leave the idle power state first: untimed steps for --prewarm-ms of wall time (a GPU that has
+    # just been idle runs the first milliseconds of work at lower clocks), then the W warmup steps.
+    t_pw = time.perf_counter()
+    k_pw = 0
+    while (time.perf_counter() - t_pw) * 1e3 < args.prewarm_ms:
+        step(k_pw, False)
+        k_pw += 1
+        if k_pw % 8 == 0:
+            torch.cuda.synchronize()
     for i in range(args.warmup):
-        step(i, False)
+        step(k_pw + i, False)
     codec.check()
 
     barrier(world)
