@@ -81,6 +81,9 @@ struct alignas(16) Lds {
     int first[4];            // scanner: per-wave first unpublished tile
 };
 
+__device__ __forceinline__ u64 lane_u64_pub(u64 v, int l) {
+    return (u64)__builtin_amdgcn_readlane((u32)v, l) | ((u64)__builtin_amdgcn_readlane((u32)(v >> 32), l) << 32);
+}
 __device__ __forceinline__ bool tagged(u64 w, u32 epoch) { return (u32)(w >> kEpochShift) == epoch; }
 __device__ __forceinline__ u64 make_word(u32 epoch, u64 st, u64 v) {
     return ((u64)epoch << kEpochShift) | st | (v & kValMask);
@@ -231,11 +234,12 @@ __device__ void parser(const DecodeParams& p, u64* aw, u64* pw, u64 ntiles, u32 
 // Each step loads the aggregate words of the next 1024 tiles, finds the first tile whose word is not
 // yet published (the frontier), and publishes the exclusive prefix of every tile before it.  A
 // tile's prefix so depends only on earlier tiles, whoever published their aggregates.
-template <int NV, int SK, typename LdsT>
-__device__ void scanner(u64* aw, u64* pw, u64 ntiles, u32 epoch, LdsT& S) {
+template <int NV, int SK, int NT = kThreads, typename LdsT>
+__device__ void scanner(u64* aw, u64* pw, u64 ntiles, u32 epoch, LdsT& S, u64* dbg = nullptr) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     constexpr int kPer = SK;  // tiles per thread per step
-    constexpr u64 kStep = (u64)kThreads * kPer;
+    constexpr int kW = NT / 64;  // waves
+    constexpr u64 kStep = (u64)NT * kPer;
     u64 carry[NV];
 #pragma unroll
     for (int f = 0; f < NV; ++f) carry[f] = 0;
@@ -260,7 +264,9 @@ __device__ void scanner(u64* aw, u64* pw, u64 ntiles, u32 epoch, LdsT& S) {
         for (int d = 32; d > 0; d >>= 1) miss = min(miss, (u32)__shfl_xor((int)miss, d, 64));
         if (lane == 0) S.first[wave] = (int)miss;
         lds_barrier();
-        u32 m = (u32)min(min(S.first[0], S.first[1]), min(S.first[2], S.first[3]));
+        u32 m = (u32)S.first[0];
+#pragma unroll
+        for (int q = 1; q < kW; ++q) m = min(m, (u32)S.first[q]);
         lds_barrier();  // S.first is rewritten by the next step
         m = (u32)min((u64)m, ntiles - base);
         if (m == 0) {  // the frontier has not moved: wait a little (bounded)
@@ -284,7 +290,7 @@ __device__ void scanner(u64* aw, u64* pw, u64 ntiles, u32 epoch, LdsT& S) {
             lds_barrier();
             u64 wpre = 0, tot = 0;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
+            for (int q = 0; q < kW; ++q) {
                 const u64 t = S.red[q];
                 if (q < wave) wpre += t;
                 tot += t;
@@ -293,7 +299,10 @@ __device__ void scanner(u64* aw, u64* pw, u64 ntiles, u32 epoch, LdsT& S) {
             u64 run = carry[f] + wpre + inc - sum;
 #pragma unroll
             for (int k = 0; k < kPer; ++k) {
-                if ((u32)(tid * kPer + k) < m) store_word(&pw[(size_t)f * ntiles + t0 + k], make_word(epoch, kStPre, run));
+                if ((u32)(tid * kPer + k) < m) {
+                    store_word(&pw[(size_t)f * ntiles + t0 + k], make_word(epoch, kStPre, run));
+                    if (dbg && f == 0) dbg[(t0 + k) * 8 + 5] = now_ticks();  // tuning timelines only
+                }
                 run += x[k];
             }
             carry[f] += tot;
@@ -714,6 +723,12 @@ hipError_t launch_layout(const DecodeParams& p, u64* flags, u32 epoch, hipStream
     return hipErrorInvalidValue;
 }
 
+#ifdef SYMHIP_TUNING
+// The persistent "ring" decode (tuning variants 500-512): an experiment measured against the pipeline
+// above (decode section).
+#include "decode_ring.inc"
+#endif
+
 }  // namespace pipe
 
 size_t decode_pipe_flag_bytes(int nvar, uint64_t n) {
@@ -766,6 +781,14 @@ hipError_t launch_decode_pipe(const DecodeParams& p, void* flags, unsigned epoch
         case 490: return pipe::launch_layout<0, 0, 2, 2, pipe::kStage, false, 1024, true>(p, fl, epoch, stream);
         case 491: return pipe::launch_layout<0, 0, 2, 2, pipe::kStage, false, 2048, true>(p, fl, epoch, stream);
         case 492: return pipe::launch_layout<2, 0, 2, 2, pipe::kStage, false, 0, true>(p, fl, epoch, stream);
+        // the ring decode: lead 3 / 4, barrier / one-wave scanner; 51x: with timestamps
+        case 500: return pipe::launch_ring_layout<0, 3, 0>(p, fl, epoch, stream);
+        case 501: return pipe::launch_ring_layout<0, 3, 1>(p, fl, epoch, stream);
+        case 502: return pipe::launch_ring_layout<0, 4, 0>(p, fl, epoch, stream);
+        case 503: return pipe::launch_ring_layout<0, 4, 1>(p, fl, epoch, stream);
+        case 504: return pipe::launch_ring_layout<0, 3, 2>(p, fl, epoch, stream);  // no scan (WRONG output)
+        case 510: return pipe::launch_ring_layout<1, 3, 0>(p, fl, epoch, stream);
+        case 512: return pipe::launch_ring_layout<1, 4, 0>(p, fl, epoch, stream);
         default: break;
     }
 #endif

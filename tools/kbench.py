@@ -23,6 +23,10 @@ from arpc_amd.codec import Codec, DecodedBatch, to_device  # noqa: E402
 from bench import alg_bytes  # noqa: E402
 
 
+# timing-only decode variants that give wrong output by design (no digest check)
+WRONG_OUTPUT = {402, 412, 475, 476, 482, 483, 492, 504}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", type=int, default=2)
@@ -57,10 +61,18 @@ def main():
 
     variants = [("enc", int(v)) for v in a.enc.split(",") if v] + [("dec", int(v)) for v in a.dec.split(",") if v]
     times = {v: [] for v in variants}
+    dref = {}  # decode digest per buffer set (the first decode variant is the reference)
+
+    def ddigest():
+        return tuple(int(t.to(torch.int64).sum().item()) for t in
+                     [x for col, off in dec.var for x in (col, off)] + [dec.status])
     for rnd in range(a.rounds + 1):
         for kind, v in variants:
             os.environ["SYMHIP_ENCODE_VARIANT" if kind == "enc" else "SYMHIP_DECODE_VARIANT"] = str(v)
             for k in range(4):
+                if kind == "dec" and rnd <= 1:
+                    for col, _ in dec.var:
+                        col.fill_(0xA5)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 if kind == "enc":
@@ -69,6 +81,10 @@ def main():
                     codec.decode(s, enc[(k + 2) % 4][0], enc[(k + 2) % 4][1], outputs=dec)
                 e1.record()
                 e1.synchronize()
+                if kind == "dec" and rnd <= 1 and v not in WRONG_OUTPUT:
+                    codec.check()
+                    dg = ddigest()
+                    assert dref.setdefault(k, dg) == dg, f"decode variant {v} output differs on set {k}"
                 if rnd:
                     times[(kind, v)].append(e0.elapsed_time(e1))
             if kind == "enc":
