@@ -98,6 +98,9 @@ __device__ inline u32x4 wave_xor_u32x4(u32x4 v) {
 }
 
 __device__ inline u32 ld_le32(uintptr_t p) { return ld_u32(p); }
+__device__ __forceinline__ u64 lane_u64c(u64 v, int l) {
+    return (u64)__builtin_amdgcn_readlane((u32)v, l) | ((u64)__builtin_amdgcn_readlane((u32)(v >> 32), l) << 32);
+}
 
 // bytes [0, m) at p (m <= 16) as little-endian words, zero above m; reads only aligned blocks that
 // hold wanted bytes
@@ -119,10 +122,19 @@ __device__ inline void store_bytes(uint8_t* p, u32x4 v, int m) {
 
 __device__ inline u32x4 counter_block(u32x4 nonce_le, u32 ctr) { return u32x4{nonce_le.x, nonce_le.y, nonce_le.z, bswap(ctr)}; }
 
+// Per-record descriptor the plan leaves for the cipher, so that a record's geometry is one 16-byte
+// load instead of a chain of dependent loads (offsets, then the header).
+struct RecDesc {
+    u64 s;  // stream offset
+    u32 L;  // record bytes
+    u32 o;  // offsetToPrivate; kNoWork: nothing to seal/open (bad header); kSlow: L >= 2^32, read it all
+};
+constexpr u32 kNoWork = 0xFFFFFFFFu, kSlow = 0xFFFFFFFEu;
+
 // ---- plan: header checks and output sizes (encryption.go:84-95, 184-202, 313-318)
 template <bool ENC>
 __global__ __launch_bounds__(256) void plan_kernel(const uint8_t* in, const u64* rec_off, u64 n, u64* size,
-                                                   uint8_t* status, Pair* agg) {
+                                                   uint8_t* status, Pair* agg, RecDesc* desc) {
     __shared__ u64 red_b[4];
     const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
     u64 sz = 0;
@@ -144,6 +156,8 @@ __global__ __launch_bounds__(256) void plan_kernel(const uint8_t* in, const u64*
         }
         status[i] = st;
         size[i] = sz;
+        const u64 o = L >= 13 ? ld_u32((uintptr_t)(in + s) + 1) : 0;
+        desc[i] = RecDesc{s, (u32)L, st != SYM_CRYPT_OK ? kNoWork : L >> 32 ? kSlow : (u32)o};
     }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const u64 w = wave_sum_u64(sz);
@@ -175,6 +189,7 @@ struct Args {
     uint8_t* status;
     uint8_t* out;
     const Tables* tables;
+    const RecDesc* desc;
 };
 
 __device__ inline u32x4 to_be(u32x4 v) { return u32x4{bswap(v.x), bswap(v.y), bswap(v.z), bswap(v.w)}; }
@@ -205,22 +220,49 @@ __device__ inline u32x4 ghash_fold(u32x4 y, bool first, bool mine, u32x4 term, u
     return first ? c : (gf_mul(y, T.ghash[key][cnt - 1], T.red) ^ c);
 }
 
-// GHASH slots of record r (data blocks + one length block per segment), 0 when it has no work
-__device__ inline u32 record_slots(const Args& a, u64 r, bool enc) {
-    if (r >= a.n || a.status[r] != SYM_CRYPT_OK) return 0;
-    const u64 s = a.rec_off[r], L = a.rec_off[r + 1] - s;
-    const u64 o = ld_u32((uintptr_t)(a.in + s) + 1);
-    const u64 np = enc ? o - 13 : o - 41, nv = o < L ? (enc ? L - o : L - o - 28) : 0;
-    return (u32)((np + 15) / 16 + 1 + (o < L ? (nv + 15) / 16 + 1 : 0));
+// A record's geometry (the lane's own record, loaded one pair ahead).
+struct Geo {
+    u64 s, L, o, oo;  // stream offset, bytes, offsetToPrivate, output offset
+    bool work;
+};
+__device__ inline Geo load_geo(const Args& a, u64 r) {
+    Geo g{0, 0, 0, 0, false};
+    if (r >= a.n) return g;
+    const RecDesc d = a.desc[r];
+    g.oo = a.out_off[r];
+    g.work = d.o != kNoWork;
+    g.s = d.s;
+    g.L = d.L;
+    g.o = d.o;
+    if (d.o == kSlow) {  // a record of 4 GiB or more: the full-width values
+        g.L = a.rec_off[r + 1] - d.s;
+        g.o = ld_u32((uintptr_t)(a.in + d.s) + 1);
+    }
+    return g;
+}
+
+// GHASH slots of a record (data blocks + one length block per segment), 0 when it has no work
+__device__ inline u32 record_slots(const Geo& g, bool enc) {
+    if (!g.work) return 0;
+    const u64 np = enc ? g.o - 13 : g.o - 41, nv = g.o < g.L ? (enc ? g.L - g.o : g.L - g.o - 28) : 0;
+    return (u32)((np + 15) / 16 + 1 + (g.o < g.L ? (nv + 15) / 16 + 1 : 0));
+}
+__device__ inline Geo lane_geo(const Geo& g, int l) {  // lane l's geometry, wave-uniform
+    Geo u;
+    u.s = lane_u64c(g.s, l);
+    u.L = lane_u64c(g.L, l);
+    u.o = lane_u64c(g.o, l);
+    u.oo = lane_u64c(g.oo, l);
+    u.work = __builtin_amdgcn_readlane((int)g.work, l) != 0;
+    return u;
 }
 
 // One record on a sub-wave of W lanes (sl = lane within it).  W = 32 packs two records per wave.
 template <bool ENC, int W>
-__device__ void seal_or_open(const Args& a, const Tables& T, u64 r, int sl) {
-    const u64 s = a.rec_off[r], L = a.rec_off[r + 1] - s;
-    const uintptr_t d = (uintptr_t)(a.in + s);
-    const u64 o = ld_u32(d + 1);
-    uint8_t* const q = a.out + a.out_off[r];
+__device__ void seal_or_open(const Args& a, const Tables& T, const u32* ts, u64 r, const Geo& G, int sl) {
+    const u64 L = G.L, o = G.o;
+    const uintptr_t d = (uintptr_t)(a.in + G.s);
+    uint8_t* const q = a.out + G.oo;
     const bool priv = o < L;
     // segment geometry: plaintext/ciphertext source, length, destination, nonce
     u64 np, nv;
@@ -265,7 +307,7 @@ __device__ void seal_or_open(const Args& a, const Tables& T, u64 r, int sl) {
         const bool ver = !ENC && is_priv && is_data && i == 0;
         u32x4 ks = {0, 0, 0, 0};
         if (is_len || (ENC && is_data) || ver)  // J0 for the tag, J0 + 1 + i for block i
-            ks = aes_block(T.te0, T.rk[is_priv ? 1 : 0],
+            ks = aes_block(ts, T.rk[is_priv ? 1 : 0],
                            counter_block(is_priv ? nonce_priv : nonce_pub, is_len ? 1u : i + 2));
         u32x4 c = x;
         if (ENC && is_data) {
@@ -327,7 +369,7 @@ __device__ void seal_or_open(const Args& a, const Tables& T, u64 r, int sl) {
         const u64 seg_len = is_priv ? nv : np;
         const int m = (int)min((u64)16, seg_len - 16 * (u64)b);
         const u32x4 x = load_partial((is_priv ? src_priv : src_pub) + 16 * (u64)b, m);
-        const u32x4 ks = aes_block(T.te0, T.rk[is_priv ? 1 : 0], counter_block(is_priv ? nonce_priv : nonce_pub, b + 2));
+        const u32x4 ks = aes_block(ts, T.rk[is_priv ? 1 : 0], counter_block(is_priv ? nonce_priv : nonce_pub, b + 2));
         store_bytes((is_priv ? dst_priv : dst_pub) + 16 * (u64)b, x ^ ks, m);
     }
     if (sl == 0) {
@@ -349,18 +391,26 @@ __global__ __launch_bounds__(kWaves * 64) void cipher_kernel(Args a) {
     }
     __syncthreads();
     const int lane = threadIdx.x & 63;
+    const u32* ts = T.te0;
     const u64 nw = (u64)gridDim.x * kWaves;
     const u64 npairs = (a.n + 1) / 2;
-    for (u64 p = (u64)blockIdx.x * kWaves + (threadIdx.x >> 6); p < npairs; p += nw) {  // wave-uniform
+    // lanes 0..31 hold the pair's first record's geometry, 32..63 the second's; the next pair's is
+    // loaded while this one is sealed
+    u64 p = (u64)blockIdx.x * kWaves + (threadIdx.x >> 6);
+    Geo cur = load_geo(a, 2 * p + (lane >> 5));
+    for (; p < npairs; p += nw) {  // wave-uniform
+        const Geo nxt = load_geo(a, 2 * (p + nw) + (lane >> 5));
         const u64 r0 = 2 * p, r1 = 2 * p + 1;
-        const u32 s0 = record_slots(a, r0, ENC), s1 = record_slots(a, r1, ENC);  // uniform
+        const u32 sl_mine = record_slots(cur, ENC);
+        const u32 s0 = __builtin_amdgcn_readlane(sl_mine, 0), s1 = __builtin_amdgcn_readlane(sl_mine, 32);  // uniform
         if (s0 <= 32 && s1 <= 32) {
             const u64 r = lane < 32 ? r0 : r1;
-            if ((lane < 32 ? s0 : s1) != 0) seal_or_open<ENC, 32>(a, T, r, lane & 31);
+            if (sl_mine != 0) seal_or_open<ENC, 32>(a, T, ts, r, cur, lane & 31);
         } else {
-            if (s0) seal_or_open<ENC, 64>(a, T, r0, lane);
-            if (s1) seal_or_open<ENC, 64>(a, T, r1, lane);
+            if (s0) seal_or_open<ENC, 64>(a, T, ts, r0, lane_geo(cur, 0), lane);
+            if (s1) seal_or_open<ENC, 64>(a, T, ts, r1, lane_geo(cur, 32), lane);
         }
+        cur = nxt;
     }
 }
 
@@ -498,7 +548,10 @@ void crypt_build_tables(const uint8_t pub_key[32], const uint8_t priv_key[32], v
     crypt::build_tables(pub_key, priv_key, *(crypt::Tables*)host_tables);
 }
 
-size_t crypt_ws_bytes(u64 n) { return crypt::al256(n * 8) + 2 * crypt::al256((crypt::tiles(n) + 1) * sizeof(raw::Pair)); }
+size_t crypt_ws_bytes(u64 n) {
+    return crypt::al256(n * 8) + 2 * crypt::al256((crypt::tiles(n) + 1) * sizeof(raw::Pair)) +
+           crypt::al256(n * sizeof(crypt::RecDesc));
+}
 
 hipError_t launch_crypt(bool enc, const uint8_t* in, const u64* rec_off, u64 n, const uint8_t* nonces,
                         const void* d_tables, uint8_t* out, u64* out_off, uint8_t* status, void* ws, int num_cus,
@@ -507,15 +560,16 @@ hipError_t launch_crypt(bool enc, const uint8_t* in, const u64* rec_off, u64 n, 
     u64* size = (u64*)ws;
     Pair* agg = (Pair*)((char*)ws + crypt::al256(n * 8));
     Pair* tpre = (Pair*)((char*)agg + crypt::al256((crypt::tiles(n) + 1) * sizeof(Pair)));
+    crypt::RecDesc* desc = (crypt::RecDesc*)((char*)tpre + crypt::al256((crypt::tiles(n) + 1) * sizeof(Pair)));
     const dim3 g((unsigned)crypt::tiles(n)), b(256);
-    if (enc) hipLaunchKernelGGL(crypt::plan_kernel<true>, g, b, 0, stream, in, rec_off, n, size, status, agg);
-    else hipLaunchKernelGGL(crypt::plan_kernel<false>, g, b, 0, stream, in, rec_off, n, size, status, agg);
+    if (enc) hipLaunchKernelGGL(crypt::plan_kernel<true>, g, b, 0, stream, in, rec_off, n, size, status, agg, desc);
+    else hipLaunchKernelGGL(crypt::plan_kernel<false>, g, b, 0, stream, in, rec_off, n, size, status, agg, desc);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if ((e = launch_tile_scan(agg, tpre, crypt::tiles(n), stream)) != hipSuccess) return e;
     hipLaunchKernelGGL(crypt::apply_kernel, g, b, 0, stream, (const u64*)size, n, (const Pair*)tpre, out_off);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    crypt::Args a{in, rec_off, n, nonces, out_off, status, out, (const crypt::Tables*)d_tables};
+    crypt::Args a{in, rec_off, n, nonces, out_off, status, out, (const crypt::Tables*)d_tables, desc};
     const u64 want = (n + crypt::kWaves - 1) / crypt::kWaves;
     const u64 cap = (u64)num_cus * 4;
     const unsigned grid = (unsigned)(want < cap ? want : cap);
