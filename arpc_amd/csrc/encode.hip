@@ -452,9 +452,8 @@ hipError_t launch_encode(const EncodeParams& p, hipStream_t stream) {
 // Record sizes depend on the type column, so record offsets are a scan.  The size pass reads the
 // type bytes and the value offsets (Σ over Sets of 8 + V; keys contribute 22 + K per record, taken
 // from the key offsets at tile edges) and writes, per 64-record tile, its exclusive size prefix
-// inside its group of kGroupTiles tiles, and per group its total.  The last workgroup to finish
-// (ticket) scans the group totals.  The encode kernel starts tile t at group_pre[t >> kGroupShift] +
-// tile_loc[t].
+// inside its group of kGroupTiles tiles, and per group its total; one workgroup then scans the
+// group totals.  The encode kernel starts tile t at group_pre[t >> kGroupShift] + tile_loc[t].
 constexpr int kGroupTiles = 1 << kGroupShift;   // tiles per size-pass workgroup (1024 records)
 constexpr int kTilesPerWave = kGroupTiles / 4;  // 4
 
@@ -474,10 +473,8 @@ static MixedWs mixed_layout(void* ws, u64 n) {
 }
 size_t encode_mixed_ws_bytes(uint64_t n) { return (size_t)(2 * mixed_ngroups(n) + mixed_ntiles(n)) * 8; }
 
-__global__ __launch_bounds__(256) void mixed_size_kernel(EncodeParams p, MixedWs w, unsigned* ticket) {
+__global__ __launch_bounds__(256) void mixed_size_kernel(EncodeParams p, MixedWs w) {
     __shared__ u64 s_agg[kGroupTiles];
-    __shared__ u64 s_wsum[4];
-    __shared__ int s_last;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const u64 n = p.n, ntiles = mixed_ntiles(n), g = blockIdx.x;
     const u64 t0 = g * kGroupTiles + (u64)wave * kTilesPerWave;  // this wave's first tile
@@ -510,24 +507,23 @@ __global__ __launch_bounds__(256) void mixed_size_kernel(EncodeParams p, MixedWs
         const u64 inc = wave_incl_scan_u64(v, lane);
         const u64 t = g * kGroupTiles + lane;
         if (lane < kGroupTiles && t < ntiles) w.tile_loc[t] = inc - v;
-        if (lane == 63) __hip_atomic_store(&w.group_tot[g], inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 63) w.group_tot[g] = inc;
     }
-    __syncthreads();
-    if (tid == 0) {  // release this group's total, acquire everyone's when last
-        const unsigned tk = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = tk == gridDim.x - 1;
-    }
-    __syncthreads();
-    if (!s_last) return;
-    // last workgroup: exclusive scan of the group totals, 16 per thread per round
-    const u64 ng = gridDim.x;
+}
+
+// One workgroup: exclusive scan of the group totals (16 per thread per round).  A separate launch:
+// the size pass's former "last workgroup scans" ticket made every workgroup do an acq_rel atomic on
+// one word, and those serialised (30 us for 2^20 records).
+__global__ __launch_bounds__(256) void mixed_group_scan_kernel(MixedWs w, u64 ng) {
+    __shared__ u64 s_wsum[4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     u64 carry = 0;
     for (u64 base = 0; base < ng; base += 256 * 16) {
         u64 v[16], sum = 0;
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             const u64 i = base + (u64)tid * 16 + k;
-            v[k] = i < ng ? __hip_atomic_load(&w.group_tot[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+            v[k] = i < ng ? w.group_tot[i] : 0;
             sum += v[k];
         }
         const u64 inc = wave_incl_scan_u64(sum, lane);
@@ -549,15 +545,16 @@ __global__ __launch_bounds__(256) void mixed_size_kernel(EncodeParams p, MixedWs
         }
         carry += tot;
     }
-    if (tid == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next call
 }
 
-// `ticket`: a device word that is zero between calls (the last workgroup resets it).
+// `ticket`: unused (kept for the caller's workspace layout).
 hipError_t launch_encode_mixed(EncodeParams p, void* ws, unsigned* ticket, hipStream_t stream) {
+    (void)ticket;
     if (p.n == 0) return hipMemsetAsync(p.out_off, 0, sizeof(uint64_t), stream);
     if (!p.type || p.lay.nfixed != 0 || p.lay.nvar != 2) return hipErrorInvalidValue;
     const MixedWs w = mixed_layout(ws, p.n);
-    hipLaunchKernelGGL(mixed_size_kernel, dim3((unsigned)mixed_ngroups(p.n)), dim3(256), 0, stream, p, w, ticket);
+    hipLaunchKernelGGL(mixed_size_kernel, dim3((unsigned)mixed_ngroups(p.n)), dim3(256), 0, stream, p, w);
+    hipLaunchKernelGGL(mixed_group_scan_kernel, dim3(1), dim3(256), 0, stream, w, mixed_ngroups(p.n));
     p.group_pre = w.group_pre;
     p.tile_loc = w.tile_loc;
 #ifdef SYMHIP_TUNING
