@@ -250,3 +250,34 @@ def test_gpu_mixed_full_size_trace_ratio(codec, dev):
     want, _ = oracle.encode_kv_mixed(b.type[lo:hi], sub_k, sub_v, 1, 1, 2)
     a, z = int(enc.offsets[lo].item()), int(enc.offsets[hi].item())
     np.testing.assert_array_equal(enc.data[a:z].cpu().numpy(), want)
+
+
+@pytest.mark.gpu
+def test_gpu_mixed_many_groups_offsets(codec, dev):
+    """More than 4096 size-pass groups (1024 records each), so the one-workgroup group scan takes a
+    second round: 4.3M small Get/Set records; offsets equal the cumulative record sizes, and the
+    decode returns every column."""
+    n = 4200 * 1024 + 77
+    g = torch.Generator(device="cpu").manual_seed(11)
+    rtype = (torch.rand(n, generator=g) < datagen.TRACE_SET_FRACTION).to(torch.uint8)
+    klen = torch.randint(0, 9, (n,), generator=g, dtype=torch.int64)
+    vlen = torch.randint(0, 17, (n,), generator=g, dtype=torch.int64) * rtype.to(torch.int64)
+    koff = torch.zeros(n + 1, dtype=torch.int64)
+    koff[1:] = torch.cumsum(klen, 0)
+    voff = torch.zeros(n + 1, dtype=torch.int64)
+    voff[1:] = torch.cumsum(vlen, 0)
+    kb = torch.randint(0, 256, (int(koff[-1]) + 1,), generator=g, dtype=torch.int64).to(torch.uint8)
+    vb = torch.randint(0, 256, (int(voff[-1]) + 1,), generator=g, dtype=torch.int64).to(torch.uint8)
+    t = rtype.to(dev)
+    key = (kb.to(dev), koff.to(dev))
+    val = (vb.to(dev), voff.to(dev))
+    size = 22 + klen + (8 + vlen) * rtype.to(torch.int64)
+    expect = torch.zeros(n + 1, dtype=torch.int64)
+    expect[1:] = torch.cumsum(size, 0)
+    enc = codec.encode_kv_mixed(t, key, val, 1, 1, 2, out_bytes=int(expect[-1]))
+    dec = codec.decode_kv_mixed(enc.data, enc.offsets, t, caps=[kb.numel(), vb.numel()])
+    codec.check()
+    assert torch.equal(enc.offsets.cpu(), expect)
+    assert int(dec.status.sum().item()) == 0
+    assert torch.equal(dec.var[0][1].cpu(), koff) and torch.equal(dec.var[0][0][:int(koff[-1])].cpu(), kb[:int(koff[-1])])
+    assert torch.equal(dec.var[1][1].cpu(), voff) and torch.equal(dec.var[1][0][:int(voff[-1])].cpu(), vb[:int(voff[-1])])
