@@ -431,7 +431,7 @@ int sym_encode_kv_mixed(sym_ctx* ctx, const uint8_t* d_type, const uint8_t* d_ke
         const int rc = ensure_scratch(ctx, symhip::encode_mixed_ws_bytes(n), "mixed encode");
         if (rc != SYM_OK) return rc;
     }
-    hipError_t e = symhip::launch_encode_mixed(p, ctx->frag, ctx->err + 1, (hipStream_t)stream);
+    hipError_t e = symhip::launch_encode_mixed(p, ctx->frag, (hipStream_t)stream);
     return e == hipSuccess ? SYM_OK : hip_fail(e, "mixed encode launch");
 }
 

@@ -197,7 +197,7 @@ hipError_t launch_firewall(const uint8_t* in, const uint64_t* rec_off, uint64_t 
 hipError_t launch_encode(const EncodeParams& p, hipStream_t stream);
 // Mixed Get/Set batch: size pass (per-tile record-size totals, last workgroup scans them) + encode.
 size_t encode_mixed_ws_bytes(uint64_t n);
-hipError_t launch_encode_mixed(EncodeParams p, void* ws, unsigned* ticket, hipStream_t stream);
+hipError_t launch_encode_mixed(EncodeParams p, void* ws, hipStream_t stream);
 hipError_t launch_decode(const DecodeParams& p, hipStream_t stream);
 
 }  // namespace symhip

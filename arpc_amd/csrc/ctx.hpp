@@ -29,7 +29,7 @@ struct sym_ctx {
     void* flags = nullptr;  // default decode's aggregate / prefix words (epoch-tagged)
     size_t flag_bytes = 0;
     unsigned epoch = 0;     // tag of the last decode call's look-back words
-    unsigned* err = nullptr;  // [0] device error word (kErr* bits); [1] mixed-encode ticket (zero between calls)
+    unsigned* err = nullptr;  // [0] device error word (kErr* bits); [1] unused
     // scan workspace of the packetizer, the field getters, the flat decode and the mixed encode
     // (stream-ordered, so calls on one stream share it)
     void* frag = nullptr;

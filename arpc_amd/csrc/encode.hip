@@ -547,9 +547,7 @@ __global__ __launch_bounds__(256) void mixed_group_scan_kernel(MixedWs w, u64 ng
     }
 }
 
-// `ticket`: unused (kept for the caller's workspace layout).
-hipError_t launch_encode_mixed(EncodeParams p, void* ws, unsigned* ticket, hipStream_t stream) {
-    (void)ticket;
+hipError_t launch_encode_mixed(EncodeParams p, void* ws, hipStream_t stream) {
     if (p.n == 0) return hipMemsetAsync(p.out_off, 0, sizeof(uint64_t), stream);
     if (!p.type || p.lay.nfixed != 0 || p.lay.nvar != 2) return hipErrorInvalidValue;
     const MixedWs w = mixed_layout(ws, p.n);
