@@ -10,6 +10,8 @@ V in [16, 4096]), 0x5EED0003+g (config 4 shard g).
 """
 from __future__ import annotations
 
+import json
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -36,9 +38,12 @@ def random_bytes(seed: int, nbytes: int) -> np.ndarray:
 
 
 def lengths(spec, n: int, seed: int) -> np.ndarray:
-    """spec: int (every record), ("uniform", lo, hi) inclusive, ("loguniform", lo, hi) = floor(exp(U(ln lo, ln(hi+1))))."""
+    """spec: int (every record), ("uniform", lo, hi) inclusive, ("loguniform", lo, hi) = floor(exp(U(ln lo, ln(hi+1)))),
+    or an array of per-record lengths (cycled to n)."""
     if isinstance(spec, (int, np.integer)):
         return np.full(n, int(spec), dtype=np.uint64)
+    if isinstance(spec, np.ndarray):
+        return np.resize(spec.astype(np.uint64), n)
     kind, lo, hi = spec
     u = (splitmix64(seed, n) >> np.uint64(11)).astype(np.float64) * (1.0 / (1 << 53))
     if kind == "uniform":
@@ -119,12 +124,15 @@ class MixedBatch:
         return 22 * self.n + 8 * int((self.type != 0).sum()) + kl + vl
 
 
-def make_mixed_batch(n: int, key, value, set_fraction: float, seed: int, **_ignored) -> MixedBatch:
+def make_mixed_batch(n: int, key, value, set_fraction: float, seed: int, types=None, **_ignored) -> MixedBatch:
     """A kv request stream: record i is a SetRequest with probability `set_fraction` (splitmix64
-    stream seed + 0x7000), else a GetRequest; key lengths from `key`, value lengths from `value` for
-    SetRequests (GetRequests carry no value)."""
-    u = (splitmix64(seed + 0x7000, n) >> np.uint64(11)).astype(np.float64) * (1.0 / (1 << 53))
-    rtype = (u < set_fraction).astype(np.uint8)
+    stream seed + 0x7000), else a GetRequest (or `types`, per record, cycled to n); key lengths from
+    `key`, value lengths from `value` for SetRequests (GetRequests carry no value)."""
+    if types is not None:
+        rtype = np.resize(np.asarray(types, dtype=np.uint8), n)
+    else:
+        u = (splitmix64(seed + 0x7000, n) >> np.uint64(11)).astype(np.float64) * (1.0 / (1 << 53))
+        rtype = (u < set_fraction).astype(np.uint8)
     cols = []
     for f, spec in enumerate((key, value)):
         ln = lengths(spec, n, seed + 0x10000 * (f + 1))
@@ -134,6 +142,37 @@ def make_mixed_batch(n: int, key, value, set_fraction: float, seed: int, **_igno
         np.cumsum(ln, out=offs[1:])
         cols.append((random_bytes(seed + 0x100000000 * (f + 1), int(offs[-1])), offs))
     return MixedBatch(rtype, cols[0], cols[1])
+
+
+# The kv benchmark's trace (benchmark/meta-kv-trace/trace_large.req) as a size list
+# (tests/golden/trace_large_sizes.json, made by tests/golden/make_trace_sizes.py): the operation
+# sequence, key sizes 17-166, value sizes.
+TRACE_SIZES = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden",
+                           "trace_large_sizes.json")
+
+
+def trace_sizes() -> dict:
+    with open(TRACE_SIZES) as f:
+        t = json.load(f)
+    ops = np.frombuffer(t["ops"].encode(), dtype=np.uint8) == ord("S")
+    return dict(set=ops, key=np.array(t["key_size"], dtype=np.uint64), value=np.array(t["value_size"], dtype=np.uint64))
+
+
+def config3_trace(n: int = 1 << 20) -> dict:
+    """SURVEY 8d config 3, secondary variant: SetRequests with the trace's SET key sizes and its SET
+    value sizes clipped to [16, 4096], in trace order, cycled to n; bytes from the config-3 seed."""
+    t = trace_sizes()
+    k = t["key"][t["set"]]
+    v = np.clip(t["value"][t["set"]], 16, 4096)
+    return dict(schema="kv_set_request", n=n, lens=(k, v), seed=0x5EED0002)
+
+
+def config2_trace_mixed(n: int = 1 << 20) -> dict:
+    """The Get/Set request stream as the benchmark replays it: the trace's operation sequence, key
+    sizes and (SET) value sizes clipped to [16, 4096], cycled to n records (for make_mixed_batch)."""
+    t = trace_sizes()
+    return dict(n=n, key=t["key"], value=np.clip(t["value"], 16, 4096), set_fraction=TRACE_SET_FRACTION,
+                seed=0x5EED0001, types=t["set"].astype(np.uint8))
 
 
 def config4_shard(g: int, records_per_gpu: int = 1 << 23) -> dict:

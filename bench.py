@@ -550,14 +550,14 @@ def host_inclusive(codec: Codec, kw: dict, dev, steps: int) -> dict:
                     "algorithmic bytes as the headline; serial_one_stream: the same work unchunked on one stream"}
 
 
-def mixed_leg(codec: Codec, dev, reps: int) -> dict:
+def mixed_leg(codec: Codec, dev, reps: int, cfg=None) -> dict:
     """BASELINE config 2 as written ("1 M kv-store-symphony Get/Set records"): 2^20 requests at the
     trace's 36.9 % SetRequest share (datagen.CONFIG2_MIXED), K=64, V=256, encoded with
     sym_encode_kv_mixed (size pass + encode) and decoded with sym_decode_kv_mixed, device-resident,
     HIP events, two rotating buffer sets.  Algorithmic bytes -- encode: type n + keys + key offsets
     8(n+1) + Set values + value offsets 8(n+1) read, stream + 8(n+1) offsets written; decode: stream +
     8(n+1) + type n read, keys + values + 2 x 8(n+1) offsets + n status written."""
-    b = datagen.make_mixed_batch(**datagen.CONFIG2_MIXED)
+    b = datagen.make_mixed_batch(**(cfg or datagen.CONFIG2_MIXED))
     n = b.n
     total = b.encoded_size()
     kb, vb = int(b.key[1][-1]), int(b.val[1][-1])
@@ -607,10 +607,10 @@ def mixed_leg(codec: Codec, dev, reps: int) -> dict:
                     "kernel and group scan (three launches); client IDs: service 1, Get 1, Set 2"}
 
 
-def config3_leg(codec: Codec, dev, reps: int) -> dict:
+def config3_leg(codec: Codec, dev, reps: int, cfg=None) -> dict:
     """2^20 SetRequests, K=64, V log-uniform 16-4096 B (mean ~736 B, 774 MB stream:
     no set fits the Infinity Cache), encode + decode device-resident, HIP events, two buffer sets."""
-    b = datagen.make_batch(**datagen.CONFIG3)
+    b = datagen.make_batch(**(cfg or datagen.CONFIG3))
     s = b.schema
     n = b.n
     var_total = sum(int(o[-1] - o[0]) for _, o in b.var)
@@ -679,6 +679,8 @@ def main():
     ap.add_argument("--boutique-reps", type=int, default=3, help="online-boutique nested leg repetitions (0 = skip)")
     ap.add_argument("--mixed-reps", type=int, default=10, help="mixed Get/Set leg repetitions (0 = skip)")
     ap.add_argument("--config3-reps", type=int, default=6, help="config 3 leg repetitions (0 = skip)")
+    ap.add_argument("--trace-reps", type=int, default=3,
+                    help="trace-replay legs (config 3 trace sizes, Get/Set trace sequence) repetitions (0 = skip)")
     ap.add_argument("--ref-reps", type=int, default=-1,
                     help="decode reference timings (three-kernel, look-back only); -1 = max(5, steps/2), 0 = skip")
     args = ap.parse_args()
@@ -886,6 +888,17 @@ def main():
         line["mixed"] = mixed_leg(codec, dev, args.mixed_reps)
     if world == 1 and args.config3_reps > 0 and args.config == 2:
         line["config3"] = config3_leg(codec, dev, args.config3_reps)
+    if world == 1 and args.trace_reps > 0:
+        t3 = config3_leg(codec, dev, args.trace_reps, datagen.config3_trace())
+        t3["note"] = ("SURVEY 8d config 3, secondary variant: 2^20 SetRequests with the SET key sizes and "
+                      "the SET value sizes (clipped to [16, 4096]) of benchmark/meta-kv-trace/trace_large.req "
+                      "in trace order (tests/golden/trace_large_sizes.json), seed 0x5EED0002")
+        line["config3_trace"] = t3
+        tm = mixed_leg(codec, dev, args.trace_reps, datagen.config2_trace_mixed())
+        tm["note"] = ("the kv benchmark's request stream replayed: trace_large.req's GET/SET sequence, key sizes "
+                      "and SET value sizes (clipped to [16, 4096]), cycled to 2^20 requests; three-launch "
+                      "encode, pipeline decode")
+        line["mixed_trace"] = tm
     if world == 1 and args.host_steps > 0:
         line["host_inclusive"] = host_inclusive(codec, kw, dev, args.host_steps)
     if world == 1 and args.packetize_reps > 0:
