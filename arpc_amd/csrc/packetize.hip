@@ -32,7 +32,7 @@ namespace frag {
 constexpr int kHdr = 31;       // DataPacket header bytes (builtin_packets.go:68)
 constexpr int kWaveRecs = 64;  // records per wave tile
 constexpr int kWaves = 4;
-constexpr int kSlot = 64;      // header template slot: 16 zero bytes, 31 header bytes, zero padding
+constexpr int kSlot = 48;      // header template slot: 16 zero bytes, 31 header bytes, one zero byte
 
 // Fragment layout of one record (FragmentPackets): kpub full public packets, nmeet (0-2) meeting
 // packets of meet0 / meet1 bytes, then full private packets; M = payload bytes per datagram.
@@ -130,11 +130,13 @@ __global__ __launch_bounds__(256) void frag_count_kernel(const uint8_t* in, cons
 }
 
 // ---- write
+// 5.1 KiB per wave (7 workgroups per CU; 7.5 KiB with 64-byte slots and u64 layouts gave 5).  A
+// header window reads up to 15 bytes past its slot: the next slot's leading zeros, or `pad`.
 struct WaveLds {
-    char tmpl[kWaveRecs * kSlot];  // per record: 16 zero bytes, the 31-byte header (seq = len = 0), zeros
-    int o[kWaveRecs + 1];          // record's wire start relative to the tile; [cnt] = span
-    u64 kpub[kWaveRecs], nmeet[kWaveRecs], meet0[kWaveRecs], meet1[kWaveRecs], npk[kWaveRecs];
-    u64 addr[kWaveRecs];           // record's first byte (address)
+    char tmpl[kWaveRecs * kSlot + 16];  // per record: 16 zero bytes, the 31-byte header (seq = len = 0), a zero
+    int o[kWaveRecs + 1];               // record's wire start relative to the tile; [cnt] = span
+    u32 kpub[kWaveRecs], nmeet[kWaveRecs], meet0[kWaveRecs], meet1[kWaveRecs], npk[kWaveRecs];  // < 2^31: tile check
+    u64 addr[kWaveRecs];                // record's first byte (address)
 };
 
 struct WriteParams {
@@ -212,7 +214,11 @@ __global__ __launch_bounds__(kWaves * 64) void frag_write_kernel(WriteParams p) 
             p.dg_off[f0 + d] = O + fs + kHdr * d;
         }
         if (r == p.n - 1) p.dg_off[p.first[p.n]] = p.out_off[p.n];
+    } else {  // a slot past the tile's last record: its leading zeros end the last record's windows
+        uint2* slot = (uint2*)&S.tmpl[lane * kSlot];
+        slot[0] = slot[1] = make_uint2(0, 0);
     }
+    if (lane == 0) ((uint2*)&S.tmpl[kWaveRecs * kSlot])[0] = ((uint2*)&S.tmpl[kWaveRecs * kSlot])[1] = make_uint2(0, 0);
     wave_sync();
 
     // ---- phase 2 (lane = aligned 16-byte wire chunk)
