@@ -160,7 +160,7 @@ int sym_decode_echo(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_off
  * (kv.syn.go:74-185, 22 + K bytes), any other value a SetRequest{Key, Value} (:611-745, 30 + K + V).
  * Columns as above; a GetRequest's value slice is not part of its record (it is normally empty, and
  * decode writes it empty).  Record sizes depend on the type, so the record offsets are a device-wide
- * scan (a size pass over the type column + the encode); d_out must hold
+ * scan (a size pass over the type column, a scan of its group totals, then the encode); d_out must hold
  * sym_encoded_size_kv_mixed(...) bytes.  The client's ID patch writes get_method_id into GetRequests
  * and set_method_id into SetRequests (KVService: service 1, Get 1, Set 2, kv_arpc.syn.go:11-28);
  * 0/0/0 reproduces MarshalSymphony.  Decode takes the type column the server's method dispatch
