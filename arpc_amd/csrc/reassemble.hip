@@ -154,7 +154,11 @@ __global__ __launch_bounds__(256) void parse_kernel(Args a, unsigned* complex_fl
         if (st == SYM_RX_PENDING) c = Pair{pl, ((u64)1 << 32) | 1u};
     }
     if (i <= a.n) a.cnt[i] = c;
-    if (__ballot(!simple) && (threadIdx.x & 63) == 0) atomicOr(complex_flag, 1u);
+    // one flag check per workgroup, and the atomic only while the flag is still clear: a wave-level
+    // atomicOr on one word serialised ~20k atomics per batch of multi-datagram messages (~200 us)
+    if (__syncthreads_or(!simple) && threadIdx.x == 0 &&
+        __hip_atomic_load(complex_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+        atomicOr(complex_flag, 1u);
     Pair e, t;  // this tile's totals, for the scan of the triples (simple batches)
     block_scan_pair(c, e, t);
     if (threadIdx.x == 0) a.agg[blockIdx.x] = t;

@@ -888,6 +888,16 @@ def main():
         line["mixed"] = mixed_leg(codec, dev, args.mixed_reps)
     if world == 1 and args.config3_reps > 0 and args.config == 2:
         line["config3"] = config3_leg(codec, dev, args.config3_reps)
+    if world == 1 and args.reassembly_reps > 0:  # the general (multi-datagram) reassembly path
+        b3 = datagen.make_batch(**datagen.CONFIG3)
+        f3, v3 = to_device(b3, dev)
+        e3 = codec.encode(b3.schema, f3, v3, var_total=b3.encoded_size() - b3.n * b3.schema.overhead)
+        del b3, f3, v3
+        rc3 = reassembly_leg(codec, e3.data, e3.offsets, dev, args.reassembly_reps)
+        rc3["note"] = ("config 3 (V log-uniform 16-4096 B) packetized: records over 1369 payload bytes span "
+                       "several datagrams, so the general path runs (hash grouping, radix sort, group passes)")
+        line["reassembly_config3"] = rc3
+        del e3
     if world == 1 and args.trace_reps > 0:
         t3 = config3_leg(codec, dev, args.trace_reps, datagen.config3_trace())
         t3["note"] = ("SURVEY 8d config 3, secondary variant: 2^20 SetRequests with the SET key sizes and "
