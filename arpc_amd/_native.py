@@ -120,6 +120,7 @@ SYM_SET_PUBLIC_ONLY = 3
 SYM_SET_TOO_SHORT = 4
 SYM_SET_UNMARSHAL = 5
 SYM_SET_BOUNDS = 6
+SYM_SET_BAD_LENGTH = 7
 
 SYM_MAX_FLAT_FIELDS = 16
 SYM_FIELD_REPEATED = 0x80

@@ -185,6 +185,8 @@ def _decode_kv_mixed(codec: "Codec", data: torch.Tensor, rec_off: torch.Tensor, 
     _check_col(rec_off, torch.int64, "rec_off", codec.device)
     _check_col(rtype, torch.uint8, "type", codec.device)
     n = rec_off.numel() - 1
+    if rtype.numel() < n:  # the kernels read type[r] for every record
+        raise ValueError(f"type column has {rtype.numel()} entries for {n} records")
     if outputs is None:
         if caps is None:
             span = int(rec_off[-1].item() - rec_off[0].item()) if n else 0

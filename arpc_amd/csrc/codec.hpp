@@ -2,7 +2,18 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
+
+// Kernel-argument arrays indexed by a field / column number at run time must be 4-byte typed and
+// sit at a 4-byte-aligned (pointers: 8-byte) offset of their struct.  With a 1-byte array the
+// compiler once folded a field index into the base of a scalar load from the kernel arguments at a
+// misaligned offset; the scalar load ignored the low address bits, read a wrong pointer and the
+// kernel faulted on hardware (general schemas).  Every such array is checked here.
+#define SYMHIP_KERNARG_ARRAY(S, m)                                                                      \
+    static_assert(sizeof(((S*)nullptr)->m[0]) >= 4 && offsetof(S, m) % 4 == 0 &&                        \
+                      offsetof(S, m) % alignof(decltype(((S*)nullptr)->m[0])) == 0,                      \
+                  #S "::" #m ": an indexed kernel-argument array must be 4-byte typed and aligned")
 
 namespace symhip {
 
@@ -42,6 +53,10 @@ struct EncodeParams {
     int variant;    // kernel tuning variant (tuning builds only, tuning_variant("SYMHIP_ENCODE_VARIANT"))
 };
 
+SYMHIP_KERNARG_ARRAY(EncodeParams, fixed);
+SYMHIP_KERNARG_ARRAY(EncodeParams, bytes);
+SYMHIP_KERNARG_ARRAY(EncodeParams, offs);
+
 // Decode implementations selectable per ctx (sym_ctx_set_decode_impl).
 constexpr int kImplPipeline = 0;      // one launch: parsers, streaming scanner, copiers (default)
 constexpr int kImplThreeKernel = 1;   // parse -> scan -> copy, three stream-ordered launches
@@ -68,6 +83,11 @@ struct DecodeParams {
     int impl;       // kImpl*
     int variant;    // kernel tuning variant (tuning builds only, tuning_variant("SYMHIP_DECODE_VARIANT"))
 };
+
+SYMHIP_KERNARG_ARRAY(DecodeParams, fixed);
+SYMHIP_KERNARG_ARRAY(DecodeParams, bytes);
+SYMHIP_KERNARG_ARRAY(DecodeParams, cap);
+SYMHIP_KERNARG_ARRAY(DecodeParams, offs);
 
 // Device workspace for the single-pass decode scan: [0,16) tile ticket, then per var
 // field one u64 look-back word per tile.  Zeroed (as one block from its start) per call.

@@ -25,6 +25,12 @@ struct Schema {
     uint32_t seg[kMax], width[kMax], shift[kMax], list[kMax];
     uint32_t table[2];  // public / private table bytes
 };
+SYMHIP_KERNARG_ARRAY(Schema, seg);
+SYMHIP_KERNARG_ARRAY(Schema, width);
+SYMHIP_KERNARG_ARRAY(Schema, shift);
+SYMHIP_KERNARG_ARRAY(Schema, list);
+SYMHIP_KERNARG_ARRAY(Schema, table);
+static_assert(alignof(Schema) >= 4 && sizeof(Schema) % 4 == 0, "Schema is embedded in kernel arguments");
 
 inline bool is_payload(const sym_field& f) { return f.width == 0 || (f.width & (SYM_FIELD_REPEATED | SYM_FIELD_MESSAGE)); }
 inline uint8_t list_kind(const sym_field& f) {

@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdint>
 #include <cstring>
 #include <vector>
 
@@ -79,15 +80,27 @@ bool is_pinned(const void* p) {
     return a.type == hipMemoryTypeHost;
 }
 
-// Bump allocator over a slot buffer.
+// Bump allocator over a slot buffer.  `bad` latches a size that would wrap (never for validated
+// offsets; the sizing pass checks it before anything is allocated or copied).
 struct Carve {
     size_t at = 0;
+    bool bad = false;
     size_t take(size_t bytes) {
         const size_t o = at;
-        at = align256(at + bytes + 16);  // +16: kernels may read 16 bytes past a column
+        if (bytes > (SIZE_MAX >> 2) || at > (SIZE_MAX >> 2)) bad = true;
+        else at = align256(at + bytes + 16);  // +16: kernels may read 16 bytes past a column
         return o;
     }
 };
+
+// Every offset of a host column is >= the one before it.  The chunk sizes, the pinned copies and
+// the kernels' record placement all assume it; one pass over n+1 host words (~1 ms per 2^20
+// records), far below the PCIe time of the batch.
+bool monotone(const uint64_t* o, uint64_t n) {
+    uint64_t bad = 0;
+    for (uint64_t i = 0; i < n; ++i) bad |= (uint64_t)(o[i + 1] < o[i]);
+    return bad == 0;
+}
 
 uint64_t records_per_chunk(uint64_t n, uint64_t bytes) {
     const uint64_t avg = std::max<uint64_t>(1, bytes / std::max<uint64_t>(1, n));
@@ -158,7 +171,7 @@ int sym_encode_host(sym_ctx* ctx, int schema, uint64_t n, const int32_t* const* 
     uint64_t var_total = 0;
     for (int f = 0; f < lay.nvar; ++f) {
         if (!h_offs[f] || !h_bytes[f]) return fail(SYM_ERR_INVALID, "sym_encode_host: NULL var column %d", f);
-        if (h_offs[f][n] < h_offs[f][0]) return fail(SYM_ERR_INVALID, "sym_encode_host: offsets of field %d decrease", f);
+        if (!monotone(h_offs[f], n)) return fail(SYM_ERR_INVALID, "sym_encode_host: offsets of field %d decrease", f);
         var_total += h_offs[f][n] - h_offs[f][0];
     }
     const uint64_t ovh = sym_record_overhead(schema);
@@ -185,6 +198,8 @@ int sym_encode_host(sym_ctx* ctx, int schema, uint64_t n, const int32_t* const* 
         }
         d.take(m * ovh + vb);
         d.take(8 * (m + 1));
+        if (d.bad) return fail(SYM_ERR_INVALID, "sym_encode_host: chunk %llu does not fit the address space",
+                               (unsigned long long)c);
         dev_need = std::max(dev_need, d.at);
         if (!direct) pin_need = std::max(pin_need, d.at);
     }
@@ -292,7 +307,7 @@ int sym_decode_host(sym_ctx* ctx, int schema, uint64_t n, const uint8_t* h_in, c
         if (!h_fixed[f]) return fail(SYM_ERR_INVALID, "sym_decode_host: NULL fixed column %d", f);
     for (int f = 0; f < lay.nvar; ++f)
         if (!h_bytes[f] && caps[f]) return fail(SYM_ERR_INVALID, "sym_decode_host: NULL byte column %d", f);
-    if (h_rec_off[n] < h_rec_off[0]) return fail(SYM_ERR_INVALID, "sym_decode_host: record offsets decrease");
+    if (!monotone(h_rec_off, n)) return fail(SYM_ERR_INVALID, "sym_decode_host: record offsets decrease");
     const uint64_t R = records_per_chunk(n, h_rec_off[n] - h_rec_off[0]);
     const uint64_t C = (n + R - 1) / R;
 
@@ -313,6 +328,8 @@ int sym_decode_host(sym_ctx* ctx, int schema, uint64_t n, const uint8_t* h_in, c
             d.take(span);
             d.take(8 * (m + 1));
         }
+        if (d.bad) return fail(SYM_ERR_INVALID, "sym_decode_host: chunk %llu does not fit the address space",
+                               (unsigned long long)c);
         dev_need = std::max(dev_need, d.at);
     }
     DeviceGuard g(ctx->device);

@@ -52,6 +52,9 @@ struct SetArgs {
     unsigned* err;
 };
 
+SYMHIP_KERNARG_ARRAY(SetArgs, sc.seg);
+SYMHIP_KERNARG_ARRAY(SetArgs, sc.shift);
+
 // The buffer as Go sees it.  fake: the public remarshal's data + [0x01] + zeroed private table,
 // whose [1:5] holds len(data) (written before the marker, main.go:397-400).
 struct View {
@@ -165,6 +168,10 @@ __device__ Plan plan_one(const SetArgs& a, u64 i, View& v, u64 (&fx)[kMax], u64 
     }
     if (w) {  // fixed: in place
         p.mode = kPatch;
+        return p;
+    }
+    if (p.vn & ((1ull << sc.shift[k]) - 1)) {  // a repeated field's value is not whole elements
+        p.st = SYM_SET_BAD_LENGTH;
         return p;
     }
     u64 po = v.u32at(p.toff);

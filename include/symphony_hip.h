@@ -443,6 +443,9 @@ int sym_flat_nested_status(sym_ctx* ctx, const sym_field* fields, int nfields, i
 #define SYM_SET_TOO_SHORT 4       /* error "buffer too short" / "buffer too short for table entry" */
 #define SYM_SET_UNMARSHAL 5       /* error "failed to unmarshal: ..." (remarshal path) */
 #define SYM_SET_BOUNDS 6          /* Go panics with an index out of range (in-place write, fake segment) */
+#define SYM_SET_BAD_LENGTH 7      /* batch convention: a repeated field's value bytes are not a whole number of
+                                     elements (Go's typed setters cannot express it; sym_flat_encode reports
+                                     the same input as SYM_ERR_INVALID); the buffer is copied unchanged */
 int sym_raw_set(sym_ctx* ctx, const sym_field* fields, int nfields, int field, const uint8_t* d_in,
                 const uint64_t* d_rec_off, uint64_t n, const void* d_val, const uint64_t* d_val_off, uint8_t* d_out,
                 uint64_t out_cap, uint64_t* d_out_off, uint8_t* d_status, void* stream);

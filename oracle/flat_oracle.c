@@ -201,6 +201,7 @@ void sym_oracle_flat_decode(int nf, const Field* f, uint64_t n, const uint8_t* i
 #define SET_TOO_SHORT 4
 #define SET_UNMARSHAL 5
 #define SET_BOUNDS 6
+#define SET_BAD_LENGTH 7  /* batch convention: a repeated value that is not whole elements */
 
 /* table offset of field k inside its segment's table (public: absolute from 13; private: from 1) */
 static uint64_t field_table_off(const Field* f, int k) {
@@ -304,6 +305,7 @@ uint64_t sym_oracle_raw_set(int nf, const Field* f, int k, uint64_t n, const uin
         const uint64_t vn = sw ? (uint64_t)sw : val_off[i + 1] - val_off[i];
         uint64_t size = L;
         if (st == SET_OK && L < toff + (sw ? (uint64_t)sw : 4)) st = SET_TOO_SHORT;
+        if (st == SET_OK && !sw && vn % (uint64_t)ew) st = SET_BAD_LENGTH;
         if (st == SET_OK && sw) {          /* fixed: in place */
             memcpy(o, m, L);
             memcpy(o + toff, v, sw);

@@ -469,7 +469,8 @@ def flat_decode(fields, data, rec_off):
     return cols, st[:n]
 
 
-SET_OK, SET_COMPLETE_BUFFER, SET_INVALID_BUFFER, SET_PUBLIC_ONLY, SET_TOO_SHORT, SET_UNMARSHAL, SET_BOUNDS = range(7)
+(SET_OK, SET_COMPLETE_BUFFER, SET_INVALID_BUFFER, SET_PUBLIC_ONLY, SET_TOO_SHORT, SET_UNMARSHAL, SET_BOUNDS,
+ SET_BAD_LENGTH) = range(8)
 
 
 def raw_set_bound(fields, rec_off, val_bytes: int) -> int:

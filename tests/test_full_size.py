@@ -1,0 +1,157 @@
+"""Whole-stream parity at BASELINE.json's full sizes, and the N-rank HIP path.
+
+* config 4: one 2^23-record shard (K=64, V=256, seed 0x5EED0003), encoded on the GPU; the whole
+  2.9 GB stream's SHA-256 equals the C oracle's encoding of the same records (run beside it) and the
+  digest pinned in tests/golden/full_size_digests.json; the decode returns every column and offset.
+* configs 2 / 3 / the Get/Set mix at 2^20: the GPU stream digests equal the pinned oracle digests
+  (tests/test_gpu_parity.py and tests/test_mixed.py compare the same streams with the oracle run
+  beside them).
+* world 2: two processes, each running the HIP encoder and decoder on its own config-4-seeded shard
+  (device 0, gloo for the control traffic), rebase their offsets by the all_gather of shard totals;
+  the concatenated streams equal the oracle's encoding of both shards as ONE batch.
+
+Reference: benchmark/kv-store-symphony/symphony/kv.syn.go:611-745 (SetRequest), :74-185
+(GetRequest); the shards exchange no data.
+"""
+import hashlib
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from arpc_amd import datagen
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def pins():
+    with open(os.path.join(ROOT, "tests", "golden", "full_size_digests.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="module")
+def codec(dev):
+    from arpc_amd.codec import Codec
+    c = Codec(dev)
+    yield c
+    c.close()
+
+
+def sha(a: np.ndarray) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def encode_decode(codec, dev, kw):
+    """GPU encode of the seeded batch, then GPU decode of that stream; every decoded column checked
+    on the device.  Returns (batch, stream on host, offsets on host)."""
+    from arpc_amd.codec import to_device
+    b = datagen.make_batch(**kw)
+    fixed, var = to_device(b, dev)
+    enc = codec.encode(b.schema, fixed, var, var_total=b.encoded_size() - b.n * b.schema.overhead)
+    dec = codec.decode(b.schema, enc.data, enc.offsets, caps=[int(o[-1]) for _, o in b.var])
+    codec.check()
+    assert int(dec.status.sum().item()) == 0
+    for f, (bcol, ocol) in enumerate(var):
+        assert torch.equal(dec.var[f][1], ocol - ocol[0])
+        assert torch.equal(dec.var[f][0][:bcol.numel()], bcol)
+    stream = enc.data[:b.encoded_size()].cpu().numpy()
+    off = enc.offsets.cpu().numpy().view(np.uint64)
+    del enc, dec, fixed, var
+    torch.cuda.empty_cache()
+    return b, stream, off
+
+
+def test_config4_shard_whole_stream(codec, dev, pins):
+    """shard 0 of the 2^26-record batch, 2^23 records, 2.94 GB encoded."""
+    b, stream, off = encode_decode(codec, dev, datagen.config4_shard(0))
+    assert b.n == 1 << 23 and stream.size == 350 * (1 << 23)
+    got = sha(stream)
+    assert got == pins["config4_shard0"]["sha256_stream"]
+    assert sha(off) == pins["config4_shard0"]["sha256_offsets"]
+    want, woff = oracle.encode_batch(b.fixed, b.var)
+    assert got == sha(want)
+    np.testing.assert_array_equal(off, woff)
+
+
+@pytest.mark.parametrize("name", ["config2", "config3"])
+def test_full_size_stream_matches_pin(codec, dev, pins, name):
+    kw = datagen.CONFIG2 if name == "config2" else datagen.CONFIG3
+    _, stream, off = encode_decode(codec, dev, kw)
+    assert stream.size == pins[name]["stream_bytes"]
+    assert sha(stream) == pins[name]["sha256_stream"]
+    assert sha(off) == pins[name]["sha256_offsets"]
+
+
+def test_mixed_full_size_stream_matches_pin(codec, dev, pins):
+    b = datagen.make_mixed_batch(**datagen.CONFIG2_MIXED)
+    t = torch.from_numpy(b.type).to(dev)
+    key = (torch.from_numpy(b.key[0]).to(dev), torch.from_numpy(b.key[1].view(np.int64)).to(dev))
+    val = (torch.from_numpy(b.val[0]).to(dev), torch.from_numpy(b.val[1].view(np.int64)).to(dev))
+    enc = codec.encode_kv_mixed(t, key, val, 1, 1, 2, out_bytes=b.encoded_size())
+    codec.check()
+    assert sha(enc.data[:b.encoded_size()].cpu().numpy()) == pins["config2_mixed"]["sha256_stream"]
+    assert sha(enc.offsets.cpu().numpy().view(np.uint64)) == pins["config2_mixed"]["sha256_offsets"]
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_world2_hip_shards(pins, tmp_path):
+    """SURVEY 8e on hardware: two ranks (fresh interpreters, started before they touch the GPU), each
+    running the HIP codec on its own shard; no data-path collective, one all_gather of shard totals.
+    The concatenated rank streams and rebased offsets equal ONE oracle encode of both shards."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    records, world, port = 1 << 20, 2, _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), PYTHONPATH=ROOT)
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "shard_worker.py"), str(tmp_path),
+                                       str(records)], env=env))
+    try:
+        codes = [p.wait(timeout=100) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    assert codes == [0] * world, codes
+    metas = [open(tmp_path / f"meta{r}.txt").read().split() for r in range(world)]
+    bases, gtotals, totals = ([int(m[i]) for m in metas] for i in range(3))
+    assert bases == [0, totals[0]] and gtotals == [sum(totals)] * world
+    stream = np.concatenate([np.load(tmp_path / f"stream{r}.npy") for r in range(world)])
+    offs = [np.load(tmp_path / f"off{r}.npy") for r in range(world)]
+    goff = np.concatenate([offs[0][:-1], offs[1]])
+    assert sha(stream) == pins["config4_w2"]["sha256_stream"]
+    assert sha(goff) == pins["config4_w2"]["sha256_offsets"]
+    # and the oracle run here agrees: both shards' records as one batch
+    shards = [datagen.make_batch(**datagen.config4_shard(g, records)) for g in range(world)]
+    cols = []
+    for f in range(len(shards[0].var)):
+        by = np.concatenate([s.var[f][0] for s in shards])
+        o0, o1 = shards[0].var[f][1], shards[1].var[f][1]
+        cols.append((by, np.concatenate([o0, o1[1:] + o0[-1]])))
+    want, woff = oracle.encode_batch([], cols)
+    assert sha(stream) == sha(want)
+    np.testing.assert_array_equal(goff, woff)

@@ -6,6 +6,8 @@ KVService Get = 1, Set = 2, kv_arpc.syn.go:25-28).  sym_encode_kv_mixed / sym_de
 per-record type column.  Bar: bit-exact against the oracle (oracle/symphony_oracle.c
 sym_oracle_*_kv_mixed), whose mixed form is pinned here to the per-type hand-derived KATs.
 """
+import hashlib
+
 import numpy as np
 import pytest
 
@@ -244,12 +246,28 @@ def test_gpu_mixed_full_size_trace_ratio(codec, dev):
     assert int(dec.status.sum().item()) == 0
     assert torch.equal(dec.var[0][1], key[1]) and torch.equal(dec.var[0][0][:key[0].numel()], key[0])
     assert torch.equal(dec.var[1][1], val[1]) and torch.equal(dec.var[1][0][:val[0].numel()], val[0])
-    lo, hi = n // 3, n // 3 + 3000  # a slice equals the oracle's encoding of the same records
-    sub_k = (b.key[0][b.key[1][lo]:b.key[1][hi]], b.key[1][lo:hi + 1] - b.key[1][lo])
-    sub_v = (b.val[0][b.val[1][lo]:b.val[1][hi]], b.val[1][lo:hi + 1] - b.val[1][lo])
-    want, _ = oracle.encode_kv_mixed(b.type[lo:hi], sub_k, sub_v, 1, 1, 2)
-    a, z = int(enc.offsets[lo].item()), int(enc.offsets[hi].item())
-    np.testing.assert_array_equal(enc.data[a:z].cpu().numpy(), want)
+    # the WHOLE stream equals the oracle's encoding of the same records (kv.syn.go:74-132, :611-678)
+    want, woff = oracle.encode_kv_mixed(b.type, b.key, b.val, 1, 1, 2)
+    got = enc.data[:b.encoded_size()].cpu().numpy()
+    assert hashlib.sha256(got.tobytes()).hexdigest() == hashlib.sha256(want.tobytes()).hexdigest()
+    np.testing.assert_array_equal(enc.offsets.cpu().numpy().view(np.uint64), woff)
+    # and the decode of the oracle's stream equals the oracle's decode, column by column
+    wcols, wst = oracle.decode_kv_mixed(want, woff, b.type)
+    np.testing.assert_array_equal(dec.status.cpu().numpy()[:n], wst)
+    for (gb, go), (wb, wo) in zip(dec.var, wcols):
+        np.testing.assert_array_equal(go.cpu().numpy().view(np.uint64), wo)
+        np.testing.assert_array_equal(gb[:len(wb)].cpu().numpy(), wb)
+
+
+@pytest.mark.gpu
+def test_gpu_mixed_short_type_column_rejected(codec, dev):
+    """The decode reads type[r] for every record: a type column shorter than the batch is refused on
+    the host (as the encode does) instead of being read past its end on the device."""
+    b = datagen.make_mixed_batch(n=100, key=8, value=16, set_fraction=0.5, seed=3)
+    stream, off = oracle.encode_kv_mixed(b.type, b.key, b.val)
+    d = _put(np.concatenate([stream, np.zeros(1, np.uint8)]).astype(np.uint8), dev)
+    with pytest.raises(ValueError, match="type column"):
+        codec.decode_kv_mixed(d, _put(off, dev), _put(b.type[:99], dev))
 
 
 @pytest.mark.gpu

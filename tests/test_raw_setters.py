@@ -120,6 +120,19 @@ def test_repeated_fixed_setter():
     assert got[0][0].tobytes() == struct.pack("<i", 9)
 
 
+def test_repeated_value_not_whole_elements():
+    """A repeated int32 value of 6 bytes is not a whole number of elements: Go's typed setters cannot
+    express it, and the batch setter reports SET_BAD_LENGTH and copies the buffer unchanged (in place
+    and remarshal cases alike), as sym_flat_encode rejects the same column."""
+    fields = [(1, REP | 4), (0, REP | 8)]
+    rec, _ = oracle.flat_encode(fields, [one(struct.pack("<3i", 1, 2, 3)), one(b"")], 1)
+    for v in (b"\x01" * 6, b"\x01" * 13, b"\x07"):
+        b, st = set1(fields, 0, rec.tobytes(), v)
+        assert st == oracle.SET_BAD_LENGTH and b == rec.tobytes()
+    b, st = set1(fields, 0, rec.tobytes(), b"\x01" * 8)  # two whole elements: in place
+    assert st == oracle.SET_OK and len(b) == len(rec)
+
+
 # ---------------------------------------------------------------- batch generators shared with the GPU tests
 def make_batch(rng, fields, n):
     """n buffers of `fields`: complete records, public-only prefixes, truncated and corrupted ones."""
@@ -235,6 +248,26 @@ def test_gpu_reference_sequences(codec, dev):
         np.testing.assert_array_equal(gst, wst)
         np.testing.assert_array_equal(goff, woff)
         np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.gpu
+def test_gpu_repeated_value_not_whole_elements(codec, dev):
+    """SET_BAD_LENGTH on the GPU: ragged value lengths against a repeated int32 field, in-place and
+    remarshal candidates mixed, bit-exact with the oracle."""
+    fields = [(1, REP | 4), (0, REP | 8), (1, 0)]
+    rng = np.random.default_rng(77)
+    n = 900
+    data, off = make_batch(rng, fields, n)
+    ln = rng.integers(0, 20, n).astype(np.uint64)  # any byte length, most not multiples of 4
+    voff = np.zeros(n + 1, np.uint64)
+    np.cumsum(ln, out=voff[1:])
+    vals = (rng.integers(0, 256, int(voff[-1]), dtype=np.uint8), voff)
+    want, woff, wst = oracle.raw_set(fields, 0, data, off, vals)
+    assert (wst == oracle.SET_BAD_LENGTH).any() and (wst == oracle.SET_OK).any()
+    got, goff, gst = gpu_set(codec, dev, fields, 0, data, off, vals)
+    np.testing.assert_array_equal(gst, wst)
+    np.testing.assert_array_equal(goff, woff)
+    np.testing.assert_array_equal(got, want)
 
 
 @pytest.mark.gpu
