@@ -75,6 +75,11 @@ SIGNATURES = {
     "sym_flat_decode_ex": (_int, [_ctx, _vp, _int, _u64, _u8p, _u64p, _vp, _vp, _vp, _vp, _vp, _u8p, _u8p, _vp]),
     "sym_flat_nested_status": (_int, [_ctx, _vp, _int, _int, _u64, _u64p, _u8p, _u8p, _u8p, _vp]),
     "sym_raw_set": (_int, [_ctx, _vp, _int, _int, _u8p, _u64p, _u64, _vp, _u64p, _u8p, _u64, _u64p, _u8p, _vp]),
+    "sym_batcher_create": (_int, [_int, _int, _u32, _u64, _u32, ctypes.POINTER(ctypes.c_void_p)]),
+    "sym_batcher_destroy": (_int, [_vp]),
+    "sym_batcher_encode_one": (_int, [_vp, _vp, _vp, _vp, _u32, _u32, _u8p, _u64, _u64p]),
+    "sym_batcher_decode_one": (_int, [_vp, _u8p, _u64, _vp, _vp, _vp, _vp, _u8p]),
+    "sym_batcher_stats": (_int, [_vp, _u64p, _u64p, _u64p, _u64p]),
     "sym_encrypt": (_int, [_ctx, _u8p, _u64p, _u64, ctypes.c_char_p, ctypes.c_char_p, _u8p, _u8p, _u64p, _u8p, _vp]),
     "sym_decrypt": (_int, [_ctx, _u8p, _u64p, _u64, ctypes.c_char_p, ctypes.c_char_p, _u8p, _u64p, _u8p, _vp]),
 }

@@ -239,6 +239,84 @@ class SymphonySerializer:
         return errs
 
 
+class BatchingSerializer:
+    """The per-record drop-in for pkg/serializer.SymphonySerializer under concurrency: every
+    marshal / unmarshal call is one record (as Go's Call goroutines make them, pkg/rpc/client.go:233-310,
+    server.go:152 / :173), coalesced with the calls other threads make meanwhile into one device
+    batch by the C ABI's batcher (sym_batcher_*, arpc_amd/csrc/batcher.cpp).  Same results and
+    errors as SymphonySerializer; safe to share across threads (ctypes releases the GIL while a
+    call waits for its batch)."""
+
+    def __init__(self, device: int = 0, service_id: int = 0, method_id: int = 0, max_records: int = 4096,
+                 max_bytes: int = 8 << 20, max_wait_us: int = 0):
+        self.device, self.service_id, self.method_id = device, service_id, method_id
+        self._cfg = (max_records, max_bytes, max_wait_us)
+        self._batchers: dict = {}
+        self._lock = threading.Lock()
+
+    def _batcher(self, s: schemas.Schema):
+        b = self._batchers.get(s.schema_id)
+        if b is None:
+            with self._lock:
+                b = self._batchers.get(s.schema_id)
+                if b is None:
+                    h = ctypes.c_void_p()
+                    _native.check(_native.lib().sym_batcher_create(self.device, s.schema_id, *self._cfg,
+                                                                   ctypes.byref(h)), "sym_batcher_create")
+                    b = self._batchers[s.schema_id] = h
+        return b
+
+    def marshal(self, msg) -> bytes:
+        s = _schema_of(msg)
+        vals = [_b(getattr(msg, f)) for f in s.var_fields]
+        fixed = (ctypes.c_int32 * max(1, s.nfixed))(*[_i32(getattr(msg, f)) for f in s.fixed_fields])
+        bufs = [ctypes.create_string_buffer(v, max(1, len(v))) for v in vals]
+        ptrs = (ctypes.c_void_p * max(1, s.nvar))(*[ctypes.addressof(b) for b in bufs])
+        lens = (ctypes.c_uint64 * max(1, s.nvar))(*[len(v) for v in vals])
+        size = s.overhead + sum(len(v) for v in vals)
+        out = ctypes.create_string_buffer(max(1, size))
+        n = ctypes.c_uint64()
+        _native.check(_native.lib().sym_batcher_encode_one(self._batcher(s), fixed, ptrs, lens, self.service_id,
+                                                           self.method_id, out, size, ctypes.byref(n)),
+                      "sym_batcher_encode_one")
+        return out.raw[:n.value]
+
+    def unmarshal(self, data: bytes, out) -> None:
+        s = _schema_of(out)
+        data = bytes(data)
+        cap = max(1, len(data))
+        fixed = (ctypes.c_int32 * max(1, s.nfixed))()
+        bufs = [ctypes.create_string_buffer(cap) for _ in range(s.nvar)]
+        ptrs = (ctypes.c_void_p * max(1, s.nvar))(*[ctypes.addressof(b) for b in bufs])
+        caps = (ctypes.c_uint64 * max(1, s.nvar))(*([cap] * s.nvar))
+        lens = (ctypes.c_uint64 * max(1, s.nvar))()
+        st = ctypes.c_uint8()
+        _native.check(_native.lib().sym_batcher_decode_one(self._batcher(s), data, len(data), fixed, ptrs, caps, lens,
+                                                           ctypes.byref(st)), "sym_batcher_decode_one")
+        for f, name in enumerate(s.fixed_fields):
+            setattr(out, name, int(fixed[f]))
+        for f, name in enumerate(s.var_fields):
+            setattr(out, name, bufs[f].raw[:lens[f]])
+        if st.value:
+            raise SymphonyError(int(st.value))
+
+    def stats(self) -> dict:
+        """Batches flushed and records carried per schema and direction (sym_batcher_stats)."""
+        out = {}
+        for sid, b in list(self._batchers.items()):
+            v = [ctypes.c_uint64() for _ in range(4)]
+            _native.check(_native.lib().sym_batcher_stats(b, *[ctypes.byref(x) for x in v]), "sym_batcher_stats")
+            out[sid] = {"encode_batches": v[0].value, "encode_records": v[1].value,
+                        "decode_batches": v[2].value, "decode_records": v[3].value}
+        return out
+
+    def close(self) -> None:
+        with self._lock:
+            for b in self._batchers.values():
+                _native.lib().sym_batcher_destroy(b)
+            self._batchers.clear()
+
+
 def _group_by_schema(msgs) -> dict:
     groups: dict = {}
     for i, m in enumerate(msgs):
@@ -250,6 +328,6 @@ def message_fields(msg) -> dict:
     return {f.name: getattr(msg, f.name) for f in fields(msg)}
 
 
-__all__ = ["SymphonySerializer", "SymphonyError", "ERROR_TEXT", "GetRequest", "SetRequest", "GetResponse",
+__all__ = ["SymphonySerializer", "BatchingSerializer", "SymphonyError", "ERROR_TEXT", "GetRequest", "SetRequest", "GetResponse",
            "SetResponse", "EchoRequest", "EchoResponse", "MESSAGE_TYPES", "encode_columns_host",
            "decode_columns_host", "message_fields"]

@@ -550,6 +550,40 @@ def host_inclusive(codec: Codec, kw: dict, dev, steps: int) -> dict:
                     "algorithmic bytes as the headline; serial_one_stream: the same work unchunked on one stream"}
 
 
+def per_record_leg(records: int, threads: int) -> dict:
+    """The per-record Serializer path (SURVEY.md 8b "Threading"; pkg/rpc/client.go:233-310,
+    pkg/serializer/symphony.go:10-16): one SetRequest per call, from a plain-C client
+    (tests/batcher_driver.c, a child process) -- without coalescing (one sym_encode_host +
+    sym_decode_host call per record: the latency of a record alone) and through the coalescing
+    batcher (sym_batcher_encode_one + decode_one) at 1 thread (its per-record latency) and at
+    `threads` threads (throughput).  Records: key 0-69 B, value 0-299 B (the driver's rec())."""
+    import subprocess
+    drv = os.path.join(ROOT, "tests", "bin", "batcher_driver")
+    if not os.path.exists(drv):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests")], check=True, capture_output=True)
+
+    def run(*args) -> float:
+        r = subprocess.run([drv, *[str(a) for a in args]], capture_output=True, text=True, timeout=120)
+        if r.returncode != 0:
+            raise RuntimeError(r.stdout + r.stderr)
+        return float(r.stdout.rsplit("elapsed_s=", 1)[1].split()[0])
+
+    h1 = run(1, records, "-", "host1")
+    b1 = run(1, records, "-", "bench")
+    per = max(1, (4 * records) // threads)
+    bt = run(threads, per, "-", "bench")
+    us = lambda el, k: round(el / k * 1e6, 2)  # noqa: E731
+    return {"unbatched_n1": {"records": records, "us_per_record_enc_plus_dec": us(h1, records),
+                             "records_per_s": round(records / h1, 1)},
+            "batcher_1_thread": {"records": records, "us_per_record_enc_plus_dec": us(b1, records),
+                                 "records_per_s": round(records / b1, 1)},
+            f"batcher_{threads}_threads": {"records": threads * per, "records_per_s": round(threads * per / bt, 1),
+                                           "calls_per_s": round(2 * threads * per / bt, 1)},
+            "note": "plain-C client (tests/batcher_driver.c): each record is one Marshal-like and one "
+                    "Unmarshal-like call; records_per_s counts records through both; compare "
+                    "cpu_baseline.config1_echo (the C restatement, one record per call on one core)"}
+
+
 def mixed_leg(codec: Codec, dev, reps: int, cfg=None) -> dict:
     """BASELINE config 2 as written ("1 M kv-store-symphony Get/Set records"): 2^20 requests at the
     trace's 36.9 % SetRequest share (datagen.CONFIG2_MIXED), K=64, V=256, encoded with
@@ -681,6 +715,8 @@ def main():
     ap.add_argument("--config3-reps", type=int, default=6, help="config 3 leg repetitions (0 = skip)")
     ap.add_argument("--trace-reps", type=int, default=3,
                     help="trace-replay legs (config 3 trace sizes, Get/Set trace sequence) repetitions (0 = skip)")
+    ap.add_argument("--per-record", type=int, default=2000,
+                    help="per-record Serializer path: records per timing run of tests/batcher_driver (0 = skip)")
     ap.add_argument("--ref-reps", type=int, default=-1,
                     help="decode reference timings (three-kernel, look-back only); -1 = max(5, steps/2), 0 = skip")
     args = ap.parse_args()
@@ -923,6 +959,8 @@ def main():
         line["flat"] = flat_leg(codec, dev, args.flat_reps)
     if world == 1 and args.boutique_reps > 0:
         line["boutique"] = boutique_leg(codec, dev, args.boutique_reps)
+    if world == 1 and args.per_record > 0:
+        line["per_record"] = per_record_leg(args.per_record, 64)
     if world == 1 and args.cpu_seconds > 0:
         line["cpu_baseline"] = cpu_baseline(kw, args.cpu_seconds)
     print(json.dumps(line), flush=True)

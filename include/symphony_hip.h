@@ -192,6 +192,45 @@ int sym_decode_host(sym_ctx* ctx, int schema, uint64_t n, const uint8_t* h_in, c
                     int32_t* const* h_fixed, uint8_t* const* h_bytes, const uint64_t* caps, uint64_t* const* h_offs,
                     uint8_t* h_status);
 
+/* ---- coalescing batcher: the per-record Serializer path (SURVEY.md 8b "Threading") --------
+ * The reference Serializer takes ONE record per call, concurrently from many goroutines:
+ *   Marshal   client Call per request  pkg/rpc/client.go:233-310 (:252), server reply :173
+ *   Unmarshal server receive loop      pkg/rpc/server.go:152, client response  client.go:205
+ *   adapter                            pkg/serializer/symphony.go:10-16
+ * A batcher turns those concurrent one-record calls into device batches.  A caller appends its
+ * record to the open batch of its direction and blocks; when no batch of that direction is on the
+ * GPU, one caller of the open batch runs it (no extra thread): at once with max_wait_us = 0 --
+ * under load a batch is whatever arrived while the previous one ran -- else once it holds
+ * max_records records or max_bytes bytes of records or its first record has waited max_wait_us;
+ * every caller then copies its own result out.  All entry points are thread-safe.  The batcher
+ * owns two contexts on `device` (one per direction) and pinned staging that the kernels read and
+ * write in place (mapped host memory), so one batch is one kernel launch and one stream
+ * synchronisation.  Results are bit-identical to sym_encode / sym_decode of the same records.
+ *   sym_batcher_encode_one  MarshalSymphony of one record + the client's ID patch of bytes [5:13]
+ *                           (service_id / method_id; 0 / 0 = MarshalSymphony's own bytes):
+ *                           fixed[nfixed] int32 values, fields[nvar] pointers with lens[nvar]; out
+ *                           receives sym_encoded_size(schema, 1, sum(lens)) bytes (*out_len; a
+ *                           smaller out_cap returns SYM_ERR_CAPACITY with *out_len set).
+ *   sym_batcher_decode_one  UnmarshalSymphony of data[0, len) into a fresh struct: fixed[nfixed],
+ *                           field f's bytes into fields[f] (caps[f] bytes; len always suffices) and
+ *                           lens[f]; *status = SYM_STATUS_* (a malformed record is SYM_OK with its
+ *                           status, as Go returns an error value); a field longer than its cap
+ *                           returns SYM_ERR_CAPACITY with the bytes that fit copied.
+ * A record larger than max_bytes is SYM_ERR_INVALID.  The caller's memory is read and written only
+ * during the call (cgo's pointer rules hold: nothing is kept after return). */
+typedef struct sym_batcher sym_batcher;
+int sym_batcher_create(int device, int schema, uint32_t max_records, uint64_t max_bytes, uint32_t max_wait_us,
+                       sym_batcher** out);
+int sym_batcher_destroy(sym_batcher* b); /* no call may be in progress */
+int sym_batcher_encode_one(sym_batcher* b, const int32_t* fixed, const uint8_t* const* fields, const uint64_t* lens,
+                           uint32_t service_id, uint32_t method_id, uint8_t* out, uint64_t out_cap,
+                           uint64_t* out_len);
+int sym_batcher_decode_one(sym_batcher* b, const uint8_t* data, uint64_t len, int32_t* fixed, uint8_t* const* fields,
+                           const uint64_t* caps, uint64_t* lens, uint8_t* status);
+/* batches run and records carried, per direction (any pointer may be NULL) */
+int sym_batcher_stats(sym_batcher* b, uint64_t* enc_batches, uint64_t* enc_records, uint64_t* dec_batches,
+                      uint64_t* dec_records);
+
 /* ---- packetization: aRPC's send side over a batch of marshalled records ----------
  * What UDPTransport.Send does to one message (pkg/transport/transport.go:146-201), for n records:
  * FragmentPackets(data, max_udp_payload - 31) (pkg/transport/symphony_fragmentation.go:23-125), then

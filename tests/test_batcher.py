@@ -1,0 +1,183 @@
+"""The coalescing batcher (sym_batcher_*, arpc_amd/csrc/batcher.cpp): concurrent one-record
+Marshal / Unmarshal calls carried by device batches, bit-exact with the oracle.
+
+The reference Serializer is one record per call, called concurrently from many goroutines
+(pkg/rpc/client.go:233-310 Call / :252 Marshal, server.go:152 / :173, pkg/serializer/symphony.go:10-16;
+SURVEY.md 8b "Threading").  Here:
+* tests/batcher_driver.c: POSIX threads in a plain C program (gcc against include/symphony_hip.h),
+  each encoding and decoding its own records one per call; every encoded record is compared here
+  with the C oracle's MarshalSymphony (+ the client's ID patch, client.go:267-271);
+* arpc_amd.serializer.BatchingSerializer from many Python threads over every schema, against the
+  oracle, including Go's error texts and int32 fields kept up to the error (echo.syn.go:223-231).
+"""
+import os
+import struct
+import subprocess
+import threading
+
+import numpy as np
+import pytest
+
+from arpc_amd import _native
+from oracle import oracle
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DRIVER = os.path.join(ROOT, "tests", "bin", "batcher_driver")
+
+
+def _build():
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests")], check=True)
+    return DRIVER
+
+
+def test_batcher_driver_builds_against_header():
+    assert os.path.exists(_build())
+
+
+def test_batcher_rejects_bad_arguments_without_gpu():
+    import ctypes
+    L = _native.lib()
+    h = ctypes.c_void_p()
+    assert L.sym_batcher_create(0, 99, 16, 1 << 20, 0, ctypes.byref(h)) == _native.SYM_ERR_INVALID
+    assert L.sym_batcher_create(0, 1, 0, 1 << 20, 0, ctypes.byref(h)) == _native.SYM_ERR_INVALID
+    assert L.sym_batcher_create(0, 1, 16, 8, 0, ctypes.byref(h)) == _native.SYM_ERR_INVALID
+    assert L.sym_batcher_create(0, 1, 16, 1 << 20, 0, None) == _native.SYM_ERR_INVALID
+    assert L.sym_batcher_destroy(None) == 0
+
+
+def driver_record(t: int, i: int):
+    """The record batcher_driver.c's rec() builds for thread t, record i."""
+    kl, vl = (t * 7 + i * 3) % 70, (t * 13 + i * 5) % 300
+    key = bytes((t * 31 + i * 17 + j) & 0xFF for j in range(kl))
+    val = bytes((t * 11 + i * 29 + 3 * j) & 0xFF for j in range(vl))
+    return key, val
+
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return 0
+
+
+@pytest.mark.gpu
+def test_c_threads_through_batcher(gpu, tmp_path):
+    path = DRIVER if os.path.exists(DRIVER) else _build()
+    out = tmp_path / "enc.bin"
+    threads, per = 48, 120
+    r = subprocess.run([path, str(threads), str(per), str(out)], capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert f"{threads * per} records ok" in r.stdout, r.stdout
+    batches = int(r.stdout.split(" in ")[1].split()[0])
+    assert batches < threads * per  # concurrent calls shared batches
+    blob = out.read_bytes()
+    pos = 0
+    for t in range(threads):
+        for i in range(per):
+            (n,) = struct.unpack_from("<I", blob, pos)
+            got = blob[pos + 4:pos + 4 + n]
+            pos += 4 + n
+            key, val = driver_record(t, i)
+            ids = (1, 2) if i & 1 else (0, 0)
+            assert got == oracle.marshal([], [key, val], *ids), (t, i)
+    assert pos == len(blob)
+
+
+def _messages(rng, k):
+    from arpc_amd.serializer import EchoRequest, GetRequest, GetResponse, SetRequest, SetResponse
+    kind = k % 5
+    b = lambda n: rng.integers(0, 256, n, dtype=np.uint8).tobytes()  # noqa: E731
+    if kind == 0:
+        return SetRequest(b(int(rng.integers(0, 80))), b(int(rng.integers(0, 600))))
+    if kind == 1:
+        return GetRequest(b(int(rng.integers(0, 80))))
+    if kind == 2:
+        return GetResponse(b(int(rng.integers(0, 400))))
+    if kind == 3:
+        return SetResponse(b(int(rng.integers(0, 40))))
+    return EchoRequest(int(rng.integers(-2**31, 2**31)), int(rng.integers(-2**31, 2**31)), b(int(rng.integers(0, 20))),
+                       b(int(rng.integers(0, 200))))
+
+
+@pytest.mark.gpu
+def test_python_threads_every_schema(gpu):
+    from arpc_amd.serializer import BatchingSerializer
+    ser = BatchingSerializer(gpu, max_records=128, max_wait_us=50)
+    errors = []
+
+    def work(t):
+        try:
+            rng = np.random.default_rng(t)
+            for k in range(60):
+                m = _messages(rng, k + t)
+                data = ser.marshal(m)
+                s = m.SCHEMA
+                want = oracle.marshal([getattr(m, f) for f in s.fixed_fields], [getattr(m, f) for f in s.var_fields])
+                assert data == want, (t, k)
+                out = type(m)()
+                ser.unmarshal(data, out)
+                assert out == m, (t, k)
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(32)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=120)
+    assert not errors, errors[:3]
+    st = ser.stats()
+    assert sum(v["encode_records"] for v in st.values()) == 32 * 60
+    assert sum(v["encode_batches"] for v in st.values()) < 32 * 60
+    ser.close()
+
+
+@pytest.mark.gpu
+def test_batcher_errors_and_ids(gpu):
+    """Go's error texts (kv.syn.go:681-698, echo.syn.go:223-231) and the client ID patch."""
+    from arpc_amd.serializer import BatchingSerializer, EchoRequest, SetRequest, SymphonyError
+    ser = BatchingSerializer(gpu, service_id=1, method_id=2)
+    m = SetRequest(b"ab", b"xyz")
+    assert ser.marshal(m).hex() == "010d00000001000000020000000109000000" "0f00000002000000616203000000" "78797a"
+    for data, text in [(b"", "invalid data: too short"), (b"\x02" * 13, "wrong public version"),
+                       (bytes.fromhex("010d00000000000000000000000000"), "missing private segment")]:
+        with pytest.raises(SymphonyError, match=text):
+            ser.unmarshal(data, SetRequest())
+    out = EchoRequest()
+    with pytest.raises(SymphonyError, match="too short for field"):
+        ser.unmarshal(bytes.fromhex("010d0000000000000000000000012a000000"), out)
+    assert out.Id == 42 and out.Score == 0
+    ser.close()
+
+
+@pytest.mark.gpu
+def test_batcher_capacity_and_size_limits(gpu):
+    import ctypes
+    L = _native.lib()
+    h = ctypes.c_void_p()
+    _native.check(L.sym_batcher_create(0, 1, 8, 4096, 0, ctypes.byref(h)), "create")
+    key, val = b"k" * 10, b"v" * 100
+    f = (ctypes.c_void_p * 2)(ctypes.cast(ctypes.c_char_p(key), ctypes.c_void_p),
+                              ctypes.cast(ctypes.c_char_p(val), ctypes.c_void_p))
+    lens = (ctypes.c_uint64 * 2)(10, 100)
+    out = ctypes.create_string_buffer(200)
+    n = ctypes.c_uint64()
+    assert L.sym_batcher_encode_one(h, None, f, lens, 0, 0, out, 100, ctypes.byref(n)) == _native.SYM_ERR_CAPACITY
+    assert n.value == 140
+    assert L.sym_batcher_encode_one(h, None, f, lens, 0, 0, out, 200, ctypes.byref(n)) == 0
+    assert out.raw[:140] == oracle.marshal([], [key, val])
+    big = (ctypes.c_uint64 * 2)(10, 5000)  # a record over max_bytes
+    assert L.sym_batcher_encode_one(h, None, f, big, 0, 0, out, 200, ctypes.byref(n)) == _native.SYM_ERR_INVALID
+    # a decoded field longer than its cap: SYM_ERR_CAPACITY, the bytes that fit copied
+    rec = oracle.marshal([], [key, val])
+    kb, vb = ctypes.create_string_buffer(16), ctypes.create_string_buffer(16)
+    outs = (ctypes.c_void_p * 2)(ctypes.addressof(kb), ctypes.addressof(vb))
+    caps = (ctypes.c_uint64 * 2)(16, 16)
+    got = (ctypes.c_uint64 * 2)()
+    st = ctypes.c_uint8()
+    assert L.sym_batcher_decode_one(h, rec, len(rec), None, outs, caps, got, ctypes.byref(st)) == _native.SYM_ERR_CAPACITY
+    assert list(got) == [10, 100] and kb.raw[:10] == key and vb.raw == val[:16]
+    L.sym_batcher_destroy(h)
