@@ -9,15 +9,17 @@
 // which saves two thread hand-offs per batch:
 //
 //   caller:  lock; append the record to slot[fill] (pinned, mapped); then, until the slot is DONE:
-//            if no batch of this queue is on the GPU and the slot is still the open one, LEAD it:
-//              wait (up to max_wait_us from the slot's first record, or until it is full) for more
-//              records; point fill at a free slot (later callers append there); unlock; launch the
-//              kernel on the slot in place; synchronise; lock; mark it DONE; wake its callers and
-//              one caller of the new open slot (the next leader)
+//            if no other caller is launching a batch of this queue and the slot is still the open
+//              one, LEAD it: wait (up to max_wait_us from the slot's first record, or until it is
+//              full) for more records; point fill at a free slot (later callers append there);
+//              unlock; launch the kernel on the slot in place and record the slot's event; hand the
+//              queue to one caller of the new open slot (the next leader, whose launch then queues
+//              behind this one on the stream); wait for the event; mark the slot DONE; wake its
+//              callers
 //            else sleep on the slot's condition variable
 //            copy its own result out of the slot; the last reader frees the slot
 //
-// Three slots per queue: one filling, one on the GPU, one draining (callers copying out).  The
+// Four slots per queue: one filling, up to two on the GPU, one draining (callers copying out).  The
 // kernels read their inputs from and write their outputs to the pinned slot directly (host memory
 // allocated with hipHostMalloc is mapped into the device's address space), so a batch is one
 // launch plus one hipStreamSynchronize and no copies.  The encode and decode queues each own a
@@ -41,7 +43,7 @@ using symhip::Layout;
 namespace {
 
 using Clock = std::chrono::steady_clock;
-constexpr int kBSlots = 3;
+constexpr int kBSlots = 4;
 enum SlotState { kFree = 0, kClosed = 1, kRunning = 2, kDone = 3 };
 
 struct BSlot {
@@ -62,6 +64,7 @@ struct BSlot {
     int rc = SYM_OK;
     char msg[256] = "";
     Clock::time_point first;
+    hipEvent_t ev = nullptr;     // the slot's batch has finished on the GPU
     std::condition_variable cv;  // the slot's callers: DONE, or "lead me"
 };
 
@@ -72,7 +75,7 @@ struct Queue {
     std::condition_variable cv_space;  // callers waiting for room / a leader waiting for a free slot
     BSlot slot[kBSlots];
     int fill = 0;
-    bool busy = false;  // a leader owns the queue (waiting for records or running a batch)
+    bool busy = false;  // a leader owns the queue (waiting for records or launching a batch)
     uint64_t batches = 0, records = 0;
 };
 
@@ -136,8 +139,8 @@ void slot_reset(BSlot& s, int nvar) {
     for (int f = 0; f < nvar; ++f) s.offs[f][0] = 0;
 }
 
-// One batch on the GPU, in place in its pinned slot.
-int run_batch(sym_batcher* b, int dir, BSlot& s) {
+// One batch on the GPU, in place in its pinned slot; the slot's event marks its end.
+int launch_batch(sym_batcher* b, int dir, BSlot& s) {
     Queue& q = b->q[dir];
     DeviceGuard g(b->device);
     if (g.err != hipSuccess) return hip_fail(g.err, "sym_batcher: hipSetDevice");
@@ -155,8 +158,8 @@ int run_batch(sym_batcher* b, int dir, BSlot& s) {
     if (rc != SYM_OK) return rc;
     // The kernels cannot raise device error bits here: a batch's record bytes are bounded by
     // max_bytes (< 2 GiB per tile) and every decode column's capacity is the batch's stream size.
-    hipError_t e = hipStreamSynchronize(q.stream);
-    return e == hipSuccess ? SYM_OK : hip_fail(e, "sym_batcher: hipStreamSynchronize");
+    hipError_t e = hipEventRecord(s.ev, q.stream);
+    return e == hipSuccess ? SYM_OK : hip_fail(e, "sym_batcher: hipEventRecord");
 }
 
 // The calling thread runs the open batch of queue `dir` (q.busy set by the caller).  Entered and
@@ -181,7 +184,16 @@ void lead(sym_batcher* b, int dir, std::unique_lock<std::mutex>& lk) {
     s.state = kRunning;
     q.cv_space.notify_all();
     lk.unlock();
-    const int rc = run_batch(b, dir, s);
+    int rc = launch_batch(b, dir, s);
+    lk.lock();
+    q.busy = false;  // the next batch may launch now (it queues behind this one on the stream)
+    q.slot[q.fill].cv.notify_one();
+    lk.unlock();
+    if (rc == SYM_OK) {
+        DeviceGuard g(b->device);
+        const hipError_t e = hipEventSynchronize(s.ev);
+        if (e != hipSuccess) rc = hip_fail(e, "sym_batcher: hipEventSynchronize");
+    }
     char msg[256] = "";
     if (rc != SYM_OK) snprintf(msg, sizeof(msg), "%s", sym_last_error());
     lk.lock();
@@ -191,9 +203,7 @@ void lead(sym_batcher* b, int dir, std::unique_lock<std::mutex>& lk) {
     s.state = kDone;
     ++q.batches;
     q.records += s.n;
-    q.busy = false;
     s.cv.notify_all();
-    q.slot[q.fill].cv.notify_one();  // a caller of the open batch becomes the next leader
 }
 
 // Append under q.mu: wait for room in the open slot (closing a full one), return it.
@@ -237,8 +247,10 @@ void release(Queue& q, std::unique_lock<std::mutex>& lk, BSlot& s) {
 
 void destroy_queue(Queue& q) {
     if (q.stream) (void)hipStreamDestroy(q.stream);
-    for (BSlot& s : q.slot)
+    for (BSlot& s : q.slot) {
         if (s.pin) (void)hipHostFree(s.pin);
+        if (s.ev) (void)hipEventDestroy(s.ev);
+    }
     if (q.ctx) (void)sym_ctx_destroy(q.ctx);
 }
 
@@ -274,7 +286,11 @@ int sym_batcher_create(int device, int schema, uint32_t max_records, uint64_t ma
             break;
         }
         if (dir == 1 && (rc = sym_ctx_reserve(q.ctx, b->R)) != SYM_OK) break;
-        for (int k = 0; k < kBSlots && rc == SYM_OK; ++k) rc = slot_alloc(b, dir, q.slot[k]);
+        for (int k = 0; k < kBSlots && rc == SYM_OK; ++k) {
+            rc = slot_alloc(b, dir, q.slot[k]);
+            if (rc == SYM_OK && (e = hipEventCreateWithFlags(&q.slot[k].ev, hipEventDisableTiming)) != hipSuccess)
+                rc = hip_fail(e, "sym_batcher_create: event");
+        }
         if (rc != SYM_OK) break;
         for (BSlot& s : q.slot) slot_reset(s, b->lay.nvar);
     }

@@ -164,6 +164,8 @@ struct GatherArgs {
 };
 }  // namespace raw
 hipError_t launch_tile_scan(const raw::Pair* agg, raw::Pair* pre, uint64_t ntiles, hipStream_t stream);
+hipError_t launch_tile_scan_gated(const raw::Pair* agg, raw::Pair* pre, uint64_t ntiles, const unsigned* gate,
+                                  hipStream_t stream);
 hipError_t launch_segment_gather(const raw::GatherArgs& a, hipStream_t stream);
 
 // ---- any flat schema (flat.hip); sym_field is defined in include/symphony_hip.h

@@ -138,7 +138,9 @@ __global__ __launch_bounds__(256) void firewall_mark_kernel(const uint8_t* in, c
 
 // ---- exclusive scan of the tile totals (one workgroup; pre[ntiles] = grand total).  Each thread
 // takes 4 consecutive tiles, so up to 4096 tiles (2^20 records) take one block-wide scan.
-__global__ __launch_bounds__(1024) void tile_scan_kernel(const Pair* agg, Pair* pre, u64 ntiles) {
+__global__ __launch_bounds__(1024) void tile_scan_kernel(const Pair* agg, Pair* pre, u64 ntiles,
+                                                        const unsigned* gate = nullptr) {
+    if (gate && *gate == 0) return;  // a gated launch (reassembly's general path) with nothing to do
     constexpr int kPer = 4;
     __shared__ u64 wb[16], wc[16];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -200,6 +202,7 @@ __global__ __launch_bounds__(kWaves * 64) void gather_kernel(GatherArgs a) {
     const u64 ntiles = (a.n + 255) / 256;    // of the tile scan (a.n bounds the segment count)
     const u64 n = a.n_ptr ? *a.n_ptr : a.n;  // segments
     const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
+    if ((u64)blockIdx.x * 256 >= n && blockIdx.x > 0) return;  // a tile past the segments writes nothing
     mask_table_init(masks, threadIdx.x);
 
     // ---- phase 1 (thread = record): length, keep flag, in-tile exclusive scan
@@ -350,7 +353,13 @@ size_t raw_bytes_ws_bytes(u64 n) { return tile_ws(n) + 2 * raw::al256(n * sizeof
 size_t firewall_ws_bytes(u64 n) { return tile_ws(n); }
 
 hipError_t launch_tile_scan(const raw::Pair* agg, raw::Pair* pre, u64 ntiles, hipStream_t stream) {
-    hipLaunchKernelGGL(raw::tile_scan_kernel, dim3(1), dim3(1024), 0, stream, agg, pre, ntiles);
+    hipLaunchKernelGGL(raw::tile_scan_kernel, dim3(1), dim3(1024), 0, stream, agg, pre, ntiles, nullptr);
+    return hipGetLastError();
+}
+
+hipError_t launch_tile_scan_gated(const raw::Pair* agg, raw::Pair* pre, u64 ntiles, const unsigned* gate,
+                                  hipStream_t stream) {
+    hipLaunchKernelGGL(raw::tile_scan_kernel, dim3(1), dim3(1024), 0, stream, agg, pre, ntiles, gate);
     return hipGetLastError();
 }
 
@@ -361,7 +370,7 @@ hipError_t launch_segment_gather(const raw::GatherArgs& a, hipStream_t stream) {
 
 static hipError_t scan_and_gather(raw::GatherArgs& a, bool fw, raw::Pair* agg, raw::Pair* pre, hipStream_t stream) {
     const u64 nt = raw::tiles_of(a.n);
-    hipLaunchKernelGGL(raw::tile_scan_kernel, dim3(1), dim3(1024), 0, stream, agg, pre, nt);
+    hipLaunchKernelGGL(raw::tile_scan_kernel, dim3(1), dim3(1024), 0, stream, agg, pre, nt, nullptr);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     a.pre = pre;

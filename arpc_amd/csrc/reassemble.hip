@@ -12,8 +12,8 @@
 //     hash table (agent-scope CAS) that also keeps each RPCID's first arrival (atomicMin); that
 //     first arrival index is the group key, so groups sort in order of first appearance and an
 //     in-order stream keeps its arrival order through every later pass (coalesced);
-//  2. a stable radix sort (rocPRIM) of (group key, arrival index) on ~log2(n)+1 key bits:
-//     each group becomes a contiguous run in arrival order;
+//  2. a stable LSD radix sort of (group key, arrival index) on ~log2(n)+1 key bits, 8 bits a pass
+//     (sort_*_kernel below): each group becomes a contiguous run in arrival order;
 //  3. group pass (thread per group): the ProcessFragment state machine over the group's run, with
 //     per-sequence state (fragment-index bitmap, last index, latest index-0 fragment) in a scratch
 //     slice owned by the group, O(1) work per datagram; it records, at each completing datagram,
@@ -24,13 +24,16 @@
 //  5. the group pass again, now writing message offsets / RPCIDs / completing datagrams and the
 //     message's payload segments (wire offset, length) in (seq, fragment index) order;
 //  6. the segment gather of raw_fields.hip copies the payloads into the message stream.
-#include <cstring>  // rocprim/iterator/texture_cache_iterator.hpp uses memset
-
-#include <rocprim/device/device_radix_sort.hpp>
+// Most batches are "simple" (every DataPacket one whole message) and finish after step 1 with a
+// scan, an emit and the gather.  The call never waits on the host: steps 1a-6 are queued for every
+// batch and each of their kernels reads the parse's device flag first and exits at once for a
+// simple batch (the stream stays asynchronous and capturable).
 
 #include "../../include/symphony_hip.h"
 #include "codec.hpp"
 #include "device_util.hpp"
+
+#include <algorithm>
 
 namespace symhip {
 
@@ -92,6 +95,144 @@ struct Args {
 };
 
 __device__ inline void block_scan_pair(Pair v, Pair& excl, Pair& tile_total);
+
+// The general path's kernels run only when the parse flagged the batch as not simple (uniform).
+__device__ __forceinline__ bool gated_off(const unsigned* gate) { return *gate == 0; }
+
+// ---- 1a'. the hash table and first-arrival slots set to "empty" (general path only)
+__global__ __launch_bounds__(256) void init_kernel(u64* table, u32* first, u64 ts, const unsigned* gate) {
+    if (gated_off(gate)) return;
+    for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; i <= ts; i += (u64)gridDim.x * 256) {
+        if (i < ts) table[i] = kEmpty;
+        first[i] = ~0u;
+    }
+}
+
+// ---- 2. stable LSD radix sort of (key, value) u32 pairs, 8 key bits per pass, 2048 pairs a tile.
+// A pass: per-tile digit counts (digit-major, so a row scan per digit gives every tile its offset
+// inside the digit), the row scans, then the scatter: a tile's pairs in order -- wave w takes its
+// 512, eight steps of 64 -- ranked among equal digits by a ballot match inside the wave and a
+// running per-wave count in LDS, then offset by the earlier waves' counts, the tile's offset and
+// the digit's start.  Every kernel is gated (general path only).
+constexpr int kSortTile = 2048;
+constexpr int kSortWaveItems = kSortTile / 4;
+constexpr int kDigits = 256;
+
+// lanes of the wave whose digit equals this lane's (among lanes with `valid`)
+__device__ __forceinline__ u64 match_digit(u32 d, bool valid) {
+    u64 m = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        const u64 bal = __ballot(valid && ((d >> b) & 1u));
+        m &= ((d >> b) & 1u) ? bal : ~bal;
+    }
+    return m;
+}
+
+__device__ __forceinline__ u32 rank_below(u64 m) {
+    return __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u));
+}
+
+__global__ __launch_bounds__(256) void sort_hist_kernel(const u32* keys, u64 n, int shift, u32* hist, u64 ntiles,
+                                                        const unsigned* gate) {
+    if (gated_off(gate)) return;
+    __shared__ u32 h[kDigits];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const u64 base = (u64)blockIdx.x * kSortTile;
+    for (int k = 0; k < kSortTile / 256; ++k) {
+        const u64 j = base + (u64)k * 256 + threadIdx.x;
+        const bool valid = j < n;
+        const u32 d = valid ? (keys[j] >> shift) & (kDigits - 1) : 0u;
+        const u64 m = match_digit(d, valid);
+        if (valid && rank_below(m) == 0) atomicAdd(&h[d], (u32)__popcll(m));  // one add per digit and wave
+    }
+    __syncthreads();
+    hist[(u64)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
+}
+
+// block-wide exclusive scan of one u32 per thread (256 threads)
+__device__ __forceinline__ u32 block_excl_u32(u32 v, u32& total) {
+    __shared__ u32 ws[4];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const u32 inc = wave_incl_scan_u32(v, lane);
+    if (lane == 63) ws[wave] = inc;
+    __syncthreads();
+    u32 pre = 0;
+    for (int q = 0; q < wave; ++q) pre += ws[q];
+    total = ws[0] + ws[1] + ws[2] + ws[3];
+    __syncthreads();
+    return pre + inc - v;
+}
+
+__global__ __launch_bounds__(256) void sort_rowscan_kernel(u32* hist, u64 ntiles, u32* rowtot, const unsigned* gate) {
+    if (gated_off(gate)) return;
+    u32* row = hist + (u64)blockIdx.x * ntiles;
+    u32 carry = 0;
+    for (u64 b = 0; b < ntiles; b += 256) {  // uniform loop
+        const u64 i = b + threadIdx.x;
+        const u32 v = i < ntiles ? row[i] : 0u;
+        u32 tot;
+        const u32 ex = block_excl_u32(v, tot);
+        if (i < ntiles) row[i] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) rowtot[blockIdx.x] = carry;
+}
+
+__global__ __launch_bounds__(256) void sort_scatter_kernel(const u32* kin, const u32* vin, u32* kout, u32* vout, u64 n,
+                                                           int shift, const u32* hist, u64 ntiles, const u32* rowtot,
+                                                           const unsigned* gate) {
+    if (gated_off(gate)) return;
+    __shared__ u32 cnt[4][kDigits];  // per wave: running count of each digit, then its output base
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    u32 tot;
+    const u32 dstart = block_excl_u32(rowtot[threadIdx.x], tot);  // the digit's first output position
+    const u32 tbase = dstart + hist[(u64)threadIdx.x * ntiles + blockIdx.x];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) cnt[w][threadIdx.x] = 0;
+    __syncthreads();
+    constexpr int kSteps = kSortWaveItems / 64;
+    u32 key[kSteps], val[kSteps], pos[kSteps];
+    const u64 base = (u64)blockIdx.x * kSortTile + (u64)wave * kSortWaveItems;
+#pragma unroll
+    for (int k = 0; k < kSteps; ++k) {
+        const u64 j = base + (u64)k * 64 + lane;
+        const bool valid = j < n;
+        key[k] = valid ? kin[j] : 0u;
+        val[k] = valid ? vin[j] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < kSteps; ++k) {  // in order: the rank is stable
+        const bool valid = base + (u64)k * 64 + lane < n;
+        const u32 d = (key[k] >> shift) & (kDigits - 1);
+        const u64 m = match_digit(d, valid);
+        const u32 r = rank_below(m);
+        pos[k] = valid ? cnt[wave][d] + r : 0u;
+        wave_sync();  // every lane has read its digit's count before the leaders advance it
+        if (valid && r == 0) cnt[wave][d] += (u32)__popcll(m);
+        wave_sync();
+    }
+    __syncthreads();
+    {  // per digit: the waves' counts -> their output bases
+        const int d = threadIdx.x;
+        u32 b = tbase;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const u32 c = cnt[w][d];
+            cnt[w][d] = b;
+            b += c;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kSteps; ++k) {
+        if (base + (u64)k * 64 + lane >= n) continue;
+        const u32 at = cnt[wave][(key[k] >> shift) & (kDigits - 1)] + pos[k];
+        kout[at] = key[k];
+        vout[at] = val[k];
+    }
+}
 
 // ---- 1. parse (transport.go:266-283, builtin_packets.go:118-161): status, RPCID, meta, payload
 // length, and whether the batch is "simple" -- every DataPacket a whole message in one datagram
@@ -168,7 +309,8 @@ __global__ __launch_bounds__(256) void parse_kernel(Args a, unsigned* complex_fl
 // also keeps each RPCID's first arrival (atomicMin); that first arrival index is the group key,
 // so groups sort in order of first appearance and an in-order stream keeps its arrival order
 // through every later pass (coalesced).  The per-arrival triples are recomputed by group pass 0.
-__global__ __launch_bounds__(256) void hash_kernel(Args a) {
+__global__ __launch_bounds__(256) void hash_kernel(Args a, const unsigned* gate) {
+    if (gated_off(gate)) return;
     const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
     if (i >= a.n) return;
     a.cnt[i] = Pair{0, 0};
@@ -226,7 +368,8 @@ __global__ __launch_bounds__(256) void emit_simple_kernel(Args a, const Pair* tp
 
 // ---- 1b. group key = the RPCID's first arrival: groups sort in order of first appearance, so an
 // in-order stream keeps its arrival order and every later pass reads and writes it coalesced
-__global__ __launch_bounds__(256) void key_kernel(Args a) {
+__global__ __launch_bounds__(256) void key_kernel(Args a, const unsigned* gate) {
+    if (gated_off(gate)) return;
     const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
     if (i >= a.n) return;
     const u32 s = a.slot[i];
@@ -248,7 +391,8 @@ __device__ inline bool seq_complete(const SeqState& x) {
 
 // ---- 3 / 5. the ProcessFragment state machine over one group's run (fragmentation.go:62-181)
 template <int PASS>
-__global__ __launch_bounds__(256) void group_kernel(Args a) {
+__global__ __launch_bounds__(256) void group_kernel(Args a, const unsigned* gate) {
+    if (gated_off(gate)) return;
     const u64 q0 = (u64)blockIdx.x * 256 + threadIdx.x;
     if (q0 >= a.n) return;
     const u32 g = a.gs[q0];
@@ -351,14 +495,17 @@ __device__ inline void block_scan_pair(Pair v, Pair& excl, Pair& tile_total) {
     tile_total = Pair{wb[0] + wb[1] + wb[2] + wb[3], wc[0] + wc[1] + wc[2] + wc[3]};
 }
 
-__global__ __launch_bounds__(256) void pair_tile_total_kernel(const Pair* v, u64 m, Pair* agg) {
+__global__ __launch_bounds__(256) void pair_tile_total_kernel(const Pair* v, u64 m, Pair* agg, const unsigned* gate) {
+    if (gated_off(gate)) return;
     const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
     Pair e, t;
     block_scan_pair(i < m ? v[i] : Pair{0, 0}, e, t);
     if (threadIdx.x == 0) agg[blockIdx.x] = t;
 }
 
-__global__ __launch_bounds__(256) void pair_scan_apply_kernel(const Pair* v, u64 m, const Pair* tpre, Pair* out) {
+__global__ __launch_bounds__(256) void pair_scan_apply_kernel(const Pair* v, u64 m, const Pair* tpre, Pair* out,
+                                                              const unsigned* gate) {
+    if (gated_off(gate)) return;
     const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
     Pair e, t;
     block_scan_pair(i < m ? v[i] : Pair{0, 0}, e, t);
@@ -367,7 +514,8 @@ __global__ __launch_bounds__(256) void pair_scan_apply_kernel(const Pair* v, u64
 }
 
 // message count, closing offset and segment count from the grand total
-__global__ void finalize_kernel(const Pair* total, u64* msg_off, u64* nmsg, u64* nseg) {
+__global__ void finalize_kernel(const Pair* total, u64* msg_off, u64* nmsg, u64* nseg, const unsigned* gate) {
+    if (gated_off(gate)) return;
     const Pair t = *total;
     const u64 nm = t.count & 0xffffffffull;
     *nmsg = nm;
@@ -376,7 +524,9 @@ __global__ void finalize_kernel(const Pair* total, u64* msg_off, u64* nmsg, u64*
 }
 
 // ---- 6. tile totals of the segment lengths (segment count on the device)
-__global__ __launch_bounds__(256) void seg_tile_total_kernel(const u64* seg_len, const u64* nseg, Pair* agg) {
+__global__ __launch_bounds__(256) void seg_tile_total_kernel(const u64* seg_len, const u64* nseg, Pair* agg,
+                                                             const unsigned* gate) {
+    if (gate && gated_off(gate)) return;
     const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
     Pair e, t;
     block_scan_pair(Pair{i < *nseg ? seg_len[i] : 0, 0}, e, t);
@@ -399,9 +549,10 @@ inline unsigned key_bits(u64 n) { return log2u(n + 1) + 1; }  // keys in [0, n]
 
 struct Layout {
     size_t table, first, slot, rpc, meta, plen, gid, idx, gs, is, state, cnt, pre, agg, tpre, seg_src, seg_len, agg2,
-        pre2, nseg, flag, temp, total;
-    size_t temp_bytes;
+        pre2, nseg, nseg2, flag, hist, rowtot, total;
 };
+
+inline u64 sort_tiles(u64 n) { return (n + kSortTile - 1) / kSortTile; }
 
 inline Layout layout(u64 n) {
     Layout L{};
@@ -432,12 +583,10 @@ inline Layout layout(u64 n) {
     L.agg2 = take((tiles(n) + 1) * sizeof(Pair));
     L.pre2 = take((tiles(n) + 1) * sizeof(Pair));
     L.nseg = take(8);
-    L.flag = take(4);
-    size_t tb = 0;
-    (void)rocprim::radix_sort_pairs(nullptr, tb, (const u32*)nullptr, (u32*)nullptr, (const u32*)nullptr,
-                                    (u32*)nullptr, (size_t)n, 0u, key_bits(n));
-    L.temp_bytes = al256(tb);
-    L.temp = take(L.temp_bytes);
+    L.nseg2 = take(16);  // the general path's segment count, then the parse's flag: zeroed together
+    L.flag = L.nseg2 + 8;
+    L.hist = take((size_t)kDigits * sort_tiles(n) * 4);
+    L.rowtot = take(kDigits * 4);
     L.total = o;
     return L;
 }
@@ -468,8 +617,6 @@ hipError_t launch_reassemble(const uint8_t* wire, const u64* dg_off, u64 n, uint
     a.plen = (u32*)(w + L.plen);
     a.gid = (u32*)(w + L.gid);
     a.idx = (u32*)(w + L.idx);
-    a.gs = (const u32*)(w + L.gs);
-    a.is = (const u32*)(w + L.is);
     a.state = (rx::SeqState*)(w + L.state);
     a.status = status;
     a.cnt = (Pair*)(w + L.cnt);
@@ -480,20 +627,21 @@ hipError_t launch_reassemble(const uint8_t* wire, const u64* dg_off, u64 n, uint
     a.seg_src = (u64*)(w + L.seg_src);
     a.seg_len = (u64*)(w + L.seg_len);
     const dim3 b256(256);
-    unsigned* flag = (unsigned*)(w + L.flag);
+    const unsigned* flag = (const unsigned*)(w + L.flag);
     const dim3 gq((unsigned)rx::tiles(n));
     const u64 nt = rx::tiles(n + 1), ns = rx::tiles(n);
     Pair* agg = (Pair*)(w + L.agg);
     Pair* tpre = (Pair*)(w + L.tpre);
-    u64* nseg = (u64*)(w + L.nseg);
     a.agg = agg;
-    auto seg_tail = [&]() -> hipError_t {  // the payload segments' tile prefixes, then the gather
+    // the payload segments' tile prefixes, then the gather (segment count on the device); gate:
+    // the general path's copy, which does nothing for a simple batch
+    auto seg_tail = [&](u64* nseg, const unsigned* gate) -> hipError_t {
         Pair* agg2 = (Pair*)(w + L.agg2);
         Pair* pre2 = (Pair*)(w + L.pre2);
         hipLaunchKernelGGL(rx::seg_tile_total_kernel, dim3((unsigned)ns), b256, 0, stream, (const u64*)a.seg_len,
-                           (const u64*)nseg, agg2);
+                           (const u64*)nseg, agg2, gate);
         hipError_t r = hipGetLastError();
-        if (r == hipSuccess) r = launch_tile_scan(agg2, pre2, ns, stream);
+        if (r == hipSuccess) r = launch_tile_scan_gated(agg2, pre2, ns, gate, stream);
         if (r != hipSuccess) return r;
         raw::GatherArgs ga{};
         ga.in = wire;
@@ -509,49 +657,64 @@ hipError_t launch_reassemble(const uint8_t* wire, const u64* dg_off, u64 n, uint
         ga.err = err;
         return launch_segment_gather(ga, stream);
     };
-    // Simple batches (every DataPacket one whole message) complete on the device without a host
-    // decision: parse (with the tile totals of the per-arrival triples), their scan, the messages,
-    // the gather.  Queued for every batch; for the others the emit writes no message and zero
-    // segments, so the gather after it is empty.
-    hipError_t e = hipMemsetAsync(flag, 0, sizeof(unsigned), stream);
+    // Simple batches (every DataPacket one whole message) complete here: parse (with the tile
+    // totals of the per-arrival triples), their scan, the messages, the gather.  For other batches
+    // the emit writes no message and zero segments, so this gather is empty.
+    u64* nseg = (u64*)(w + L.nseg);
+    u64* nseg2 = (u64*)(w + L.nseg2);
+    hipError_t e = hipMemsetAsync(w + L.nseg2, 0, 16, stream);  // nseg2 and the flag
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(rx::parse_kernel, dim3((unsigned)nt), b256, 0, stream, a, flag);
+    hipLaunchKernelGGL(rx::parse_kernel, dim3((unsigned)nt), b256, 0, stream, a, (unsigned*)flag);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = launch_tile_scan(agg, tpre, nt, stream)) != hipSuccess) return e;
-    hipLaunchKernelGGL(rx::emit_simple_kernel, dim3((unsigned)nt), b256, 0, stream, a, (const Pair*)tpre,
-                       (const unsigned*)flag, nmsg, nseg);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    if ((e = seg_tail()) != hipSuccess) return e;
-    // the one host read of the call: whether the general path has to run
-    unsigned complex_batch = 1;
-    if ((e = hipMemcpyAsync(&complex_batch, flag, sizeof(unsigned), hipMemcpyDeviceToHost, stream)) != hipSuccess)
-        return e;
-    if ((e = hipStreamSynchronize(stream)) != hipSuccess) return e;
-    if (!complex_batch) return hipSuccess;
-    if ((e = hipMemsetAsync(a.table, 0xff, TS * 8, stream)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(a.first, 0xff, (TS + 1) * 4, stream)) != hipSuccess) return e;
-    hipLaunchKernelGGL(rx::hash_kernel, gq, b256, 0, stream, a);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(rx::key_kernel, gq, b256, 0, stream, a);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    size_t tb = L.temp_bytes;
-    e = rocprim::radix_sort_pairs(w + L.temp, tb, (const u32*)a.gid, (u32*)(w + L.gs), (const u32*)a.idx,
-                                  (u32*)(w + L.is), (size_t)n, 0u, rx::key_bits(n), stream);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(rx::group_kernel<0>, gq, b256, 0, stream, a);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(rx::pair_tile_total_kernel, dim3((unsigned)nt), b256, 0, stream, (const Pair*)a.cnt, n + 1, agg);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    if ((e = launch_tile_scan(agg, tpre, nt, stream)) != hipSuccess) return e;
-    hipLaunchKernelGGL(rx::pair_scan_apply_kernel, dim3((unsigned)nt), b256, 0, stream, (const Pair*)a.cnt, n + 1,
-                       (const Pair*)tpre, (Pair*)(w + L.pre));
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(rx::finalize_kernel, dim3(1), dim3(1), 0, stream, (const Pair*)(w + L.pre) + n, msg_off, nmsg,
+    hipLaunchKernelGGL(rx::emit_simple_kernel, dim3((unsigned)nt), b256, 0, stream, a, (const Pair*)tpre, flag, nmsg,
                        nseg);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(rx::group_kernel<1>, gq, b256, 0, stream, a);
+    if ((e = seg_tail(nseg, nullptr)) != hipSuccess) return e;
+    // The general path, queued for every batch; each kernel exits at once unless the parse set the
+    // flag (no host read, the stream stays asynchronous).
+    hipLaunchKernelGGL(rx::init_kernel, dim3((unsigned)std::min<u64>(rx::tiles(TS + 1), 4096)), b256, 0, stream, a.table,
+                       a.first, TS, flag);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    return seg_tail();
+    hipLaunchKernelGGL(rx::hash_kernel, gq, b256, 0, stream, a, flag);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(rx::key_kernel, gq, b256, 0, stream, a, flag);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    {  // 2. the stable radix sort, ping-ponging between (gid, idx) and (gs, is)
+        u32* kb[2] = {a.gid, (u32*)(w + L.gs)};
+        u32* vb[2] = {a.idx, (u32*)(w + L.is)};
+        const u64 st = rx::sort_tiles(n);
+        u32* hist = (u32*)(w + L.hist);
+        u32* rowtot = (u32*)(w + L.rowtot);
+        const unsigned bits = rx::key_bits(n);
+        int cur = 0;
+        for (unsigned shift = 0; shift < bits; shift += 8, cur ^= 1) {
+            hipLaunchKernelGGL(rx::sort_hist_kernel, dim3((unsigned)st), b256, 0, stream, (const u32*)kb[cur], n,
+                               (int)shift, hist, st, flag);
+            hipLaunchKernelGGL(rx::sort_rowscan_kernel, dim3(rx::kDigits), b256, 0, stream, hist, st, rowtot, flag);
+            hipLaunchKernelGGL(rx::sort_scatter_kernel, dim3((unsigned)st), b256, 0, stream, (const u32*)kb[cur],
+                               (const u32*)vb[cur], kb[cur ^ 1], vb[cur ^ 1], n, (int)shift, (const u32*)hist, st,
+                               (const u32*)rowtot, flag);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+        }
+        a.gs = kb[cur];
+        a.is = vb[cur];
+    }
+    hipLaunchKernelGGL(rx::group_kernel<0>, gq, b256, 0, stream, a, flag);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(rx::pair_tile_total_kernel, dim3((unsigned)nt), b256, 0, stream, (const Pair*)a.cnt, n + 1, agg,
+                       flag);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = launch_tile_scan_gated(agg, tpre, nt, flag, stream)) != hipSuccess) return e;
+    hipLaunchKernelGGL(rx::pair_scan_apply_kernel, dim3((unsigned)nt), b256, 0, stream, (const Pair*)a.cnt, n + 1,
+                       (const Pair*)tpre, (Pair*)(w + L.pre), flag);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(rx::finalize_kernel, dim3(1), dim3(1), 0, stream, (const Pair*)(w + L.pre) + n, msg_off, nmsg,
+                       nseg2, flag);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(rx::group_kernel<1>, gq, b256, 0, stream, a, flag);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    return seg_tail(nseg2, flag);
 }
 
 }  // namespace symhip

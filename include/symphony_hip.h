@@ -337,9 +337,9 @@ int sym_firewall_filter(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec
  * datagram: its header carries the packet type and addresses Receive returns); *d_nmsg; all
  * arrays sized for n messages (n+1 offsets).  d_status[n]: SYM_RX_*.  n < 2^31.
  * When every DataPacket is a whole message (TotalPackets 1, one fragment) the messages are the
- * DataPackets in arrival order, found on the device without grouping.  The call then synchronizes
- * `stream` once (after that work) to learn whether the general path -- grouping, sort, the
- * ProcessFragment state machine -- has to run. */
+ * DataPackets in arrival order, found on the device without grouping.  The general path --
+ * grouping, sort, the ProcessFragment state machine -- is queued too and its kernels exit at once
+ * for such a batch: the call is asynchronous on `stream` like the others (no host read). */
 #define SYM_RX_CONSUMED 0   /* part of a returned message */
 #define SYM_RX_PENDING 1    /* still held by the reassembler after the batch */
 #define SYM_RX_NOT_DATA 2   /* not a Request / Response DataPacket: not reassembled */
