@@ -126,12 +126,99 @@ __device__ __forceinline__ int rec_nvar(const DecodeParams& p, u64 r) {
 // the header lines it reads are still cached when that tile's copier stages them.  XCDP: a parser
 // takes only tiles whose copier shares its blockIdx % 8 group (one XCD under round-robin placement),
 // so those lines are in that XCD's L2 (speed only; any placement gives the same results).
-template <int NF, int NV, bool MIX, int R = 2, int WB = 32, bool LIGHT = false, int PACE = 0, bool XCDP = false>
-__device__ void parser(const DecodeParams& p, u64* aw, u64* pw, u64 ntiles, u32 epoch, u32 P) {
+// R tiles th[] by one wave (lane = record): the records' field lengths with Go's checks, then each
+// tile's aggregate word per column.  Every load of the R records is issued before any is used.
+template <int NF, int NV, bool MIX, int R, int WB, bool LIGHT = false>
+__device__ __forceinline__ void parse_tiles(const DecodeParams& p, u64* aw, u64 ntiles, u32 epoch, const u64 (&th)[R]) {
     constexpr int NW = WB / 4;  // window dwords
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
     const u64 n = p.n;
     const uintptr_t in = (uintptr_t)p.in;
+    bool live[R], win[R];
+    u64 start[R], L[R];
+    int nvr[R];
+    u32 w[R][NW];
+#pragma unroll
+    for (int h = 0; h < R; ++h) {
+        const u64 r = th[h] * kRecs + lane;
+        live[h] = th[h] < ntiles && r < n;
+        const u64 rc = live[h] ? r : n;
+        start[h] = p.rec_off[rc];
+        L[h] = p.rec_off[live[h] ? rc + 1 : rc] - start[h];
+        nvr[h] = rec_nvar<NV, MIX>(p, live[h] ? r : 0);
+    }
+#pragma unroll
+    for (int h = 0; h < R; ++h) {
+        win[h] = live[h] && L[h] >= (u64)WB;
+        if constexpr (LIGHT) live[h] = win[h] = false;  // timing: offsets only, no header reads
+        const uintptr_t wa = win[h] ? in + start[h] : (uintptr_t)aw;  // readable filler (>= 256 B)
+#pragma unroll
+        for (int k = 0; k < WB / 16; ++k) {
+            const u32x4 a = ld16u(wa + 16 * k);
+            w[h][4 * k] = a.x;
+            w[h][4 * k + 1] = a.y;
+            w[h][4 * k + 2] = a.z;
+            w[h][4 * k + 3] = a.w;
+        }
+    }
+#pragma unroll
+    for (int h = 0; h < R; ++h) {
+        const uintptr_t A = in + start[h];
+        const bool wh = win[h];
+        const u64 Lh = L[h];
+        auto rd8 = [&](u64 q) -> u32 {
+            constexpr u64 M = WB - 4;
+            return wh && q < (u64)WB ? (win_u32<NW>(w[h], (u32)min(q, M)) >> (8 * (q > M ? q - M : 0))) & 0xffu
+                                     : ld_u8(A + q);
+        };
+        auto rd32 = [&](u64 q) -> u32 {
+            return wh && q + 4 <= (u64)WB ? win_u32<NW>(w[h], (u32)q) : *(gc_u32*)(A + q);  // unaligned OK
+        };
+        u64 flen[NV];
+#pragma unroll
+        for (int f = 0; f < NV; ++f) flen[f] = 0;
+        if (live[h] && Lh >= 13 && rd8(0) == 0x01) {
+            const u64 off2p = rd32(1);
+            if (off2p < Lh && rd8(off2p) == 0x01) {
+                const u64 pts = off2p + 1;
+                const u64 vt = pts + 4 * (u64)NF;  // var table: only if every int32 field fits
+                if (Lh >= vt) {
+#pragma unroll
+                    for (int f = 0; f < NV; ++f) {
+                        const u64 te = vt + 4 * (u64)f;
+                        if (f < nvr[h] && Lh >= te + 4) {
+                            u64 q = rd32(te);
+                            if (q > 0) q += off2p;
+                            if (q > 0 && Lh >= q + 4) {
+                                const u64 nb = rd32(q);
+                                if (Lh >= q + 4 + nb) flen[f] = nb;
+                            }
+                        }
+                    }
+                }
+            }
+        }
+        if (th[h] < ntiles) {
+#pragma unroll
+            for (int f = 0; f < NV; ++f) {
+                const u64 inc = wave_incl_scan_u32w_dpp((u32)flen[f]);
+                const u64 agg = (u64)__builtin_amdgcn_readlane((u32)inc, 63) |
+                                ((u64)__builtin_amdgcn_readlane((u32)(inc >> 32), 63) << 32);
+                if (lane == f) store_word(&aw[(size_t)f * ntiles + th[h]], make_word(epoch, kStAgg, agg));
+            }
+        }
+    }
+}
+
+// PACE > 0: a parser wave starts a step only once tile t0 - PACE has its prefix (bounded wait), so
+// the header lines it reads are still cached when that tile's copier stages them.  XCDP: a parser
+// takes only tiles whose copier shares its blockIdx % 8 group (one XCD under round-robin placement),
+// so those lines are in that XCD's L2 (speed only; any placement gives the same results).  tmax:
+// only tiles below it (the copiers parse the others ahead, AHEAD in decode_pipe_kernel).
+template <int NF, int NV, bool MIX, int R = 2, int WB = 32, bool LIGHT = false, int PACE = 0, bool XCDP = false>
+__device__ void parser(const DecodeParams& p, u64* aw, u64* pw, u64 ntiles, u32 epoch, u32 P, u64 tmax = ~0ull) {
+    const int wave = threadIdx.x >> 6;
+    const u64 tlim = min(ntiles, tmax);
     // tile of (sequence index j, slot h) = tb + ts * (j + h)
     u64 tb = 0, ts = 1, j0 = ((u64)blockIdx.x * 4 + wave) * R, jstep = (u64)P * 4 * R;
     if (XCDP && P % 8 == 0) {
@@ -141,10 +228,13 @@ __device__ void parser(const DecodeParams& p, u64* aw, u64* pw, u64 ntiles, u32 
         j0 = (i * 4 + wave) * R;
         jstep = (u64)(P / 8) * 4 * R;
     }
-    for (u64 j = j0; tb + ts * j < ntiles; j += jstep) {
+    for (u64 j = j0; tb + ts * j < tlim; j += jstep) {
         u64 th[R];
 #pragma unroll
-        for (int h = 0; h < R; ++h) th[h] = tb + ts * (j + h);
+        for (int h = 0; h < R; ++h) {
+            th[h] = tb + ts * (j + h);
+            if (th[h] >= tlim) th[h] = ntiles;  // past the parsers' range: skipped
+        }
         const u64 t0 = th[0];
         if constexpr (PACE > 0) {
             if (t0 >= (u64)PACE) {
@@ -153,80 +243,7 @@ __device__ void parser(const DecodeParams& p, u64* aw, u64* pw, u64 ntiles, u32 
                     __builtin_amdgcn_s_sleep(8);
             }
         }
-        bool live[R], win[R];
-        u64 start[R], L[R];
-        int nvr[R];
-        u32 w[R][NW];
-#pragma unroll
-        for (int h = 0; h < R; ++h) {
-            const u64 r = th[h] * kRecs + lane;
-            live[h] = th[h] < ntiles && r < n;
-            const u64 rc = live[h] ? r : n;
-            start[h] = p.rec_off[rc];
-            L[h] = p.rec_off[live[h] ? rc + 1 : rc] - start[h];
-            nvr[h] = rec_nvar<NV, MIX>(p, live[h] ? r : 0);
-        }
-#pragma unroll
-        for (int h = 0; h < R; ++h) {
-            win[h] = live[h] && L[h] >= (u64)WB;
-            if constexpr (LIGHT) live[h] = win[h] = false;  // timing: offsets only, no header reads
-            const uintptr_t wa = win[h] ? in + start[h] : (uintptr_t)aw;  // readable filler (>= 256 B)
-#pragma unroll
-            for (int k = 0; k < WB / 16; ++k) {
-                const u32x4 a = ld16u(wa + 16 * k);
-                w[h][4 * k] = a.x;
-                w[h][4 * k + 1] = a.y;
-                w[h][4 * k + 2] = a.z;
-                w[h][4 * k + 3] = a.w;
-            }
-        }
-#pragma unroll
-        for (int h = 0; h < R; ++h) {
-            const uintptr_t A = in + start[h];
-            const bool wh = win[h];
-            const u64 Lh = L[h];
-            auto rd8 = [&](u64 q) -> u32 {
-                constexpr u64 M = WB - 4;
-                return wh && q < (u64)WB ? (win_u32<NW>(w[h], (u32)min(q, M)) >> (8 * (q > M ? q - M : 0))) & 0xffu
-                                         : ld_u8(A + q);
-            };
-            auto rd32 = [&](u64 q) -> u32 {
-                return wh && q + 4 <= (u64)WB ? win_u32<NW>(w[h], (u32)q) : *(gc_u32*)(A + q);  // unaligned OK
-            };
-            u64 flen[NV];
-#pragma unroll
-            for (int f = 0; f < NV; ++f) flen[f] = 0;
-            if (live[h] && Lh >= 13 && rd8(0) == 0x01) {
-                const u64 off2p = rd32(1);
-                if (off2p < Lh && rd8(off2p) == 0x01) {
-                    const u64 pts = off2p + 1;
-                    const u64 vt = pts + 4 * (u64)NF;  // var table: only if every int32 field fits
-                    if (Lh >= vt) {
-#pragma unroll
-                        for (int f = 0; f < NV; ++f) {
-                            const u64 te = vt + 4 * (u64)f;
-                            if (f < nvr[h] && Lh >= te + 4) {
-                                u64 q = rd32(te);
-                                if (q > 0) q += off2p;
-                                if (q > 0 && Lh >= q + 4) {
-                                    const u64 nb = rd32(q);
-                                    if (Lh >= q + 4 + nb) flen[f] = nb;
-                                }
-                            }
-                        }
-                    }
-                }
-            }
-            if (th[h] < ntiles) {
-#pragma unroll
-                for (int f = 0; f < NV; ++f) {
-                    const u64 inc = wave_incl_scan_u32w_dpp((u32)flen[f]);
-                    const u64 agg = (u64)__builtin_amdgcn_readlane((u32)inc, 63) |
-                                    ((u64)__builtin_amdgcn_readlane((u32)(inc >> 32), 63) << 32);
-                    if (lane == f) store_word(&aw[(size_t)f * ntiles + th[h]], make_word(epoch, kStAgg, agg));
-                }
-            }
-        }
+        parse_tiles<NF, NV, MIX, R, WB, LIGHT>(p, aw, ntiles, epoch, th);
     }
 }
 
@@ -234,6 +251,8 @@ __device__ void parser(const DecodeParams& p, u64* aw, u64* pw, u64 ntiles, u32 
 // Each step loads the aggregate words of the next 1024 tiles, finds the first tile whose word is not
 // yet published (the frontier), and publishes the exclusive prefix of every tile before it.  A
 // tile's prefix so depends only on earlier tiles, whoever published their aggregates.
+constexpr int kScanPerG = 2;  // the gather copier's scanner: tiles per thread per step
+
 template <int NV, int SK, int NT = kThreads, typename LdsT>
 __device__ void scanner(u64* aw, u64* pw, u64 ntiles, u32 epoch, LdsT& S, u64* dbg = nullptr) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -410,8 +429,12 @@ __device__ void lookback(const DecodeParams& p, u64* aw, u64* pw, u64 ntiles, u6
 // STG: staged bytes per tile (LDS: 24.7 KB at kStage -> 6 copiers per CU; below ~21 KB -> 7).
 // EARLY: the prefix word is loaded when the tile starts, so its cross-XCD round trip overlaps the
 // stage instead of following the parse.  PACE, XCDP: see parser().
+// AHEAD > 0: the parsers take only tiles [0, AHEAD); the copier of tile t parses tile t + AHEAD
+// (wave 1, while wave 0 parses its own tile from LDS) -- the same XCD under round-robin placement
+// when AHEAD % 8 == 0, so the header lines it reads are still in that XCD's L2 when tile t + AHEAD
+// is staged, and the stream is fetched from HBM about once.
 template <int NF, int NV, bool MIX, int MODE = 0, int DIAG = 0, int SK = 4, int PR = 2, int STG = kStage,
-          bool EARLY = false, int PACE = 0, bool XCDP = false>
+          bool EARLY = false, int PACE = 0, bool XCDP = false, int AHEAD = 0>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))) void decode_pipe_kernel(
     DecodeParams p, u64* flags, u32 epoch) {
     static_assert(NV == 1 || NV == 2, "decode handles one or two string columns");
@@ -432,7 +455,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
     // MODE 2 / 3 (timing): roles run, copiers never wait; 3: parsers read only the offsets
     constexpr bool kRoles = MODE == 0 || MODE == 2 || MODE == 3;
     if (kRoles && blockIdx.x < P) {
-        if (!forced) parser<NF, NV, MIX, PR, 32, MODE == 3, PACE, XCDP>(p, aw, pw, ntiles, epoch, P);
+        if (!forced)
+            parser<NF, NV, MIX, PR, 32, MODE == 3, PACE, XCDP>(p, aw, pw, ntiles, epoch, P, AHEAD > 0 ? (u64)AHEAD : ~0ull);
         return;
     }
     if (kRoles && blockIdx.x == P) {
@@ -476,7 +500,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
     lds_barrier();
     stamp(1);
 
-    // ---- 2. parse + 3. prefix (wave 0) ----
+    // ---- 2. parse + 3. prefix (wave 0); with AHEAD, wave 1 parses tile + AHEAD meanwhile ----
+    if constexpr (AHEAD > 0) {
+        if (wave == 1 && !forced && tile + AHEAD < ntiles) {
+            const u64 ta[1] = {tile + AHEAD};
+            parse_tiles<NF, NV, MIX, 1, 32>(p, aw, ntiles, epoch, ta);
+        }
+    }
     if (wave == 0) {
         const bool live = lane < cnt;
         const u64 L = endv - start;
@@ -682,8 +712,303 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
         if (tid == 0) p.dbg[tile * 8 + 5] = blockIdx.x;
 }
 
+// ---------------------------------------------------------------- the gather copier
+// A copier without the LDS stage.  Wave 0 parses its 64 records straight from HBM through a 96-byte
+// register window per record -- the lines the copy reads next, so they are fetched once -- runs Go's
+// checks, publishes the tile's aggregate and takes its prefix as the staged copier does.  Then all
+// four waves write the tile's column ranges output-stationary, as encode_kernel writes records: lane
+// = aligned 16-byte output chunk, assembled from byte-unaligned 16-byte loads of the one or two
+// fields it covers (more only under fields shorter than 16 bytes) under byte masks, one
+// global_store_dwordx4 per chunk (byte stores only at a range's two edges).  kGU chunks per lane per
+// step, every load of the step issued before its stores.  LDS holds only the field tables (~2 KB),
+// so a CU keeps up to 8 copiers resident instead of 6.
+constexpr int kGWin = 96;  // parse window bytes per record
+constexpr int kGU = 4;     // output chunks per lane per step
+
+struct ScanLds {  // the scanner's scratch (scanner() needs red / first)
+    u64 red[4];
+    int first[4];
+};
+
+template <int NV>
+struct GatherLds {
+    u64 addr[NV][kRecs];   // the tile's non-empty fields, compacted: source address
+    int o[NV][kRecs + 1];  // output start inside the tile's column range; [nl] = the range length
+    i64 pre[NV];           // the range's start in the column
+    int hi[NV];            // bytes of the range to write (the capacity may cut it)
+    int nl[NV];
+    int nch[NV];           // output chunks of the range
+    int first[NV];         // the first chunk's start relative to the range, in (-16, 0]
+    int safe;              // every 16-byte window of the tile lies inside the stream's readable extent
+    int skip;              // a range of 2 GiB or more (reported): nothing is written
+};
+
+template <int NF, int NV, bool MIX, int MODE = 0>
+__global__ __launch_bounds__(kThreads) void decode_gather_kernel(DecodeParams p, u64* flags, u32 epoch) {
+    static_assert(NV == 1 || NV == 2, "decode handles one or two string columns");
+    constexpr int NW = kGWin / 4;
+    __shared__ GatherLds<NV> S;
+    __shared__ ScanLds SL;
+    __shared__ MaskTable masks;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const u64 n = p.n, ntiles = num_tiles(n);
+    const uintptr_t in = (uintptr_t)p.in;
+    const uintptr_t in_lo = in + p.rec_off[0];
+    const uintptr_t in_end16 = (in + p.rec_off[n] + 15) & ~(uintptr_t)15;  // readable limit (ABI rule)
+    u64* aw = flags;
+    u64* pw = flags + (size_t)NV * ntiles;
+    const u32 P = p.pipe_parsers;
+    const bool forced = p.impl == kImplLookback;
+    if (blockIdx.x < P) {
+        if (!forced) parser<NF, NV, MIX, 2, 32>(p, aw, pw, ntiles, epoch, P);
+        return;
+    }
+    if (blockIdx.x == P) {
+        if (!forced) scanner<NV, kScanPerG>(aw, pw, ntiles, epoch, SL);
+        return;
+    }
+    const u64 tile = blockIdx.x - P - 1;
+    if (tile >= ntiles) return;
+    mask_table_init(masks, tid);
+    const u64 r0 = tile * kRecs;
+    const int cnt = (int)min((u64)kRecs, n - r0);
+
+    // ---- 1. parse from HBM (wave 0, lane = record), prefix, tables ----
+    if (wave == 0) {
+        const bool live = lane < cnt;
+        const u64 start = p.rec_off[r0 + min(lane, cnt)];
+        const u64 L = p.rec_off[r0 + min(lane + 1, cnt)] - start;
+        const uintptr_t A = in + start;
+        // the window: every 16-byte block that lies inside the readable extent (zero past it)
+        u32 w[NW];
+        const u64 room = in_end16 > A ? (u64)(in_end16 - A) : 0;
+        const int wv = live ? (int)min((u64)kGWin, room) & ~15 : 0;  // window bytes loaded
+#pragma unroll
+        for (int k = 0; k < kGWin / 16; ++k) {
+            const u32x4 a = ld16u(16 * k < wv ? A + 16 * k : (uintptr_t)flags);
+            w[4 * k] = a.x;
+            w[4 * k + 1] = a.y;
+            w[4 * k + 2] = a.z;
+            w[4 * k + 3] = a.w;
+        }
+        auto rd8 = [&](u64 q) -> u32 {
+            constexpr u64 M = kGWin - 4;
+            return q < (u64)wv ? (win_u32<NW>(w, (u32)min(q, M)) >> (8 * (q > M ? q - M : 0))) & 0xffu : ld_u8(A + q);
+        };
+        auto rd32 = [&](u64 q) -> u32 {
+            return q + 4 <= (u64)wv ? win_u32<NW>(w, (u32)q) : *(gc_u32*)(A + q);  // unaligned OK
+        };
+        u32 st = 0;
+        int32_t fx[NF > 0 ? NF : 1] = {};
+        u64 flen[NV], fpos[NV];
+#pragma unroll
+        for (int f = 0; f < NV; ++f) flen[f] = fpos[f] = 0;
+        const int nvr = rec_nvar<NV, MIX>(p, live ? r0 + lane : 0);
+        if (live) {  // kv.syn.go:681-745, echo.syn.go:186-263
+            if (L < 13) {
+                st = SYM_STATUS_TOO_SHORT;
+            } else if (rd8(0) != 0x01) {
+                st = SYM_STATUS_BAD_VERSION;
+            } else {
+                const u64 off2p = rd32(1);
+                if (off2p >= L || rd8(off2p) != 0x01) {
+                    st = SYM_STATUS_NO_PRIVATE;
+                } else {
+                    const u64 pts = off2p + 1;
+                    u64 toff = 0;
+#pragma unroll
+                    for (int f = 0; f < NF; ++f, toff += 4) {
+                        if (st == 0) {
+                            if (L < pts + toff + 4) st = SYM_STATUS_FIELD_TOO_SHORT;
+                            else fx[f] = (int32_t)rd32(pts + toff);
+                        }
+                    }
+                    if (st == 0) {
+#pragma unroll
+                        for (int f = 0; f < NV; ++f, toff += 4) {
+                            if (f < nvr && L >= pts + toff + 4) {
+                                u64 q = rd32(pts + toff);
+                                if (q > 0) q += off2p;
+                                if (q > 0 && L >= q + 4) {
+                                    const u64 nb = rd32(q);
+                                    if (L >= q + 4 + nb) {
+                                        flen[f] = nb;
+                                        fpos[f] = q + 4;
+                                    }
+                                }
+                            }
+                        }
+                    }
+                }
+            }
+            p.status[r0 + lane] = (uint8_t)st;
+#pragma unroll
+            for (int f = 0; f < NF; ++f) p.fixed[f][r0 + lane] = fx[f];
+        }
+        u64 agg[NV], excl[NV];
+        bool too_large = false;
+#pragma unroll
+        for (int f = 0; f < NV; ++f) {
+            const u64 inc = wave_incl_scan_u32w_dpp((u32)flen[f]);
+            agg[f] = (u64)__builtin_amdgcn_readlane((u32)inc, 63) |
+                     ((u64)__builtin_amdgcn_readlane((u32)(inc >> 32), 63) << 32);
+            excl[f] = inc - flen[f];
+            too_large |= agg[f] >= ((u64)1 << 31);  // positions inside a tile's range are 32-bit
+        }
+        // the prefix: from the scanner, else (after kFallbackTicks, or forced) by look-back
+        i64 pre[NV];
+        if constexpr (MODE == 0) {
+            u64 wvv = 0;
+            bool got = true;
+            if (lane < NV) {
+                store_word(&aw[(size_t)lane * ntiles + tile], make_word(epoch, kStAgg, lane == 0 ? agg[0] : agg[NV - 1]));
+                u64* a = &pw[(size_t)lane * ntiles + tile];
+                wvv = load_word(a);
+                if (!forced) {
+                    for (const u64 t0 = now_ticks(); !tagged(wvv, epoch) && now_ticks() - t0 <= kFallbackTicks;) {
+                        __builtin_amdgcn_s_sleep(2);
+                        wvv = load_word(a);
+                    }
+                }
+                got = tagged(wvv, epoch);
+            }
+            if (__ballot(!got)) {
+                lookback<NF, NV, MIX>(p, aw, pw, ntiles, tile, epoch, pre);
+#pragma unroll
+                for (int f = 0; f < NV; ++f)
+                    if (lane == 0) store_word(&pw[(size_t)f * ntiles + tile], make_word(epoch, kStPre, (u64)pre[f]));
+            } else {
+                pre[0] = (i64)((u64)__shfl((long long)wvv, 0, 64) & kValMask);
+                if constexpr (NV == 2) pre[1] = (i64)((u64)__shfl((long long)wvv, 1, 64) & kValMask);
+            }
+        } else {  // timing only (wrong output): every prefix in proportion to the stream offset
+            const double frac = (double)(start - p.rec_off[0]) / (double)(p.rec_off[n] - p.rec_off[0] + 1);
+#pragma unroll
+            for (int f = 0; f < NV; ++f) pre[f] = uniform_i64((i64)(__shfl(frac, 0, 64) * (double)p.cap[f]));
+        }
+#pragma unroll
+        for (int f = 0; f < NV; ++f) {
+            if (live) p.offs[f][r0 + lane] = (u64)pre[f] + excl[f];
+            if (lane == 0 && r0 + cnt == n) p.offs[f][n] = (u64)pre[f] + agg[f];
+        }
+        // the tables: non-empty fields compacted, each with its source and its output start
+        bool safe = true;
+#pragma unroll
+        for (int f = 0; f < NV; ++f) {
+            const bool ne = live && flen[f] > 0;
+            const u64 m = __ballot(ne);
+            const int slot = (int)__builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u));
+            const uintptr_t src = A + fpos[f];
+            if (ne) {
+                S.addr[f][slot] = (u64)src;
+                S.o[f][slot] = (int)excl[f];
+                safe = safe && src >= in_lo + 16 && src + flen[f] + 16 <= in_end16 - 16;
+            }
+            if (lane == 0) {
+                const int nl = (int)__popcll(m);
+                S.o[f][nl] = (int)agg[f];
+                S.nl[f] = nl;
+                S.pre[f] = pre[f];
+                const i64 cap = (i64)p.cap[f];
+                if (MODE == 0 && agg[f] > 0 && pre[f] + (i64)agg[f] > cap) atomicOr(p.err, kErrCapacity);
+                S.hi[f] = (int)max((i64)0, min((i64)agg[f], cap - pre[f]));
+                const int first = -(int)(((uintptr_t)p.bytes[f] + (uintptr_t)pre[f]) & 15);
+                S.first[f] = first;
+                S.nch[f] = agg[f] > 0 ? (int)(((i64)agg[f] - first + 15) >> 4) : 0;
+            }
+        }
+        const bool all_safe = __all(safe);
+        if (lane == 0) {
+            S.safe = all_safe;
+            S.skip = __ballot(too_large) != 0;
+            if (too_large) atomicOr(p.err, kErrTooLarge);
+        }
+    }
+    __syncthreads();
+    if (S.skip) return;
+
+    // ---- 2. the column ranges, output-stationary (all lanes) ----
+    const int n0 = S.nch[0];
+    const int ntot = n0 + (NV == 2 ? S.nch[NV - 1] : 0);
+    const bool safe = S.safe != 0;
+    const uintptr_t dummy = (uintptr_t)flags;  // readable; its bytes are masked off
+    for (int c0 = 0; c0 < ntot; c0 += kThreads * kGU) {  // uniform loop
+        u32x4 r[kGU];
+        int Pq[kGU], fq[kGU];
+#pragma unroll
+        for (int u = 0; u < kGU; ++u) {
+            const int c = c0 + kThreads * u + tid;
+            const int f = NV == 2 && c >= n0 ? 1 : 0;
+            fq[u] = c < ntot ? f : -1;
+            const int Pc = S.first[f] + 16 * (c - (f ? n0 : 0));
+            Pq[u] = Pc;
+            r[u] = u32x4{0, 0, 0, 0};
+            if (c >= ntot) continue;
+            const int nl = S.nl[f];
+            const int k0 = lds_search_64(S.o[f], nl, max(Pc, 0));
+            const int o0 = S.o[f][k0], o1 = S.o[f][k0 + 1];
+            const bool two = k0 + 1 < nl && o1 < Pc + 16;  // the next field starts inside this chunk
+            if (safe) {
+                const int o2 = two ? S.o[f][k0 + 2] : o1;
+                const uintptr_t X0 = (uintptr_t)(S.addr[f][k0] + (u64)(i64)(Pc - o0));
+                const uintptr_t X1 = two ? (uintptr_t)(S.addr[f][k0 + 1] + (u64)(i64)(Pc - o1)) : dummy;
+                r[u] = (ld16u(X0) & range_mask(masks, o0 - Pc, o1 - Pc)) |
+                       (ld16u(X1) & range_mask(masks, two ? o1 - Pc : 16, o2 - Pc));
+                for (int k = k0 + 2; two && k < nl && S.o[f][k] < Pc + 16; ++k)  // fields under 16 bytes
+                    r[u] |= ld16u((uintptr_t)(S.addr[f][k] + (u64)(i64)(Pc - S.o[f][k]))) &
+                            range_mask(masks, S.o[f][k] - Pc, S.o[f][k + 1] - Pc);
+            } else {  // batch edges: aligned blocks holding valid bytes only
+                u32 t[4] = {0, 0, 0, 0};
+                for (int k = k0; k < nl && S.o[f][k] < Pc + 16; ++k) {
+                    const int lo = S.o[f][k] - Pc, hi = S.o[f][k + 1] - Pc;
+                    if (hi <= 0) continue;
+                    or_window_global((uintptr_t)(S.addr[f][k] + (u64)(i64)(Pc - S.o[f][k])), max(lo, 0), min(hi, 16), t);
+                }
+                r[u] = u32x4{t[0], t[1], t[2], t[3]};
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kGU; ++u) {
+            if (fq[u] < 0) continue;
+            const int f = fq[u];
+            const u32 rr[4] = {r[u].x, r[u].y, r[u].z, r[u].w};
+            store_chunk(p.bytes[f] + S.pre[f], Pq[u], 0, S.hi[f], rr);
+        }
+    }
+}
+
+template <int NF, int NV, bool MIX, int MODE>
+hipError_t launch_gather(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stream, int pnum, int pden) {
+    static int cus[16] = {0};
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    int& ncu = cus[dev & 15];
+    if (ncu == 0 && (e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
+    const u64 nt = num_tiles(p.n);
+    u64 P = (u64)ncu * pnum / pden;
+    if (P > (nt + 3) / 4) P = (nt + 3) / 4;
+    DecodeParams q = p;
+    q.pipe_parsers = (unsigned)P;
+    hipLaunchKernelGGL((decode_gather_kernel<NF, NV, MIX, MODE>), dim3((unsigned)(P + 1 + nt)), dim3(kThreads), 0,
+                       stream, q, flags, epoch);
+    return hipGetLastError();
+}
+
+template <int MODE>
+hipError_t launch_gather_layout(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stream, int pnum = 3,
+                                int pden = 4) {
+    if (p.type)
+        return p.lay.nfixed == 0 && p.lay.nvar == 2 ? launch_gather<0, 2, true, MODE>(p, flags, epoch, stream, pnum, pden)
+                                                     : hipErrorInvalidValue;
+    if (p.lay.nfixed == 0 && p.lay.nvar == 1) return launch_gather<0, 1, false, MODE>(p, flags, epoch, stream, pnum, pden);
+    if (p.lay.nfixed == 0 && p.lay.nvar == 2) return launch_gather<0, 2, false, MODE>(p, flags, epoch, stream, pnum, pden);
+    if (p.lay.nfixed == 2 && p.lay.nvar == 2) return launch_gather<2, 2, false, MODE>(p, flags, epoch, stream, pnum, pden);
+    return hipErrorInvalidValue;
+}
+
 template <int NF, int NV, bool MIX, int MODE, int DIAG, int SK = 4, int PR = 2, int STG = kStage, bool EARLY = false,
-          int PACE = 0, bool XCDP = false>
+          int PACE = 0, bool XCDP = false, int AHEAD = 0>
 hipError_t launch(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stream, int pnum = 1, int pden = 1) {
     if (DIAG && !p.dbg) return hipErrorInvalidValue;  // timestamps need SYMHIP_DEBUG_PTR (tuning builds)
     static int cus[16] = {0};
@@ -696,11 +1021,12 @@ hipError_t launch(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stre
     constexpr bool kRoles = MODE == 0 || MODE == 2 || MODE == 3;
     u64 P = kRoles ? (u64)ncu * pnum / pden : 0;  // parser workgroups: pnum / pden per CU
     if (P > (nt + 3) / 4) P = (nt + 3) / 4;
+    if (AHEAD > 0 && P > (u64)(AHEAD + 4 * PR - 1) / (4 * PR)) P = (AHEAD + 4 * PR - 1) / (4 * PR);  // tiles [0, AHEAD)
     DecodeParams q = p;
     q.pipe_parsers = (unsigned)P;
     const u64 grid = kRoles ? P + 1 + nt : nt;
-    hipLaunchKernelGGL((decode_pipe_kernel<NF, NV, MIX, MODE, DIAG, SK, PR, STG, EARLY, PACE, XCDP>), dim3((unsigned)grid), dim3(kThreads), 0,
-                       stream, q, flags, epoch);
+    hipLaunchKernelGGL((decode_pipe_kernel<NF, NV, MIX, MODE, DIAG, SK, PR, STG, EARLY, PACE, XCDP, AHEAD>), dim3((unsigned)grid),
+                       dim3(kThreads), 0, stream, q, flags, epoch);
     return hipGetLastError();
 }
 
@@ -709,11 +1035,11 @@ constexpr int kParsersNum = 3;   // parser workgroups = #CUs * 3/4
 constexpr int kParsersDen = 4;
 
 template <int MODE, int DIAG, int SK = kScanPer, int PR = 2, int STG = kStage, bool EARLY = false, int PACE = 0,
-          bool XCDP = false>
+          bool XCDP = false, int AHEAD = 0>
 hipError_t launch_layout(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stream, int pnum = kParsersNum,
                          int pden = kParsersDen) {
 #define SYMHIP_PIPE_LAUNCH(NF, NV, MIX) \
-    launch<NF, NV, MIX, MODE, DIAG, SK, PR, STG, EARLY, PACE, XCDP>(p, flags, epoch, stream, pnum, pden)
+    launch<NF, NV, MIX, MODE, DIAG, SK, PR, STG, EARLY, PACE, XCDP, AHEAD>(p, flags, epoch, stream, pnum, pden)
     if (p.type)  // mixed kv batch: GetRequest / SetRequest per record
         return p.lay.nfixed == 0 && p.lay.nvar == 2 ? SYMHIP_PIPE_LAUNCH(0, 2, true) : hipErrorInvalidValue;
     if (p.lay.nfixed == 0 && p.lay.nvar == 1) return SYMHIP_PIPE_LAUNCH(0, 1, false);
@@ -781,6 +1107,17 @@ hipError_t launch_decode_pipe(const DecodeParams& p, void* flags, unsigned epoch
         case 490: return pipe::launch_layout<0, 0, 2, 2, pipe::kStage, false, 1024, true>(p, fl, epoch, stream);
         case 491: return pipe::launch_layout<0, 0, 2, 2, pipe::kStage, false, 2048, true>(p, fl, epoch, stream);
         case 492: return pipe::launch_layout<2, 0, 2, 2, pipe::kStage, false, 0, true>(p, fl, epoch, stream);
+        // copiers parse ahead (AHEAD tiles; the parsers take only the first AHEAD tiles)
+        case 620: return pipe::launch_layout<0, 0, 2, 2, pipe::kStage, false, 0, false, 256>(p, fl, epoch, stream);
+        case 621: return pipe::launch_layout<0, 0, 2, 2, pipe::kStage, false, 0, false, 512>(p, fl, epoch, stream);
+        case 622: return pipe::launch_layout<0, 0, 2, 2, pipe::kStage, false, 0, false, 1024>(p, fl, epoch, stream);
+        case 623: return pipe::launch_layout<0, 0, 2, 2, pipe::kStage, false, 0, false, 2048>(p, fl, epoch, stream);
+        case 624: return pipe::launch_layout<0, 0, 2, 2, pipe::kStage, false, 0, false, 4096>(p, fl, epoch, stream);
+        // the gather copier (no LDS stage, output-stationary copy); 601: its timing mode (WRONG output)
+        case 600: return pipe::launch_gather_layout<0>(p, fl, epoch, stream);
+        case 601: return pipe::launch_gather_layout<1>(p, fl, epoch, stream);
+        case 602: return pipe::launch_gather_layout<0>(p, fl, epoch, stream, 1, 2);
+        case 603: return pipe::launch_gather_layout<0>(p, fl, epoch, stream, 1, 1);
         // the ring decode: lead 3 / 4, barrier / one-wave scanner; 51x: with timestamps
         case 500: return pipe::launch_ring_layout<0, 3, 0>(p, fl, epoch, stream);
         case 501: return pipe::launch_ring_layout<0, 3, 1>(p, fl, epoch, stream);

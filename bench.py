@@ -96,8 +96,25 @@ def workload(args, world, rank):
     return base
 
 
+def cgroup_cpus() -> float | None:
+    """CPUs this process may use by its cgroup's CPU quota (cgroup v2 cpu.max, or v1 cfs quota /
+    period); None when unlimited or unreadable."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else int(q) / int(p)
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else q / p
+    except (OSError, ValueError):
+        return None
+
+
 def host_cpu_info() -> dict:
-    """nproc, the CPU model (lscpu's "Model name", from /proc/cpuinfo) and this process's core share."""
+    """nproc, the CPU model (lscpu's "Model name", from /proc/cpuinfo), this process's affinity and
+    its cgroup CPU quota."""
     model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -107,15 +124,19 @@ def host_cpu_info() -> dict:
     except OSError:
         pass
     share = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    return {"nproc": os.cpu_count(), "affinity": share, "model": model}
+    quota = cgroup_cpus()
+    return {"nproc": os.cpu_count(), "affinity": share, "cgroup_cpu_quota": quota, "model": model,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
 def cpu_baseline(kw: dict, seconds: float) -> dict:
     """The C restatement of the Go codec (oracle/symphony_oracle.c; no Go toolchain exists here or
-    on the GPU box) on a bounded sample of the same workload: encode+decode at 1 thread and
-    record-sharded over the host's core share (at most 16 threads: the box's CPU share per GPU;
-    ctypes releases the GIL, so the shards run in parallel), plus config 1's echo record
-    (ns per MarshalSymphony / UnmarshalSymphony, one record per call)."""
+    on the GPU box) on a bounded sample of the same workload: encode+decode at 1 thread, then
+    record-sharded over the CPUs this process may actually use (its cgroup CPU quota, else its
+    affinity, else OMP_NUM_THREADS) and over nproc threads (above the quota the threads
+    time-slice, so that row shows what the quota caps); ctypes releases the GIL, so the shards run in
+    parallel.  Plus config 1's echo record (ns per MarshalSymphony / UnmarshalSymphony, one record
+    per call)."""
     from concurrent.futures import ThreadPoolExecutor
 
     from oracle import oracle
@@ -137,19 +158,29 @@ def cpu_baseline(kw: dict, seconds: float) -> dict:
             if el >= budget:
                 return reps, el
 
-    reps1, el1 = run(seconds / 2)
-    threads = max(1, min(16, info["affinity"]))
-    t0 = time.perf_counter()
-    with ThreadPoolExecutor(threads) as ex:
-        res = list(ex.map(run, [seconds / 2] * threads))
-    elN = time.perf_counter() - t0
-    repsN = sum(r for r, _ in res)
+    def sharded(threads: int, budget: float) -> tuple[int, float]:
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(threads) as ex:
+            res = list(ex.map(run, [budget] * threads))
+        return sum(r for r, _ in res), time.perf_counter() - t0
+
+    reps1, el1 = run(seconds / 3)
+    omp = int(info["omp_num_threads"]) if (info["omp_num_threads"] or "").isdigit() else None
+    share = info["cgroup_cpu_quota"] or omp or info["affinity"]
+    threads = max(1, min(int(share), info["affinity"]))
+    repsN, elN = sharded(threads, seconds / 3)
+    nproc = max(1, min(info["nproc"] or 1, 512))
+    repsP, elP = sharded(nproc, seconds / 3) if nproc != threads else (repsN, elN)
     m_ns, u_ns = oracle.bench_echo(2_000_000)
     gb = lambda reps, el: round((enc_b + dec_b) * reps / el / 1e9, 4)
     return {"value": gb(reps1, el1), "unit": "GB/s", "cores": 1, "kind": "port",
             "mrecords_per_s": round(2 * b.n * reps1 / el1 / 1e6, 4),
             "all_cores": {"value": gb(repsN, elN), "cores": threads,
-                          "mrecords_per_s": round(2 * b.n * repsN / elN / 1e6, 4)},
+                          "mrecords_per_s": round(2 * b.n * repsN / elN / 1e6, 4),
+                          "share_from": "cgroup cpu quota" if info["cgroup_cpu_quota"] else
+                                        ("OMP_NUM_THREADS" if omp else "affinity")},
+            "nproc_threads": {"value": gb(repsP, elP), "threads": nproc,
+                              "mrecords_per_s": round(2 * b.n * repsP / elP / 1e6, 4)},
             "host": info,
             "config1_echo": {"marshal_ns": round(m_ns, 2), "unmarshal_ns": round(u_ns, 2),
                              "records_per_s": round(1e9 / (m_ns + u_ns), 1),
@@ -158,9 +189,9 @@ def cpu_baseline(kw: dict, seconds: float) -> dict:
                                      "one record per call with Go's allocations (oracle/bench_oracle.c, "
                                      "testcases/simple/main.go:248-420 methodology), 1 thread"},
             "sample": f"{b.n} {s.go_type} records of the same workload (seed {sample['seed']:#x}), "
-                      f"encode+decode x{reps1} in {el1:.1f} s on 1 thread and x{repsN} in {elN:.1f} s on "
-                      f"{threads} threads by oracle/symphony_oracle.c (-O2): C restatement of the Go codec, "
-                      "not Go (no Go toolchain)"}
+                      f"encode+decode x{reps1} in {el1:.1f} s on 1 thread, x{repsN} in {elN:.1f} s on "
+                      f"{threads} threads (the CPU share) and x{repsP} in {elP:.1f} s on {nproc} threads (nproc) "
+                      "by oracle/symphony_oracle.c (-O2): C restatement of the Go codec, not Go (no Go toolchain)"}
 
 
 def load_traffic(kernel: str):
