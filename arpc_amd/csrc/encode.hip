@@ -38,16 +38,18 @@ constexpr int slot_bytes(int H0) { return ((H0 + 16) + 7) & ~7; }
 
 // A tile's stream span must stay below 2^31 (64 records; positions are 32-bit), and string
 // fields are < 2^32 bytes (Symphony's u32 length prefix).
-template <int NV, int SLOT>
+template <int NV, int SLOT, int TR = kWaveRecs>
 struct EncWaveLds {
-    char hdr[(kWaveRecs + 1) * SLOT];  // slot 0 = zero pad, slot i+1 = record i
-    int o[kWaveRecs + 1];              // record start relative to the tile start; [cnt] = span
-    u32 len[NV][kWaveRecs];
-    u64 delta[NV][kWaveRecs];          // payload byte address = delta + chunk position
-    uint8_t h0[kWaveRecs];             // mixed batches: the record's bytes before field 0's payload
-    i64 t0;                            // the tile's stream start
-    int span, ok;                      // its length; 0 if it is too long for 32-bit positions
-    int safe;                          // no payload window of the tile reaches past a column end
+    char hdr[(TR + 1) * SLOT];  // slot 0 = zero pad, slot i+1 = record i
+    int o[TR + 1];              // record start relative to the tile start; [cnt] = span
+    u32 len[NV][TR];
+    u64 delta[NV][TR];          // payload byte address = delta + chunk position
+    uint8_t h0[TR];             // mixed batches: the record's bytes before field 0's payload
+    i64 t0;                     // the tile's stream start
+    int span, ok;               // its length; 0 if it is too long for 32-bit positions
+    int safe;                   // no payload window of the tile reaches past a column end
+    int safe_h[TR / kWaveRecs]; // per header wave (TR > 64)
+    i64 end_h[TR / kWaveRecs];  // per header wave: the end of its last record
 };
 
 // MIXED: a kv batch of GetRequests (type 0: 22 + K bytes, kv.syn.go:74-132) and SetRequests (else:
@@ -56,28 +58,33 @@ struct EncWaveLds {
 // WPT (waves per tile): 1 = each wave owns a tile; kWaves = the workgroup owns one tile, wave 0
 // builds it and the waves take its output steps round-robin (4x shorter-lived workgroups, so a
 // 2^20-record launch runs ~8 rounds of workgroups instead of ~2 and its tail is short).
-template <int NF, int NV, int kVariant, bool MIXED = false, int WPT = 1, bool DIAG = false>
+// TR: records per tile (64, or 128 with whole-workgroup tiles: waves 0 and 1 build the headers of
+// 64 records each, so a tile of short records -- mixed Get/Set batches -- moves about as many bytes
+// as a 64-record tile of SetRequests).
+template <int NF, int NV, int kVariant, bool MIXED = false, int WPT = 1, bool DIAG = false, int TR = kWaveRecs>
 __global__ __launch_bounds__(256) void encode_kernel(EncodeParams p) {
     static_assert(!MIXED || (NF == 0 && NV == 2 && kVariant <= 1), "mixed batches are kv Get/Set");
     static_assert(WPT == 1 || (WPT == kWaves && kVariant <= 1), "whole-workgroup tiles take one step per wave");
+    static_assert(TR == kWaveRecs || (TR == 2 * kWaveRecs && WPT == kWaves), "128-record tiles are workgroup tiles");
+    constexpr int HW = TR / kWaveRecs;  // waves that build headers
     constexpr int NT = NF + NV;
     constexpr int H0 = 14 + 4 * NT + 4;        // bytes before field 0's payload (the largest, in mixed batches)
     constexpr i64 OVH = 14 + 4 * NT + 4 * NV;  // fixed bytes per record
     constexpr int SLOT = slot_bytes(H0);
     static_assert(SLOT - 16 >= H0 && OVH >= 16, "layout assumptions");
 
-    __shared__ EncWaveLds<NV, SLOT> lds_all[kWaves / WPT];
+    __shared__ EncWaveLds<NV, SLOT, TR> lds_all[kWaves / WPT];
     __shared__ uint8_t flags_all[kWaves][64];  // record-start marks of one phase-2 step, per wave
     __shared__ MaskTable masks;
     mask_table_init(masks, threadIdx.x);
     __syncthreads();
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    EncWaveLds<NV, SLOT>& S = lds_all[WPT == 1 ? wave : 0];
+    EncWaveLds<NV, SLOT, TR>& S = lds_all[WPT == 1 ? wave : 0];
     uint8_t* const flg = flags_all[wave];
-    const u64 r0 = (WPT == 1 ? (u64)blockIdx.x * kWaves + wave : (u64)blockIdx.x) * kWaveRecs;
+    const u64 r0 = (WPT == 1 ? (u64)blockIdx.x * kWaves + wave : (u64)blockIdx.x) * TR;
     if (r0 >= p.n) return;  // wave-uniform (workgroup-uniform when WPT > 1)
-    const int cnt = (int)min((u64)kWaveRecs, p.n - r0);
+    const int cnt = (int)min((u64)TR, p.n - r0);
     flg[lane] = 0;
     u64* const stamp = DIAG ? p.dbg + (r0 / kWaveRecs) * 8 : nullptr;  // tools/enc_timeline.py
     if (DIAG && lane == 0 && (WPT == 1 || wave == 0)) {
@@ -86,106 +93,145 @@ __global__ __launch_bounds__(256) void encode_kernel(EncodeParams p) {
     }
 
     // ---------------- phase 1: per-record offsets and header image ----------------
-    if (WPT == 1 || wave == 0) {
+    // header wave h (h < HW) takes the tile's records [64 h, 64 h + 64): record rec = 64 h + lane
+    const int hw = WPT == 1 ? 0 : wave;
+    const u64 rb = r0 + (u64)hw * kWaveRecs;   // the header wave's first record
+    const int hcnt = (int)min((u64)kWaveRecs, rb < p.n ? p.n - rb : (u64)0);
+    const int rec = hw * kWaveRecs + lane;
+    const bool hdr_wave = (WPT == 1 || wave < HW) && hcnt > 0;
     // A payload window reads up to 15 bytes beyond its field; that stays inside the column
     // unless the tile's fields sit within 16 bytes of the column's ends (batch edges).  Scalar
     // loads, issued with the per-record ones.
-    bool tile_safe = true;
-#pragma unroll
-    for (int f = 0; f < NV; ++f) {
-        const u64 c0 = p.offs[f][0], c1 = p.offs[f][p.n];
-        const u64 t0 = p.offs[f][r0], t1 = p.offs[f][r0 + cnt];
-        tile_safe = tile_safe && t0 >= c0 + 16 && t1 + 16 <= c1;
-    }
+    bool part_safe = true;
     i64 o = 0, size = 0;
     u64 L[NV];
+#pragma unroll
+    for (int f = 0; f < NV; ++f) L[f] = 0;
     bool isset = true;  // mixed batches: SetRequest (else GetRequest)
-    if constexpr (MIXED) {
-        // sizes depend on the type: the size pass's tile prefix plus a wave scan of this tile's sizes
+    if (hdr_wave) {
 #pragma unroll
-        for (int f = 0; f < NV; ++f) L[f] = 0;
-        if (lane < cnt) {
-            const u64 r = r0 + lane;
-            isset = p.type[r] != 0;
-            L[0] = p.offs[0][r + 1] - p.offs[0][r];
-            if (isset) L[1] = p.offs[1][r + 1] - p.offs[1][r];
-            size = (i64)(22 + L[0] + (isset ? 8 + L[1] : 0));
+        for (int f = 0; f < NV; ++f) {
+            const u64 c0 = p.offs[f][0], c1 = p.offs[f][p.n];
+            const u64 t0 = p.offs[f][rb], t1 = p.offs[f][rb + hcnt];
+            part_safe = part_safe && t0 >= c0 + 16 && t1 + 16 <= c1;
         }
-        const u64 tile = r0 / kWaveRecs;
-        const i64 tp = uniform_i64((i64)(p.group_pre[tile >> kGroupShift] + p.tile_loc[tile]));
-        o = tp + (i64)(wave_incl_scan_u64((u64)size, lane) - (u64)size);
-        if (lane < cnt) {
-            const u64 r = r0 + lane;
+        if constexpr (MIXED) {
+            // sizes depend on the type: the size pass's prefix of this 64-record part plus a wave scan
+            if (lane < hcnt) {
+                const u64 r = rb + lane;
+                isset = p.type[r] != 0;
+                L[0] = p.offs[0][r + 1] - p.offs[0][r];
+                if (isset) L[1] = p.offs[1][r + 1] - p.offs[1][r];
+                size = (i64)(22 + L[0] + (isset ? 8 + L[1] : 0));
+            }
+            const u64 part = rb / kWaveRecs;  // the size pass's 64-record tiles
+            const i64 tp = uniform_i64((i64)(p.group_pre[part >> kGroupShift] + p.tile_loc[part]));
+            o = tp + (i64)(wave_incl_scan_u64((u64)size, lane) - (u64)size);
+            if (lane < hcnt) {
+                const u64 r = rb + lane;
 #pragma unroll
-            for (int f = 0; f < NV; ++f) S.len[f][lane] = (u32)L[f];
+                for (int f = 0; f < NV; ++f) S.len[f][rec] = (u32)L[f];
+                p.out_off[r] = p.out_base + (u64)o;
+                if (r == p.n - 1) p.out_off[p.n] = p.out_base + (u64)(o + size);
+            }
+        } else if (lane < hcnt) {
+            const u64 r = rb + lane;
+            o = (i64)r * OVH;
+            size = OVH;
+#pragma unroll
+            for (int f = 0; f < NV; ++f) {
+                const u64 lo = p.offs[f][r];
+                L[f] = p.offs[f][r + 1] - lo;
+                o += (i64)(lo - p.offs[f][0]);
+                size += (i64)L[f];
+                S.len[f][rec] = (u32)L[f];
+            }
             p.out_off[r] = p.out_base + (u64)o;
             if (r == p.n - 1) p.out_off[p.n] = p.out_base + (u64)(o + size);
         }
-    } else if (lane < cnt) {
-        const u64 r = r0 + lane;
-        o = (i64)r * OVH;
-        size = OVH;
-#pragma unroll
-        for (int f = 0; f < NV; ++f) {
-            const u64 lo = p.offs[f][r];
-            L[f] = p.offs[f][r + 1] - lo;
-            o += (i64)(lo - p.offs[f][0]);
-            size += (i64)L[f];
-            S.len[f][lane] = (u32)L[f];
+        if constexpr (HW > 1) {  // the parts meet in LDS: tile start, part ends, edge checks
+            const i64 t0 = uniform_i64((i64)__shfl((long long)o, 0, 64));
+            const i64 t1 = uniform_i64((i64)__shfl((long long)(o + size), hcnt - 1, 64));
+            if (lane == 0) {
+                if (hw == 0) S.t0 = t0;
+                S.end_h[hw] = t1;
+                S.safe_h[hw] = part_safe;
+            }
         }
-        p.out_off[r] = p.out_base + (u64)o;
-        if (r == p.n - 1) p.out_off[p.n] = p.out_base + (u64)(o + size);
     }
-    // wave-uniform: readfirstlane keeps them (and the phase-2 loop bounds) in SGPRs
-    const i64 T0 = uniform_i64((i64)__shfl((long long)o, 0, 64));
-    const i64 T1 = uniform_i64((i64)__shfl((long long)(o + size), cnt - 1, 64));
-    const bool ok = T1 - T0 < (i64)1 << 31;  // positions are 32-bit inside a tile
-    if (lane == 0) {
-        S.t0 = T0;
-        S.span = (int)(T1 - T0);
-        S.ok = ok;
-        S.safe = tile_safe;
-        if (!ok) atomicOr(p.err, kErrTooLarge);
-    }
-    if (ok && lane < cnt) {
-        const u64 r = r0 + lane;
-        const int orel = (int)(o - T0);
-        S.o[lane] = orel;
-        if (lane == cnt - 1) S.o[cnt] = (int)(T1 - T0);
-        const int h0 = MIXED && !isset ? 22 : H0;
-        int ps = h0;
-#pragma unroll
-        for (int f = 0; f < NV; ++f) {
-            S.delta[f][lane] = (u64)(uintptr_t)(p.bytes[f] + p.offs[f][r]) - (u64)(i64)(orel + ps);
-            ps += (int)L[f] + 4;
+    if constexpr (HW > 1) {
+        __syncthreads();
+        if (hdr_wave && lane == 0 && rb + hcnt == min(r0 + (u64)TR, p.n)) {  // the header wave of the tile's last part
+            const i64 t0 = S.t0, t1 = S.end_h[hw];
+            bool safe = true;
+            for (int h = 0; h <= hw; ++h) safe = safe && S.safe_h[h] != 0;
+            const bool ok = t1 - t0 < (i64)1 << 31;
+            S.span = (int)(t1 - t0);
+            S.ok = ok;
+            S.safe = safe;
+            if (!ok) atomicOr(p.err, kErrTooLarge);
         }
-        // header image: [0]=1 | [1:5]=13 | [5:9]=sid | [9:13]=mid | [13]=1 | table | len(field 0)
-        u32 h[SLOT / 4 + 1];
-#pragma unroll
-        for (int k = 0; k < SLOT / 4 + 1; ++k) h[k] = 0;
-        img_put_u8<0>(h, 1);
-        img_put_u32<1>(h, 13);
-        img_put_u32<5>(h, p.service_id);
-        img_put_u32<9>(h, MIXED && !isset ? p.method_get : p.method_id);
-        img_put_u8<13>(h, 1);
-        if constexpr (NF > 0) img_put_u32<14>(h, (u32)p.fixed[0][r]);
-        if constexpr (NF > 1) img_put_u32<18>(h, (u32)p.fixed[1][r]);
-        // private-table entries: offset of the field's length prefix relative to privateStart
-        // (13), truncated to u32 (kv.syn.go:664, :671).
-        if (MIXED && !isset) {  // GetRequest{Key} (kv.syn.go:119-127)
-            img_put_u32<14>(h, 5u);
-            img_put_u32<18>(h, (u32)L[0]);
+        __syncthreads();
+    }
+    if (hdr_wave) {
+        // wave-uniform: readfirstlane keeps them (and the phase-2 loop bounds) in SGPRs
+        i64 T0, T1;
+        bool ok;
+        if constexpr (HW > 1) {
+            T0 = uniform_i64(S.t0);
+            T1 = T0 + __builtin_amdgcn_readfirstlane(S.span);
+            ok = S.ok != 0;
         } else {
-            img_put_u32<14 + 4 * NF>(h, (u32)(H0 - 4 - 13));
-            if constexpr (NV > 1) img_put_u32<18 + 4 * NF>(h, (u32)(H0 + L[0] + 4 - 4 - 13));
-            img_put_u32<H0 - 4>(h, (u32)L[0]);
+            T0 = uniform_i64((i64)__shfl((long long)o, 0, 64));
+            T1 = uniform_i64((i64)__shfl((long long)(o + size), hcnt - 1, 64));
+            ok = T1 - T0 < (i64)1 << 31;  // positions are 32-bit inside a tile
+            if (lane == 0) {
+                S.t0 = T0;
+                S.span = (int)(T1 - T0);
+                S.ok = ok;
+                S.safe = part_safe;
+                if (!ok) atomicOr(p.err, kErrTooLarge);
+            }
         }
-        if constexpr (MIXED) S.h0[lane] = (uint8_t)h0;
-        uint2* slot = (uint2*)&S.hdr[(lane + 1) * SLOT];
+        if (ok && lane < hcnt) {
+            const u64 r = rb + lane;
+            const int orel = (int)(o - T0);
+            S.o[rec] = orel;
+            if (rec == cnt - 1) S.o[cnt] = (int)(T1 - T0);
+            const int h0 = MIXED && !isset ? 22 : H0;
+            int ps = h0;
 #pragma unroll
-        for (int k = 0; k < SLOT / 8; ++k) slot[k] = make_uint2(h[2 * k], h[2 * k + 1]);
-    }
-    if (lane < SLOT / 4) ((u32*)S.hdr)[lane] = 0;
+            for (int f = 0; f < NV; ++f) {
+                S.delta[f][rec] = (u64)(uintptr_t)(p.bytes[f] + p.offs[f][r]) - (u64)(i64)(orel + ps);
+                ps += (int)L[f] + 4;
+            }
+            // header image: [0]=1 | [1:5]=13 | [5:9]=sid | [9:13]=mid | [13]=1 | table | len(field 0)
+            u32 h[SLOT / 4 + 1];
+#pragma unroll
+            for (int k = 0; k < SLOT / 4 + 1; ++k) h[k] = 0;
+            img_put_u8<0>(h, 1);
+            img_put_u32<1>(h, 13);
+            img_put_u32<5>(h, p.service_id);
+            img_put_u32<9>(h, MIXED && !isset ? p.method_get : p.method_id);
+            img_put_u8<13>(h, 1);
+            if constexpr (NF > 0) img_put_u32<14>(h, (u32)p.fixed[0][r]);
+            if constexpr (NF > 1) img_put_u32<18>(h, (u32)p.fixed[1][r]);
+            // private-table entries: offset of the field's length prefix relative to privateStart
+            // (13), truncated to u32 (kv.syn.go:664, :671).
+            if (MIXED && !isset) {  // GetRequest{Key} (kv.syn.go:119-127)
+                img_put_u32<14>(h, 5u);
+                img_put_u32<18>(h, (u32)L[0]);
+            } else {
+                img_put_u32<14 + 4 * NF>(h, (u32)(H0 - 4 - 13));
+                if constexpr (NV > 1) img_put_u32<18 + 4 * NF>(h, (u32)(H0 + L[0] + 4 - 4 - 13));
+                img_put_u32<H0 - 4>(h, (u32)L[0]);
+            }
+            if constexpr (MIXED) S.h0[rec] = (uint8_t)h0;
+            uint2* slot = (uint2*)&S.hdr[(rec + 1) * SLOT];
+#pragma unroll
+            for (int k = 0; k < SLOT / 8; ++k) slot[k] = make_uint2(h[2 * k], h[2 * k + 1]);
+        }
+        if (hw == 0 && lane < SLOT / 4) ((u32*)S.hdr)[lane] = 0;
     }
     if constexpr (WPT == 1) wave_sync();
     else __syncthreads();
@@ -200,22 +246,29 @@ __global__ __launch_bounds__(256) void encode_kernel(EncodeParams p) {
     uint8_t* const out_t = p.out + T0;
     const uintptr_t dummy = (uintptr_t)p.out & ~(uintptr_t)15;  // readable; its bytes get masked off
     const bool tile_safe = S.safe != 0;
-    const i64 my_o = lane < cnt ? (i64)S.o[lane] : ((i64)1 << 40);  // record-role register
+    const i64 my_o = lane < cnt ? (i64)S.o[lane] : ((i64)1 << 40);  // record-role registers
+    const i64 my_o2 = HW > 1 && 64 + lane < cnt ? (i64)S.o[64 + (HW > 1 ? lane : 0)] : ((i64)1 << 40);
 
     // Chunk -> record without searching: records are >= 22 bytes, so at most one record starts
     // inside any 16-byte chunk.  Record k first owns chunk ceil((o_k - B)/16) of this step; a
     // ballot of those marks plus mbcnt gives every lane its record.
+    u64 before2 = 0;
     auto locate = [&](int B) -> int {
         const i64 ck = (my_o - B + 15) >> 4;
         const u64 before = __ballot(ck <= 0);
         if (ck >= 1 && ck <= 63) flg[ck] = 1;
+        if constexpr (HW > 1) {  // the tile's second 64 records
+            const i64 ck2 = (my_o2 - B + 15) >> 4;
+            before2 = __ballot(ck2 <= 0);
+            if (ck2 >= 1 && ck2 <= 63) flg[ck2] = 1;
+        }
         wave_sync();
         const bool mine = flg[lane] != 0;
         const u64 m = __ballot(mine);
         if (mine) flg[lane] = 0;  // clean for the next step (each lane its own byte)
         const int below = (int)__builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u));
         // (int) casts matter: __popcll is unsigned and max(unsigned, int) picks the double overload
-        const int counted = (int)__popcll(before) + below + (mine ? 1 : 0);
+        const int counted = (int)__popcll(before) + (HW > 1 ? (int)__popcll(before2) : 0) + below + (mine ? 1 : 0);
         return counted > 0 ? counted - 1 : 0;  // 0 only for the chunk straddling the tile start
     };
 
@@ -427,6 +480,8 @@ static void launch_layout(const EncodeParams& p, hipStream_t stream) {
         case 8: hipLaunchKernelGGL((encode_kernel<NF, NV, 1, false, kWaves>), encode_grid(p.n, kWaves), block, 0, stream, p); return;
         case 9: hipLaunchKernelGGL((encode_kernel<NF, NV, 1, false, 1>), encode_grid(p.n, 1), block, 0, stream, p); return;
         case 10: hipLaunchKernelGGL((encode_kernel<NF, NV, 1, false, kWaves, true>), encode_grid(p.n, kWaves), block, 0, stream, p); return;
+        // 21: 128-record workgroup tiles (two header waves)
+        case 21: hipLaunchKernelGGL((encode_kernel<NF, NV, 1, false, kWaves, false, 2 * kWaveRecs>), dim3((unsigned)((p.n + 127) / 128)), block, 0, stream, p); return;
         // 15: workgroup tiles, one step at a time (no software pipeline)
         case 15: hipLaunchKernelGGL((encode_kernel<NF, NV, 0, false, kWaves>), encode_grid(p.n, kWaves), block, 0, stream, p); return;
         default: break;
@@ -556,6 +611,12 @@ hipError_t launch_encode_mixed(EncodeParams p, void* ws, hipStream_t stream) {
     p.group_pre = w.group_pre;
     p.tile_loc = w.tile_loc;
 #ifdef SYMHIP_TUNING
+    if (p.variant == 20) {  // 128-record workgroup tiles
+        const u64 t128 = (p.n + 127) / 128;
+        hipLaunchKernelGGL((encode_kernel<0, 2, 1, true, kWaves, false, 2 * kWaveRecs>), dim3((unsigned)t128),
+                           dim3(64 * kWaves), 0, stream, p);
+        return hipGetLastError();
+    }
     if (p.variant == 5 || p.variant == 15) {
         if (p.variant == 5) hipLaunchKernelGGL((encode_kernel<0, 2, 0, true>), encode_grid(p.n, 1), dim3(64 * kWaves), 0, stream, p);
         else hipLaunchKernelGGL((encode_kernel<0, 2, 0, true, kWaves>), encode_grid(p.n, kWaves), dim3(64 * kWaves), 0, stream, p);
