@@ -38,6 +38,7 @@ SIGNATURES = {
     "sym_ctx_reserve": (_int, [_ctx, _u64]),
     "sym_ctx_check": (_int, [_ctx, _vp]),
     "sym_ctx_set_decode_impl": (_int, [_ctx, _int]),
+    "sym_ctx_set_encode_impl": (_int, [_ctx, _int]),
     "sym_schema_info": (_int, [_int, ctypes.POINTER(_int), ctypes.POINTER(_int)]),
     "sym_record_overhead": (_u64, [_int]),
     "sym_encoded_size": (_u64, [_int, _u64, _u64]),
@@ -87,6 +88,9 @@ SIGNATURES = {
 SYM_DECODE_PIPELINE = 0
 SYM_DECODE_THREE_KERNEL = 1
 SYM_DECODE_LOOKBACK = 2
+SYM_ENCODE_PIPELINE = 0
+SYM_ENCODE_THREE_KERNEL = 1
+SYM_ENCODE_LOOKBACK = 2
 
 SYM_MAX_UDP_PAYLOAD = 1400
 SYM_DATA_PACKET_HEADER = 31

@@ -85,6 +85,11 @@ class Codec:
         """SYM_DECODE_PIPELINE (default), SYM_DECODE_THREE_KERNEL or SYM_DECODE_LOOKBACK (same results)."""
         _native.check(self._lib.sym_ctx_set_decode_impl(self._ctx, impl), "sym_ctx_set_decode_impl")
 
+    def set_encode_impl(self, impl: int):
+        """Mixed Get/Set encodes' size scan: SYM_ENCODE_PIPELINE (default), SYM_ENCODE_THREE_KERNEL or
+        SYM_ENCODE_LOOKBACK (same results)."""
+        _native.check(self._lib.sym_ctx_set_encode_impl(self._ctx, impl), "sym_ctx_set_encode_impl")
+
     # ------------------------------------------------------------------ encode
     def encode(self, schema: schemas.Schema | str, fixed, var, service_id: int = 0, method_id: int = 0,
                out: torch.Tensor | None = None, out_off: torch.Tensor | None = None,

@@ -189,6 +189,14 @@ int sym_ctx_set_decode_impl(sym_ctx* ctx, int impl) {
     return SYM_OK;
 }
 
+int sym_ctx_set_encode_impl(sym_ctx* ctx, int impl) {
+    if (!ctx) return fail(SYM_ERR_INVALID, "sym_ctx_set_encode_impl: ctx is NULL");
+    if (impl != SYM_ENCODE_PIPELINE && impl != SYM_ENCODE_THREE_KERNEL && impl != SYM_ENCODE_LOOKBACK)
+        return fail(SYM_ERR_INVALID, "sym_ctx_set_encode_impl: unknown implementation %d", impl);
+    ctx->encode_impl = impl;
+    return SYM_OK;
+}
+
 int sym_schema_info(int schema, int* nfixed, int* nvar) {
     if (!schema_ok(schema)) return fail(SYM_ERR_INVALID, "unknown schema %d", schema);
     if (nfixed) *nfixed = kLayouts[schema].nfixed;
@@ -424,12 +432,22 @@ int sym_encode_kv_mixed(sym_ctx* ctx, const uint8_t* d_type, const uint8_t* d_ke
     p.out = d_out;
     p.out_off = d_out_off;
     p.err = ctx->err;
+    p.impl = ctx->encode_impl;
 #ifdef SYMHIP_TUNING
     p.variant = symhip::tuning_variant("SYMHIP_ENCODE_VARIANT");
+    if (p.variant == 37 || p.variant == 38) {  // tools/mixed_timeline.py: 16 u64 per 64-record tile
+        if (const char* d = getenv("SYMHIP_DEBUG_PTR")) p.dbg = (uint64_t*)(uintptr_t)strtoull(d, nullptr, 16);
+        if (!p.dbg) return fail(SYM_ERR_INVALID, "mixed encode timeline needs SYMHIP_DEBUG_PTR");
+    }
 #endif
     if (n) {
-        const int rc = ensure_scratch(ctx, symhip::encode_mixed_ws_bytes(n), "mixed encode");
+        int rc = ensure_flags(ctx, n);
+        unsigned epoch = 0;
+        if (rc == SYM_OK) rc = next_epoch(ctx, (hipStream_t)stream, &epoch);
+        if (rc == SYM_OK) rc = ensure_scratch(ctx, symhip::encode_mixed_ws_bytes(n), "mixed encode");
         if (rc != SYM_OK) return rc;
+        p.flags = ctx->flags;
+        p.epoch = epoch;
     }
     hipError_t e = symhip::launch_encode_mixed(p, ctx->frag, (hipStream_t)stream);
     return e == hipSuccess ? SYM_OK : hip_fail(e, "mixed encode launch");

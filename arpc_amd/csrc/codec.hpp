@@ -41,12 +41,18 @@ struct EncodeParams {
     uint8_t* out;
     uint64_t* out_off;
     unsigned* err;  // persistent device error word (kErr* bits), cleared by the host
-    // mixed kv batch (sym_encode_kv_mixed): per-record type (0 GetRequest, else SetRequest) and the
-    // record-size prefixes from launch_encode_mixed's size pass (tile t starts at
-    // group_pre[t / 64] + tile_loc[t]); null otherwise
+    // mixed kv batch (sym_encode_kv_mixed): per-record type (0 GetRequest, else SetRequest); null
+    // otherwise.  Record-size prefixes come from the launch's own sizers and scanner through the
+    // ctx's epoch-tagged words (flags, epoch; pipe_words.hpp), or -- SYM_ENCODE_THREE_KERNEL -- from
+    // a separate size pass (tile t starts at group_pre[t / 16] + tile_loc[t]).
     const uint8_t* type;
     const uint64_t* group_pre;
     const uint64_t* tile_loc;
+    void* flags;             // decode_pipe_flag_bytes() bytes of look-back words (sym_ctx)
+    unsigned epoch;          // their tag for this call, in [1, kEpochLimit)
+    unsigned pipe_sizers;    // set by launch_encode_mixed: sizer workgroups of the launch
+    int pipe_lookback;       // set by launch_encode_mixed: no sizers / scanner, every tile looks back
+    int impl;                // mixed batches: SYM_ENCODE_* (sym_ctx_set_encode_impl)
     uint32_t method_get;  // method id written into [9:13] of GetRequest records (mixed batches)
     uint64_t out_base;    // added to every out_off value written (chunked host staging), 0 otherwise
     uint64_t* dbg;        // tuning builds only (tools/enc_timeline.py): per-tile timestamps, else null
@@ -217,8 +223,9 @@ hipError_t launch_firewall(const uint8_t* in, const uint64_t* rec_off, uint64_t 
                            hipStream_t stream);
 
 hipError_t launch_encode(const EncodeParams& p, hipStream_t stream);
-// Mixed Get/Set batch: size pass (per-tile record-size totals, last workgroup scans them) + encode.
-size_t encode_mixed_ws_bytes(uint64_t n);
+// Mixed Get/Set batch: one launch -- sizers, scanner and encode tiles over p.flags / p.epoch -- or
+// (p.impl == SYM_ENCODE_THREE_KERNEL) size pass, group scan, encode over ws.
+size_t encode_mixed_ws_bytes(uint64_t n);  // SYM_ENCODE_THREE_KERNEL's scratch
 hipError_t launch_encode_mixed(EncodeParams p, void* ws, hipStream_t stream);
 hipError_t launch_decode(const DecodeParams& p, hipStream_t stream);
 

@@ -39,6 +39,7 @@ struct sym_ctx {
     uint8_t crypt_keys[64] = {0};
     int num_cus = 0;
     int decode_impl = SYM_DECODE_PIPELINE;
+    int encode_impl = 0;  // SYM_ENCODE_* (mixed batches' size scan)
     // host-memory entry points: chunk slots (created on first use)
     symhip::host::Slot slots[symhip::host::kSlots];
     bool slots_ready = false;

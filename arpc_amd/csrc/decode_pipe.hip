@@ -44,6 +44,7 @@
 #include "../../include/symphony_hip.h"
 #include "codec.hpp"
 #include "device_util.hpp"
+#include "pipe_words.hpp"
 
 namespace symhip {
 
@@ -54,16 +55,6 @@ constexpr int kThreads = 256;   // 4 waves
 constexpr int kStage = 22528;   // staged bytes per tile: a whole 64-record tile of 350-B records
 constexpr int kU = 2;           // copy chunks per lane per step
 
-// Word: [63:44] epoch, [43:42] status (1 = aggregate, 2 = exclusive prefix), [41:0] value.
-constexpr int kEpochShift = 44;
-constexpr u64 kStAgg = 1ull << 42;
-constexpr u64 kStPre = 2ull << 42;
-constexpr u64 kValMask = (1ull << 42) - 1;
-// Bounded waits, in wall time (s_memrealtime runs at 100 MHz): a wait that outlives this reports
-// kErrTimeout (SYM_ERR_DEVICE from sym_ctx_check) and gives up, so the grid always drains.
-constexpr u64 kWaitTicks = 25000000;  // 250 ms: the scanner gives up (copiers fall back) after this idle time
-constexpr u64 kFallbackTicks = 100000; // 1 ms: a copier waits this long for its prefix before looking back
-__device__ __forceinline__ u64 now_ticks() { return __builtin_amdgcn_s_memrealtime(); }
 
 __host__ __device__ inline u64 num_tiles(u64 n) { return (n + kRecs - 1) / kRecs; }
 
@@ -81,21 +72,6 @@ struct alignas(16) Lds {
     int first[4];            // scanner: per-wave first unpublished tile
 };
 
-__device__ __forceinline__ u64 lane_u64_pub(u64 v, int l) {
-    return (u64)__builtin_amdgcn_readlane((u32)v, l) | ((u64)__builtin_amdgcn_readlane((u32)(v >> 32), l) << 32);
-}
-__device__ __forceinline__ bool tagged(u64 w, u32 epoch) { return (u32)(w >> kEpochShift) == epoch; }
-__device__ __forceinline__ u64 make_word(u32 epoch, u64 st, u64 v) {
-    return ((u64)epoch << kEpochShift) | st | (v & kValMask);
-}
-__device__ __forceinline__ void store_word(u64* w, u64 v) {
-    __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ u64 load_word(u64* w) { return __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-
-// Workgroup barrier that orders LDS only: outstanding global stores keep flying (__syncthreads()
-// would wait for them).  Global loads whose data is used were waited on at their use.
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // u32 at byte q (q <= 4*NW-4) of a register window w[0..NW): bit-select the dword pair (a dynamic
 // register index would go to scratch) and align.
@@ -247,88 +223,8 @@ __device__ void parser(const DecodeParams& p, u64* aw, u64* pw, u64 ntiles, u32 
     }
 }
 
-// ---------------------------------------------------------------- scanner role
-// Each step loads the aggregate words of the next 1024 tiles, finds the first tile whose word is not
-// yet published (the frontier), and publishes the exclusive prefix of every tile before it.  A
-// tile's prefix so depends only on earlier tiles, whoever published their aggregates.
+// ---------------------------------------------------------------- scanner role: pipe_words.hpp scanner()
 constexpr int kScanPerG = 2;  // the gather copier's scanner: tiles per thread per step
-
-template <int NV, int SK, int NT = kThreads, typename LdsT>
-__device__ void scanner(u64* aw, u64* pw, u64 ntiles, u32 epoch, LdsT& S, u64* dbg = nullptr) {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    constexpr int kPer = SK;  // tiles per thread per step
-    constexpr int kW = NT / 64;  // waves
-    constexpr u64 kStep = (u64)NT * kPer;
-    u64 carry[NV];
-#pragma unroll
-    for (int f = 0; f < NV; ++f) carry[f] = 0;
-    u64 idle_since = 0;  // 0: the frontier moved on the last step
-    for (u64 base = 0; base < ntiles;) {
-        const u64 t0 = base + (u64)tid * kPer;
-        u64 v[NV][kPer];
-#pragma unroll
-        for (int f = 0; f < NV; ++f)
-#pragma unroll
-            for (int k = 0; k < kPer; ++k)
-                v[f][k] = t0 + k < ntiles ? load_word(&aw[(size_t)f * ntiles + t0 + k]) : make_word(epoch, kStAgg, 0);
-        u32 miss = (u32)kStep;  // this thread's first unpublished tile (relative to base)
-#pragma unroll
-        for (int k = kPer - 1; k >= 0; --k) {
-            bool ok = true;
-#pragma unroll
-            for (int f = 0; f < NV; ++f) ok = ok && tagged(v[f][k], epoch);
-            if (!ok) miss = (u32)(tid * kPer + k);
-        }
-#pragma unroll
-        for (int d = 32; d > 0; d >>= 1) miss = min(miss, (u32)__shfl_xor((int)miss, d, 64));
-        if (lane == 0) S.first[wave] = (int)miss;
-        lds_barrier();
-        u32 m = (u32)S.first[0];
-#pragma unroll
-        for (int q = 1; q < kW; ++q) m = min(m, (u32)S.first[q]);
-        lds_barrier();  // S.first is rewritten by the next step
-        m = (u32)min((u64)m, ntiles - base);
-        if (m == 0) {  // the frontier has not moved: wait a little (bounded)
-            const u64 t = uniform_i64((i64)now_ticks());
-            if (idle_since == 0) idle_since = t;
-            if (t - idle_since > kWaitTicks) return;  // the copiers resolve the rest by look-back
-            __builtin_amdgcn_s_sleep(2);
-            continue;
-        }
-        idle_since = 0;
-#pragma unroll
-        for (int f = 0; f < NV; ++f) {
-            u64 x[kPer], sum = 0;
-#pragma unroll
-            for (int k = 0; k < kPer; ++k) {
-                x[k] = (u32)(tid * kPer + k) < m ? v[f][k] & kValMask : 0;
-                sum += x[k];
-            }
-            const u64 inc = wave_incl_scan_u64(sum, lane);
-            if (lane == 63) S.red[wave] = inc;
-            lds_barrier();
-            u64 wpre = 0, tot = 0;
-#pragma unroll
-            for (int q = 0; q < kW; ++q) {
-                const u64 t = S.red[q];
-                if (q < wave) wpre += t;
-                tot += t;
-            }
-            lds_barrier();  // S.red is rewritten for the next column / step
-            u64 run = carry[f] + wpre + inc - sum;
-#pragma unroll
-            for (int k = 0; k < kPer; ++k) {
-                if ((u32)(tid * kPer + k) < m) {
-                    store_word(&pw[(size_t)f * ntiles + t0 + k], make_word(epoch, kStPre, run));
-                    if (dbg && f == 0) dbg[(t0 + k) * 8 + 5] = now_ticks();  // tuning timelines only
-                }
-                run += x[k];
-            }
-            carry[f] += tot;
-        }
-        base += m;
-    }
-}
 
 // ---------------------------------------------------------------- look-back (the fallback)
 // Field lengths of record r with Go's checks (kv.syn.go:681-745, echo.syn.go:223-231), read straight
@@ -375,51 +271,11 @@ __device__ void tile_agg_global(const DecodeParams& p, u64 tile, u64 (&agg)[NV])
     for (int f = 0; f < NV; ++f) agg[f] = (u64)uniform_i64((i64)wave_sum_u64(flen[f]));
 }
 
-// Exclusive prefix of `tile` per column (wave 0 of its copier; lane k looks at tile hi - k).  The
-// nearest earlier tile with a published prefix word ends the walk: prefix = its prefix + its
-// aggregate + the aggregates of the tiles in between.  Never waits: a missing aggregate is computed
-// here and published.
+// Exclusive prefix of `tile` per column (wave 0 of its copier): pipe_words.hpp lookback_with, a
+// missing aggregate parsed from HBM.
 template <int NF, int NV, bool MIX>
 __device__ void lookback(const DecodeParams& p, u64* aw, u64* pw, u64 ntiles, u64 tile, u32 epoch, i64 (&pre)[NV]) {
-    const int lane = threadIdx.x & 63;
-    u64 sum[NV];
-#pragma unroll
-    for (int f = 0; f < NV; ++f) sum[f] = 0;
-    for (i64 hi = (i64)tile - 1; hi >= 0; hi -= 64) {  // wave-uniform loop
-        const i64 t = hi - lane;
-        const bool valid = t >= 0;
-        u64 pv[NV], av[NV];
-        bool hp = valid, ha = valid;
-#pragma unroll
-        for (int f = 0; f < NV; ++f) {
-            pv[f] = valid ? load_word(&pw[(size_t)f * ntiles + t]) : 0;
-            av[f] = valid ? load_word(&aw[(size_t)f * ntiles + t]) : 0;
-            hp = hp && tagged(pv[f], epoch);
-            ha = ha && tagged(av[f], epoch);
-        }
-        const u64 pm = __ballot(hp);
-        const int stop = pm ? (int)__builtin_ctzll(pm) : 64;  // lanes [0, stop] contribute
-        u64 need = __ballot(valid && lane <= stop && !ha);
-        while (need) {  // wave-uniform
-            const int k = (int)__builtin_ctzll(need);
-            need &= need - 1;
-            u64 a[NV];
-            tile_agg_global<NF, NV, MIX>(p, (u64)(hi - k), a);
-#pragma unroll
-            for (int f = 0; f < NV; ++f) {
-                if (lane == k) av[f] = make_word(epoch, kStAgg, a[f]);
-                if (lane == 0) store_word(&aw[(size_t)f * ntiles + (u64)(hi - k)], make_word(epoch, kStAgg, a[f]));
-            }
-        }
-#pragma unroll
-        for (int f = 0; f < NV; ++f) {
-            const u64 c = valid && lane <= stop ? (av[f] & kValMask) + (lane == stop ? pv[f] & kValMask : 0) : 0;
-            sum[f] += (u64)uniform_i64((i64)wave_sum_u64(c));
-        }
-        if (pm) break;
-    }
-#pragma unroll
-    for (int f = 0; f < NV; ++f) pre[f] = (i64)sum[f];
+    lookback_with<NV>(aw, pw, ntiles, tile, epoch, pre, [&](u64 t, u64 (&a)[NV]) { tile_agg_global<NF, NV, MIX>(p, t, a); });
 }
 
 // ---------------------------------------------------------------- the kernel
@@ -725,10 +581,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
 constexpr int kGWin = 96;  // parse window bytes per record
 constexpr int kGU = 4;     // output chunks per lane per step
 
-struct ScanLds {  // the scanner's scratch (scanner() needs red / first)
-    u64 red[4];
-    int first[4];
-};
 
 template <int NV>
 struct GatherLds {
@@ -1058,7 +910,8 @@ hipError_t launch_layout(const DecodeParams& p, u64* flags, u32 epoch, hipStream
 }  // namespace pipe
 
 size_t decode_pipe_flag_bytes(int nvar, uint64_t n) {
-    // aggregate + prefix word per column and tile; >= 256 bytes: the kernels' filler load address
+    // aggregate + prefix word per column and tile, then 256 bytes: the scanner's store sink
+    // (pipe_words.hpp); the start doubles as the kernels' filler load address
     return ((size_t)nvar * 2 * pipe::num_tiles(n) * sizeof(u64) + 256 + 255) & ~(size_t)255;
 }
 

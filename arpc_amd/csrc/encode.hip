@@ -23,8 +23,10 @@
 //    One global_store_dwordx4 per chunk, consecutive lanes on consecutive chunks: every
 //    wave store instruction writes 1 KiB of whole lines.  Only the partial chunks at a
 //    tile's two edges use byte stores, so nothing is read-modify-written.
+#include "../../include/symphony_hip.h"
 #include "codec.hpp"
 #include "device_util.hpp"
+#include "pipe_words.hpp"
 
 namespace symhip {
 
@@ -35,6 +37,140 @@ constexpr int kGroupShift = 4; // mixed batches: 2^kGroupShift tiles per size-pa
 // Header slot for H0 header bytes: a 16-byte window starting at any b < H0 stays in the slot,
 // and one starting up to 15 bytes before a slot reads only the previous slot's zero tail.
 constexpr int slot_bytes(int H0) { return ((H0 + 16) + 7) & ~7; }
+
+// ---------------------------------------------------------------- mixed Get/Set batches: record sizes
+// Record sizes depend on the type column, so record offsets are a scan.  One launch
+// (encode_pipe_kernel) runs it the way the default decode does (decode_pipe.hip), with three roles
+// by workgroup index, over epoch-tagged words in the ctx's flag buffer (pipe_words.hpp):
+//   [0, P)     sizers: workgroup takes a group of kPipeGroup 64-record tiles, computes every tile's
+//              byte total, publishes each tile's exclusive prefix inside the group (a "local" word)
+//              and the group's total (an aggregate word); groups g, g + P, ...  Never wait.
+//   P          scanner: chains the group aggregates into exclusive group prefix words.
+//   P + 1 + t  encode tile t: its stream position = group prefix + local prefix, both loaded when
+//              the tile starts (normally published long before).  A word still missing after
+//              kFallbackTicks is resolved by the tile itself (look-back over the group words, the
+//              local prefix recomputed), so progress never depends on residency.
+// Layout (u64 words): aggregate[ngroups], prefix[ngroups], 32 words of scanner store sink, local[ntiles].
+constexpr int kPipeGroup = 8;  // tiles per sizer group (512 records)
+__host__ __device__ static inline u64 mixed_ntiles(u64 n) { return (n + 63) / 64; }
+__host__ __device__ static inline u64 mixed_npgroups(u64 n) { return (mixed_ntiles(n) + kPipeGroup - 1) / kPipeGroup; }
+struct PipeWords {
+    u64 *aw, *pw, *lw;
+    u64 ng, nt;
+};
+__device__ __forceinline__ PipeWords pipe_words(const EncodeParams& p) {
+    PipeWords w;
+    w.nt = mixed_ntiles(p.n);
+    w.ng = mixed_npgroups(p.n);
+    w.aw = (u64*)p.flags;
+    w.pw = w.aw + w.ng;
+    w.lw = w.pw + w.ng + 32;  // <= 2 ng + 32 + nt <= 4 nt + 32 words: within decode_pipe_flag_bytes(2, n)
+    return w;
+}
+
+// Byte totals of 64-record tiles t[k] (< ntiles), whole wave, wave-uniform result: 22 + K bytes per
+// record (kv.syn.go:74-132) plus 8 + V per SetRequest (:611-678); K from the key offsets at the
+// tile's edges.  Every load of the R tiles is in flight before any is used.
+template <int R>
+__device__ __forceinline__ void mixed_tile_totals(const EncodeParams& p, const u64 (&t)[R], u64 (&agg)[R]) {
+    const int lane = threadIdx.x & 63;
+    const u64 n = p.n;
+    uint8_t ty[R];
+    u64 v0[R], v1[R], ke[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        const u64 a = t[k] * 64, b = min(a + 64, n);
+        const u64 r = min(a + lane, n - 1);
+        ty[k] = p.type[r];
+        v0[k] = p.offs[1][r];
+        v1[k] = p.offs[1][r + 1];
+        ke[k] = p.offs[0][lane == 0 ? a : b];  // lanes 0 and 1: the key offsets at the tile's edges
+    }
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        const u64 a = t[k] * 64, b = min(a + 64, n);
+        const u32 extra = a + lane < b && ty[k] != 0 ? (u32)(8 + (v1[k] - v0[k])) : 0u;  // < 2^32 (u32 lengths)
+        const u64 sets = pipe::lane_u64_pub(wave_incl_scan_u32w_dpp(extra), 63);
+        const u64 keys = pipe::lane_u64_pub(ke[k], 1) - pipe::lane_u64_pub(ke[k], 0);
+        agg[k] = 22 * (b - a) + keys + sets;
+    }
+}
+
+// Sizer role: one group per step (wave w sizes tiles 2w, 2w + 1 of it).
+__device__ void mixed_sizer(const EncodeParams& p, const PipeWords& W, u64* s_tot) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (u64 g = blockIdx.x; g < W.ng; g += p.pipe_sizers) {
+        const u64 tb = g * kPipeGroup + 2 * (u64)wave;
+        u64 t[2], agg[2];
+        t[0] = min(tb, W.nt - 1);
+        t[1] = min(tb + 1, W.nt - 1);
+        mixed_tile_totals<2>(p, t, agg);
+        if (lane < 2) s_tot[2 * wave + lane] = tb + lane < W.nt ? agg[lane] : 0;
+        __syncthreads();
+        if (wave == 0 && lane < kPipeGroup) {
+            u64 excl = 0, tot = 0;
+#pragma unroll
+            for (int k = 0; k < kPipeGroup; ++k) {
+                const u64 x = s_tot[k];
+                excl += k < lane ? x : 0;
+                tot += x;
+            }
+            const u64 tile = g * kPipeGroup + lane;
+            if (tile < W.nt) pipe::store_word(&W.lw[tile], pipe::make_word(p.epoch, pipe::kStAgg, excl));
+            if (lane == 0) {
+                pipe::store_word(&W.aw[g], pipe::make_word(p.epoch, pipe::kStAgg, tot));
+                if (p.dbg) p.dbg[(W.nt + g) * 8 + 4] = pipe::now_ticks();  // tools/mixed_timeline.py
+            }
+        }
+        __syncthreads();  // s_tot is rewritten for the next group
+    }
+}
+
+// Byte total of tiles [t0, t1) (whole wave, wave-uniform; t1 - t0 <= kPipeGroup).
+__device__ u64 mixed_range_total(const EncodeParams& p, u64 t0, u64 t1) {
+    u64 sum = 0;
+    for (u64 t = t0; t < t1; ++t) {
+        const u64 tt[1] = {t};
+        u64 a[1];
+        mixed_tile_totals<1>(p, tt, a);
+        sum += a[0];
+    }
+    return sum;
+}
+
+// The stream position of mixed tile `tile` (wave 0 of its workgroup).  wg / wl: its group's prefix
+// word and its local word, as loaded when the tile started.
+__device__ i64 mixed_tile_prefix(const EncodeParams& p, u64 tile, u64 wg, u64 wl) {
+    const u32 ep = p.epoch;
+    if (__builtin_amdgcn_readfirstlane(pipe::tagged(wg, ep) && pipe::tagged(wl, ep)))
+        return uniform_i64((i64)((wg & pipe::kValMask) + (wl & pipe::kValMask)));
+    const int lane = threadIdx.x & 63;
+    const PipeWords W = pipe_words(p);
+    const u64 g = tile / kPipeGroup;
+    if (!p.pipe_lookback && lane == 0) {
+        for (const u64 t0 = pipe::now_ticks(); !(pipe::tagged(wg, ep) && pipe::tagged(wl, ep)) &&
+                                               pipe::now_ticks() - t0 <= pipe::kFallbackTicks;) {
+            __builtin_amdgcn_s_sleep(2);
+            if (!pipe::tagged(wg, ep)) wg = pipe::load_word(&W.pw[g]);
+            if (!pipe::tagged(wl, ep)) wl = pipe::load_word(&W.lw[tile]);
+        }
+    }
+    wg = pipe::lane_u64_pub(wg, 0);
+    wl = pipe::lane_u64_pub(wl, 0);
+    u64 gpre, lpre;
+    if (pipe::tagged(wg, ep)) {
+        gpre = wg & pipe::kValMask;
+    } else {  // resolve the group prefix here (never waits) and publish it
+        i64 pre[1];
+        pipe::lookback_with<1>(W.aw, W.pw, W.ng, g, ep, pre, [&](u64 gi, u64 (&a)[1]) {
+            a[0] = mixed_range_total(p, gi * kPipeGroup, min((gi + 1) * kPipeGroup, W.nt));
+        });
+        gpre = (u64)pre[0];
+        if (lane == 0) pipe::store_word(&W.pw[g], pipe::make_word(ep, pipe::kStPre, gpre));
+    }
+    lpre = pipe::tagged(wl, ep) ? wl & pipe::kValMask : mixed_range_total(p, g * kPipeGroup, tile);
+    return uniform_i64((i64)(gpre + lpre));
+}
 
 // A tile's stream span must stay below 2^31 (64 records; positions are 32-bit), and string
 // fields are < 2^32 bytes (Symphony's u32 length prefix).
@@ -61,8 +197,13 @@ struct EncWaveLds {
 // TR: records per tile (64, or 128 with whole-workgroup tiles: waves 0 and 1 build the headers of
 // 64 records each, so a tile of short records -- mixed Get/Set batches -- moves about as many bytes
 // as a 64-record tile of SetRequests).
-template <int NF, int NV, int kVariant, bool MIXED = false, int WPT = 1, bool DIAG = false, int TR = kWaveRecs>
-__global__ __launch_bounds__(256) void encode_kernel(EncodeParams p) {
+// PIPE (mixed batches, workgroup tiles): the one-launch size scan above -- blocks [0, P) are sizers,
+// block P the scanner, block P + 1 + t encodes tile t (P = p.pipe_sizers; no sizers or scanner when
+// p.pipe_lookback).  SSK: the scanner's tiles per thread per step.
+template <int NF, int NV, int kVariant, bool MIXED = false, int WPT = 1, bool DIAG = false, int TR = kWaveRecs,
+          bool PIPE = false, int SSK = 8>
+__device__ __forceinline__ void encode_body(const EncodeParams& p) {
+    static_assert(!PIPE || (MIXED && WPT == kWaves && TR == kWaveRecs), "the pipelined size scan is for mixed 64-record workgroup tiles");
     static_assert(!MIXED || (NF == 0 && NV == 2 && kVariant <= 1), "mixed batches are kv Get/Set");
     static_assert(WPT == 1 || (WPT == kWaves && kVariant <= 1), "whole-workgroup tiles take one step per wave");
     static_assert(TR == kWaveRecs || (TR == 2 * kWaveRecs && WPT == kWaves), "128-record tiles are workgroup tiles");
@@ -76,13 +217,30 @@ __global__ __launch_bounds__(256) void encode_kernel(EncodeParams p) {
     __shared__ EncWaveLds<NV, SLOT, TR> lds_all[kWaves / WPT];
     __shared__ uint8_t flags_all[kWaves][64];  // record-start marks of one phase-2 step, per wave
     __shared__ MaskTable masks;
+    u64 blk = blockIdx.x;
+    if constexpr (PIPE) {
+        if (!p.pipe_lookback) {
+            const PipeWords W = pipe_words(p);
+            if (blockIdx.x < p.pipe_sizers) {
+                __shared__ u64 s_tot[kPipeGroup];
+                mixed_sizer(p, W, s_tot);
+                return;
+            }
+            if (blockIdx.x == p.pipe_sizers) {
+                __shared__ pipe::ScanLds SL;
+                pipe::scanner<1, SSK>(W.aw, W.pw, W.ng, p.epoch, SL, DIAG ? p.dbg + W.nt * 8 : nullptr);  // 256 * SSK groups per step
+                return;
+            }
+            blk = blockIdx.x - p.pipe_sizers - 1;
+        }
+    }
     mask_table_init(masks, threadIdx.x);
     __syncthreads();
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     EncWaveLds<NV, SLOT, TR>& S = lds_all[WPT == 1 ? wave : 0];
     uint8_t* const flg = flags_all[wave];
-    const u64 r0 = (WPT == 1 ? (u64)blockIdx.x * kWaves + wave : (u64)blockIdx.x) * TR;
+    const u64 r0 = (WPT == 1 ? blk * kWaves + wave : blk) * TR;
     if (r0 >= p.n) return;  // wave-uniform (workgroup-uniform when WPT > 1)
     const int cnt = (int)min((u64)TR, p.n - r0);
     flg[lane] = 0;
@@ -116,7 +274,13 @@ __global__ __launch_bounds__(256) void encode_kernel(EncodeParams p) {
             part_safe = part_safe && t0 >= c0 + 16 && t1 + 16 <= c1;
         }
         if constexpr (MIXED) {
-            // sizes depend on the type: the size pass's prefix of this 64-record part plus a wave scan
+            // sizes depend on the type: the size scan's prefix of this 64-record part plus a wave scan
+            u64 wg = 0, wl = 0;  // PIPE: the prefix words, loaded first so their round trip overlaps the size loads
+            if constexpr (PIPE) {
+                const PipeWords W = pipe_words(p);
+                wg = pipe::load_word(&W.pw[rb / kWaveRecs / kPipeGroup]);
+                wl = pipe::load_word(&W.lw[rb / kWaveRecs]);
+            }
             if (lane < hcnt) {
                 const u64 r = rb + lane;
                 isset = p.type[r] != 0;
@@ -124,9 +288,16 @@ __global__ __launch_bounds__(256) void encode_kernel(EncodeParams p) {
                 if (isset) L[1] = p.offs[1][r + 1] - p.offs[1][r];
                 size = (i64)(22 + L[0] + (isset ? 8 + L[1] : 0));
             }
-            const u64 part = rb / kWaveRecs;  // the size pass's 64-record tiles
-            const i64 tp = uniform_i64((i64)(p.group_pre[part >> kGroupShift] + p.tile_loc[part]));
-            o = tp + (i64)(wave_incl_scan_u64((u64)size, lane) - (u64)size);
+            const u64 part = rb / kWaveRecs;  // the size scan's 64-record tiles
+            const u64 incl = wave_incl_scan_u64((u64)size, lane);
+            i64 tp;
+            if constexpr (PIPE) {
+                tp = mixed_tile_prefix(p, part, wg, wl);
+                if (DIAG && lane == 0) stamp[7] = __builtin_amdgcn_s_memrealtime();
+            } else {
+                tp = uniform_i64((i64)(p.group_pre[part >> kGroupShift] + p.tile_loc[part]));
+            }
+            o = tp + (i64)(incl - (u64)size);
             if (lane < hcnt) {
                 const u64 r = rb + lane;
 #pragma unroll
@@ -457,6 +628,19 @@ __global__ __launch_bounds__(256) void encode_kernel(EncodeParams p) {
     }
 }
 
+template <int NF, int NV, int kVariant, bool MIXED = false, int WPT = 1, bool DIAG = false, int TR = kWaveRecs>
+__global__ __launch_bounds__(256) void encode_kernel(EncodeParams p) {
+    encode_body<NF, NV, kVariant, MIXED, WPT, DIAG, TR>(p);
+}
+
+// The one-launch mixed encode: its role code (sizer, scanner, look-back) would otherwise lift the
+// kernel past 64 VGPRs, i.e. from 8 to 6 waves per SIMD, and the encode tiles are latency-bound
+// (tools/mixed_timeline.py: resident tiles x lifetime sets the rate).
+template <bool DIAG = false, int SSK = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void encode_pipe_kernel(EncodeParams p) {
+    encode_body<0, 2, 1, true, kWaves, DIAG, kWaveRecs, true, SSK>(p);
+}
+
 static dim3 encode_grid(u64 n, int wpt) {
     const u64 tiles = (n + kWaveRecs - 1) / kWaveRecs;
     return dim3((unsigned)(wpt == 1 ? (tiles + kWaves - 1) / kWaves : tiles));
@@ -504,11 +688,20 @@ hipError_t launch_encode(const EncodeParams& p, hipStream_t stream) {
 }
 
 // ---------------------------------------------------------------- mixed Get/Set batches
-// Record sizes depend on the type column, so record offsets are a scan.  The size pass reads the
-// type bytes and the value offsets (Σ over Sets of 8 + V; keys contribute 22 + K per record, taken
-// from the key offsets at tile edges) and writes, per 64-record tile, its exclusive size prefix
-// inside its group of kGroupTiles tiles, and per group its total; one workgroup then scans the
-// group totals.  The encode kernel starts tile t at group_pre[t >> kGroupShift] + tile_loc[t].
+static int device_cus() {
+    static int cus[16] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    int& ncu = cus[dev & 15];
+    if (ncu == 0 && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) ncu = 0;
+    return ncu;
+}
+
+// SYM_ENCODE_THREE_KERNEL: the size scan as two launches before the encode (no inter-workgroup
+// waiting at all).  The size pass reads the type bytes and the value offsets and writes, per 64-record
+// tile, its exclusive size prefix inside its group of kGroupTiles tiles, and per group its total;
+// one workgroup then scans the group totals.  The encode kernel starts tile t at
+// group_pre[t >> kGroupShift] + tile_loc[t].
 constexpr int kGroupTiles = 1 << kGroupShift;   // tiles per size-pass workgroup (1024 records)
 constexpr int kTilesPerWave = kGroupTiles / 4;  // 4
 
@@ -517,7 +710,6 @@ struct MixedWs {
     u64* tile_loc;
     u64* group_tot;
 };
-__host__ __device__ static inline u64 mixed_ntiles(u64 n) { return (n + kWaveRecs - 1) / kWaveRecs; }
 __host__ __device__ static inline u64 mixed_ngroups(u64 n) { return (mixed_ntiles(n) + kGroupTiles - 1) / kGroupTiles; }
 static MixedWs mixed_layout(void* ws, u64 n) {
     MixedWs w;
@@ -602,28 +794,68 @@ __global__ __launch_bounds__(256) void mixed_group_scan_kernel(MixedWs w, u64 ng
     }
 }
 
-hipError_t launch_encode_mixed(EncodeParams p, void* ws, hipStream_t stream) {
-    if (p.n == 0) return hipMemsetAsync(p.out_off, 0, sizeof(uint64_t), stream);
-    if (!p.type || p.lay.nfixed != 0 || p.lay.nvar != 2) return hipErrorInvalidValue;
+static void launch_encode_mixed_3(EncodeParams p, void* ws, hipStream_t stream) {
     const MixedWs w = mixed_layout(ws, p.n);
     hipLaunchKernelGGL(mixed_size_kernel, dim3((unsigned)mixed_ngroups(p.n)), dim3(256), 0, stream, p, w);
     hipLaunchKernelGGL(mixed_group_scan_kernel, dim3(1), dim3(256), 0, stream, w, mixed_ngroups(p.n));
     p.group_pre = w.group_pre;
     p.tile_loc = w.tile_loc;
 #ifdef SYMHIP_TUNING
-    if (p.variant == 20) {  // 128-record workgroup tiles
-        const u64 t128 = (p.n + 127) / 128;
-        hipLaunchKernelGGL((encode_kernel<0, 2, 1, true, kWaves, false, 2 * kWaveRecs>), dim3((unsigned)t128),
-                           dim3(64 * kWaves), 0, stream, p);
-        return hipGetLastError();
-    }
-    if (p.variant == 5 || p.variant == 15) {
-        if (p.variant == 5) hipLaunchKernelGGL((encode_kernel<0, 2, 0, true>), encode_grid(p.n, 1), dim3(64 * kWaves), 0, stream, p);
-        else hipLaunchKernelGGL((encode_kernel<0, 2, 0, true, kWaves>), encode_grid(p.n, kWaves), dim3(64 * kWaves), 0, stream, p);
-        return hipGetLastError();
+    switch (p.variant) {
+        case 20:  // 128-record workgroup tiles
+            hipLaunchKernelGGL((encode_kernel<0, 2, 1, true, kWaves, false, 2 * kWaveRecs>), dim3((unsigned)((p.n + 127) / 128)),
+                               dim3(64 * kWaves), 0, stream, p);
+            return;
+        case 5: hipLaunchKernelGGL((encode_kernel<0, 2, 0, true>), encode_grid(p.n, 1), dim3(64 * kWaves), 0, stream, p); return;
+        case 38: hipLaunchKernelGGL((encode_kernel<0, 2, 1, true, kWaves, true>), encode_grid(p.n, kWaves), dim3(64 * kWaves), 0, stream, p); return;  // + timestamps
+        case 15: hipLaunchKernelGGL((encode_kernel<0, 2, 0, true, kWaves>), encode_grid(p.n, kWaves), dim3(64 * kWaves), 0, stream, p); return;
+        default: break;
     }
 #endif
     hipLaunchKernelGGL((encode_kernel<0, 2, 1, true, kWaves>), encode_grid(p.n, kWaves), dim3(64 * kWaves), 0, stream, p);
+}
+
+hipError_t launch_encode_mixed(EncodeParams p, void* ws, hipStream_t stream) {
+    if (p.n == 0) return hipMemsetAsync(p.out_off, 0, sizeof(uint64_t), stream);
+    if (!p.type || p.lay.nfixed != 0 || p.lay.nvar != 2) return hipErrorInvalidValue;
+    int impl = p.impl;
+#ifdef SYMHIP_TUNING
+    if (p.variant == 5 || p.variant == 15 || p.variant == 20 || p.variant == 38 || p.variant == 40) impl = SYM_ENCODE_THREE_KERNEL;  // 40: its default kernel
+#endif
+    if (impl == SYM_ENCODE_THREE_KERNEL) {
+        if (!ws) return hipErrorInvalidValue;
+        launch_encode_mixed_3(p, ws, stream);
+        return hipGetLastError();
+    }
+    if (!p.flags || p.epoch == 0) return hipErrorInvalidValue;
+    const u64 nt = mixed_ntiles(p.n);
+    const int ncu = device_cus();
+    if (ncu <= 0) return hipErrorInvalidDevice;
+    u64 P = (u64)ncu / 2;  // sizers: one per 2 CUs (kPipeGroup tiles per workgroup step)
+    p.pipe_lookback = impl == SYM_ENCODE_LOOKBACK;
+#ifdef SYMHIP_TUNING
+    if (p.variant == 30) P = (u64)ncu / 4;
+    if (p.variant == 31) P = (u64)ncu;
+#endif
+    if (P > mixed_npgroups(p.n)) P = mixed_npgroups(p.n);
+    p.pipe_sizers = (unsigned)P;
+    const u64 grid = p.pipe_lookback ? nt : P + 1 + nt;
+    if (grid > 0xFFFFFFFFull) return hipErrorInvalidValue;
+#ifdef SYMHIP_TUNING
+    if (p.variant == 37) {  // per-tile timestamps (tools/mixed_timeline.py): p.dbg holds 16 u64 per tile
+        if (!p.dbg) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((encode_pipe_kernel<true>), dim3((unsigned)grid), dim3(64 * kWaves), 0, stream, p);
+        return hipGetLastError();
+    }
+    if (p.variant == 34 || p.variant == 35 || p.variant == 36) {  // scanner steps of 512 / 1024 / 2048 groups (default 256)
+        if (p.variant == 34) hipLaunchKernelGGL((encode_pipe_kernel<false, 2>), dim3((unsigned)grid), dim3(64 * kWaves), 0, stream, p);
+        if (p.variant == 35) hipLaunchKernelGGL((encode_pipe_kernel<false, 4>), dim3((unsigned)grid), dim3(64 * kWaves), 0, stream, p);
+        if (p.variant == 36) hipLaunchKernelGGL((encode_pipe_kernel<false, 8>), dim3((unsigned)grid), dim3(64 * kWaves), 0, stream, p);
+        return hipGetLastError();
+    }
+#endif
+    hipLaunchKernelGGL((encode_pipe_kernel<>), dim3((unsigned)grid),
+                       dim3(64 * kWaves), 0, stream, p);
     return hipGetLastError();
 }
 

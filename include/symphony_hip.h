@@ -104,6 +104,16 @@ int sym_ctx_check(sym_ctx* ctx, void* stream);
 #define SYM_DECODE_THREE_KERNEL 1
 #define SYM_DECODE_LOOKBACK 2
 int sym_ctx_set_decode_impl(sym_ctx* ctx, int impl);
+/* Size-scan implementation of this ctx's mixed Get/Set encodes (sym_encode_kv_mixed; identical results):
+ *   SYM_ENCODE_PIPELINE     (default) one launch: sizer workgroups publish every 64-record tile's byte
+ *                           total, a scanner workgroup chains them into prefixes, encode workgroups
+ *                           wait for theirs (up to 1 ms, then resolve it by a look-back that never waits).
+ *   SYM_ENCODE_THREE_KERNEL size pass -> group scan -> encode, three stream-ordered launches.
+ *   SYM_ENCODE_LOOKBACK     the one launch without sizers or scanner: every tile looks back (testing). */
+#define SYM_ENCODE_PIPELINE 0
+#define SYM_ENCODE_THREE_KERNEL 1
+#define SYM_ENCODE_LOOKBACK 2
+int sym_ctx_set_encode_impl(sym_ctx* ctx, int impl);
 
 /* ---- schema metadata (host-side, no GPU needed) -------------------------------- */
 int sym_schema_info(int schema, int* nfixed, int* nvar);

@@ -133,19 +133,23 @@ def _gpu_decode(codec, dev, stream, rec_off, rtype, misalign=0):
     return cols, out.status.cpu().numpy()[:n]
 
 
-DECODE_IMPLS = {"pipe": 0, "three_kernel": 1, "lookback": 2}
+# SYM_DECODE_* and SYM_ENCODE_* (include/symphony_hip.h): the same three shapes for the decode's and
+# the mixed encode's scans -- one pipelined launch, three launches, the launch's look-back fallback
+IMPLS = {"pipe": 0, "three_kernel": 1, "lookback": 2}
 
 
-@pytest.fixture(params=sorted(DECODE_IMPLS))
+@pytest.fixture(params=sorted(IMPLS))
 def impl(request, codec):
-    codec.set_decode_impl(DECODE_IMPLS[request.param])
+    codec.set_decode_impl(IMPLS[request.param])
+    codec.set_encode_impl(IMPLS[request.param])
     yield request.param
     codec.set_decode_impl(0)
+    codec.set_encode_impl(0)
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("ids", [False, True])
-def test_gpu_mixed_kat(codec, dev, kats, ids):
+def test_gpu_mixed_kat(codec, dev, impl, kats, ids):
     idt = (1, 1, 2) if ids else (0, 0, 0)
     got, off = _gpu_encode(codec, dev, KAT_TYPES, _cols(KAT_KEYS), _cols(KAT_VALS), idt, misalign=3, out_misalign=7)
     assert got.tobytes().hex() == kat_stream(kats, ids)
@@ -271,7 +275,7 @@ def test_gpu_mixed_short_type_column_rejected(codec, dev):
 
 
 @pytest.mark.gpu
-def test_gpu_mixed_many_groups_offsets(codec, dev):
+def test_gpu_mixed_many_groups_offsets(codec, dev, impl):
     """More than 4096 size-pass groups (1024 records each), so the one-workgroup group scan takes a
     second round: 4.3M small Get/Set records; offsets equal the cumulative record sizes, and the
     decode returns every column."""
