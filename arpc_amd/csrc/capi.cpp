@@ -250,7 +250,7 @@ int symhip::capi::encode_call(sym_ctx* ctx, int schema, uint64_t n, const int32_
 #ifdef SYMHIP_TUNING
     p.variant = symhip::tuning_variant("SYMHIP_ENCODE_VARIANT");
     if (const char* d = getenv("SYMHIP_DEBUG_PTR")) p.dbg = (uint64_t*)(uintptr_t)strtoull(d, nullptr, 16);
-    if ((p.variant == 6 || p.variant == 7 || p.variant == 10) && !p.dbg) return fail(SYM_ERR_INVALID, "encode timeline needs SYMHIP_DEBUG_PTR");
+    if ((p.variant == 6 || p.variant == 7 || p.variant == 10 || p.variant == 53) && !p.dbg) return fail(SYM_ERR_INVALID, "encode timeline needs SYMHIP_DEBUG_PTR");
 #endif
     DeviceGuard g(ctx->device);
     if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
@@ -435,7 +435,7 @@ int sym_encode_kv_mixed(sym_ctx* ctx, const uint8_t* d_type, const uint8_t* d_ke
     p.impl = ctx->encode_impl;
 #ifdef SYMHIP_TUNING
     p.variant = symhip::tuning_variant("SYMHIP_ENCODE_VARIANT");
-    if (p.variant == 37 || p.variant == 38) {  // tools/mixed_timeline.py: 16 u64 per 64-record tile
+    if (p.variant == 37 || p.variant == 38 || p.variant == 52) {  // tools/mixed_timeline.py: 16 u64 per 64-record tile
         if (const char* d = getenv("SYMHIP_DEBUG_PTR")) p.dbg = (uint64_t*)(uintptr_t)strtoull(d, nullptr, 16);
         if (!p.dbg) return fail(SYM_ERR_INVALID, "mixed encode timeline needs SYMHIP_DEBUG_PTR");
     }

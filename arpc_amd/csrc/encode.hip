@@ -200,56 +200,58 @@ struct EncWaveLds {
 // PIPE (mixed batches, workgroup tiles): the one-launch size scan above -- blocks [0, P) are sizers,
 // block P the scanner, block P + 1 + t encodes tile t (P = p.pipe_sizers; no sizers or scanner when
 // p.pipe_lookback).  SSK: the scanner's tiles per thread per step.
-template <int NF, int NV, int kVariant, bool MIXED = false, int WPT = 1, bool DIAG = false, int TR = kWaveRecs,
-          bool PIPE = false, int SSK = 8>
-__device__ __forceinline__ void encode_body(const EncodeParams& p) {
-    static_assert(!PIPE || (MIXED && WPT == kWaves && TR == kWaveRecs), "the pipelined size scan is for mixed 64-record workgroup tiles");
-    static_assert(!MIXED || (NF == 0 && NV == 2 && kVariant <= 1), "mixed batches are kv Get/Set");
-    static_assert(WPT == 1 || (WPT == kWaves && kVariant <= 1), "whole-workgroup tiles take one step per wave");
-    static_assert(TR == kWaveRecs || (TR == 2 * kWaveRecs && WPT == kWaves), "128-record tiles are workgroup tiles");
+
+// The prefetching encode (PF): one tile's input rows staged in LDS by global_load_lds while the
+// previous tile is copied -- offsets [rb, rb + 64] of every string column (as dwords: three
+// 64-lane dword loads, 130 dwords used), the type bytes (mixed batches), the int32 fields.
+template <int NF, int NV>
+struct alignas(16) EncStage {
+    u32 offs[NV][3 * 64];
+    u32 type[64];  // a byte load lands in its lane's dword (LDS-DMA writes base + 4 * lane below dword size)
+    int32_t fixed[NF > 0 ? NF : 1][64];
+};
+template <int NF, int NV>
+__device__ __forceinline__ u64 stage_off(const EncStage<NF, NV>* s, int f, u64 i) {
+    return ((const u64*)s->offs[f])[i];
+}
+#define SYMHIP_LDS(ptr) ((__attribute__((address_space(3))) void*)(ptr))
+// Whole wave: issue the loads of tile rows [rb, rb + 64) into s (they land asynchronously; wait
+// with s_waitcnt vmcnt(0) before reading).  Source addresses are clamped into the columns.
+template <int NF, int NV, bool MIXED>
+__device__ __forceinline__ void enc_stage_issue(const EncodeParams& p, u64 rb, EncStage<NF, NV>& s, int lane) {
+    const u64 n = p.n;
+#pragma unroll
+    for (int f = 0; f < NV; ++f) {
+        const u32* src = (const u32*)p.offs[f];
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+            __builtin_amdgcn_global_load_lds((const void*)(src + min(2 * rb + (u64)(64 * k + lane), 2 * n + 1)),
+                                             SYMHIP_LDS(&s.offs[f][64 * k]), 4, 0, 0);
+    }
+    const u64 r = min(rb + (u64)lane, n - 1);
+    if constexpr (MIXED) __builtin_amdgcn_global_load_lds((const void*)(p.type + r), SYMHIP_LDS(s.type), 1, 0, 0);
+#pragma unroll
+    for (int f = 0; f < NF; ++f)
+        __builtin_amdgcn_global_load_lds((const void*)(p.fixed[f] + r), SYMHIP_LDS(s.fixed[f]), 4, 0, 0);
+}
+
+// Phase 1 of a tile (header waves; every wave calls it when HW > 1, for its barriers): per-record
+// offsets and header image into S.  stg: the staged rows (PF) or null (read from HBM); wg_in /
+// wl_in: the PIPE prefix words loaded with the staged rows (PF).
+
+#define OFF(f, r) (PF ? stage_off(stg, (f), (r) - rb) : p.offs[(f)][(r)])
+#define TYP(r) (PF ? (uint8_t)stg->type[(r) - rb] : p.type[(r)])
+#define FIX(f, r) (PF ? stg->fixed[(f)][(r) - rb] : p.fixed[(f)][(r)])
+template <int NF, int NV, bool MIXED, int WPT, bool DIAG, int TR, bool PIPE, bool PF>
+__device__ __forceinline__ void enc_phase1(const EncodeParams& p, EncWaveLds<NV, slot_bytes(14 + 4 * (NF + NV) + 4), TR>& S,
+                                           u64 r0, int cnt, int lane, int wave, u64* stamp,
+                                           const EncStage<NF, NV>* stg, u64 wg_in, u64 wl_in) {
     constexpr int HW = TR / kWaveRecs;  // waves that build headers
     constexpr int NT = NF + NV;
     constexpr int H0 = 14 + 4 * NT + 4;        // bytes before field 0's payload (the largest, in mixed batches)
     constexpr i64 OVH = 14 + 4 * NT + 4 * NV;  // fixed bytes per record
     constexpr int SLOT = slot_bytes(H0);
-    static_assert(SLOT - 16 >= H0 && OVH >= 16, "layout assumptions");
-
-    __shared__ EncWaveLds<NV, SLOT, TR> lds_all[kWaves / WPT];
-    __shared__ uint8_t flags_all[kWaves][64];  // record-start marks of one phase-2 step, per wave
-    __shared__ MaskTable masks;
-    u64 blk = blockIdx.x;
-    if constexpr (PIPE) {
-        if (!p.pipe_lookback) {
-            const PipeWords W = pipe_words(p);
-            if (blockIdx.x < p.pipe_sizers) {
-                __shared__ u64 s_tot[kPipeGroup];
-                mixed_sizer(p, W, s_tot);
-                return;
-            }
-            if (blockIdx.x == p.pipe_sizers) {
-                __shared__ pipe::ScanLds SL;
-                pipe::scanner<1, SSK>(W.aw, W.pw, W.ng, p.epoch, SL, DIAG ? p.dbg + W.nt * 8 : nullptr);  // 256 * SSK groups per step
-                return;
-            }
-            blk = blockIdx.x - p.pipe_sizers - 1;
-        }
-    }
-    mask_table_init(masks, threadIdx.x);
-    __syncthreads();
-
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    EncWaveLds<NV, SLOT, TR>& S = lds_all[WPT == 1 ? wave : 0];
-    uint8_t* const flg = flags_all[wave];
-    const u64 r0 = (WPT == 1 ? blk * kWaves + wave : blk) * TR;
-    if (r0 >= p.n) return;  // wave-uniform (workgroup-uniform when WPT > 1)
-    const int cnt = (int)min((u64)TR, p.n - r0);
-    flg[lane] = 0;
-    u64* const stamp = DIAG ? p.dbg + (r0 / kWaveRecs) * 8 : nullptr;  // tools/enc_timeline.py
-    if (DIAG && lane == 0 && (WPT == 1 || wave == 0)) {
-        stamp[0] = __builtin_amdgcn_s_memrealtime();
-        stamp[6] = blockIdx.x;
-    }
-
+    (void)OVH;
     // ---------------- phase 1: per-record offsets and header image ----------------
     // header wave h (h < HW) takes the tile's records [64 h, 64 h + 64): record rec = 64 h + lane
     const int hw = WPT == 1 ? 0 : wave;
@@ -270,22 +272,25 @@ __device__ __forceinline__ void encode_body(const EncodeParams& p) {
 #pragma unroll
         for (int f = 0; f < NV; ++f) {
             const u64 c0 = p.offs[f][0], c1 = p.offs[f][p.n];
-            const u64 t0 = p.offs[f][rb], t1 = p.offs[f][rb + hcnt];
+            const u64 t0 = OFF(f, rb), t1 = OFF(f, rb + hcnt);
             part_safe = part_safe && t0 >= c0 + 16 && t1 + 16 <= c1;
         }
         if constexpr (MIXED) {
             // sizes depend on the type: the size scan's prefix of this 64-record part plus a wave scan
             u64 wg = 0, wl = 0;  // PIPE: the prefix words, loaded first so their round trip overlaps the size loads
-            if constexpr (PIPE) {
+            if constexpr (PIPE && PF) {  // loaded with the staged rows
+                wg = wg_in;
+                wl = wl_in;
+            } else if constexpr (PIPE) {
                 const PipeWords W = pipe_words(p);
                 wg = pipe::load_word(&W.pw[rb / kWaveRecs / kPipeGroup]);
                 wl = pipe::load_word(&W.lw[rb / kWaveRecs]);
             }
             if (lane < hcnt) {
                 const u64 r = rb + lane;
-                isset = p.type[r] != 0;
-                L[0] = p.offs[0][r + 1] - p.offs[0][r];
-                if (isset) L[1] = p.offs[1][r + 1] - p.offs[1][r];
+                isset = TYP(r) != 0;
+                L[0] = OFF(0, r + 1) - OFF(0, r);
+                if (isset) L[1] = OFF(1, r + 1) - OFF(1, r);
                 size = (i64)(22 + L[0] + (isset ? 8 + L[1] : 0));
             }
             const u64 part = rb / kWaveRecs;  // the size scan's 64-record tiles
@@ -311,8 +316,8 @@ __device__ __forceinline__ void encode_body(const EncodeParams& p) {
             size = OVH;
 #pragma unroll
             for (int f = 0; f < NV; ++f) {
-                const u64 lo = p.offs[f][r];
-                L[f] = p.offs[f][r + 1] - lo;
+                const u64 lo = OFF(f, r);
+                L[f] = OFF(f, r + 1) - lo;
                 o += (i64)(lo - p.offs[f][0]);
                 size += (i64)L[f];
                 S.len[f][rec] = (u32)L[f];
@@ -373,7 +378,7 @@ __device__ __forceinline__ void encode_body(const EncodeParams& p) {
             int ps = h0;
 #pragma unroll
             for (int f = 0; f < NV; ++f) {
-                S.delta[f][rec] = (u64)(uintptr_t)(p.bytes[f] + p.offs[f][r]) - (u64)(i64)(orel + ps);
+                S.delta[f][rec] = (u64)(uintptr_t)(p.bytes[f] + OFF(f, r)) - (u64)(i64)(orel + ps);
                 ps += (int)L[f] + 4;
             }
             // header image: [0]=1 | [1:5]=13 | [5:9]=sid | [9:13]=mid | [13]=1 | table | len(field 0)
@@ -385,8 +390,8 @@ __device__ __forceinline__ void encode_body(const EncodeParams& p) {
             img_put_u32<5>(h, p.service_id);
             img_put_u32<9>(h, MIXED && !isset ? p.method_get : p.method_id);
             img_put_u8<13>(h, 1);
-            if constexpr (NF > 0) img_put_u32<14>(h, (u32)p.fixed[0][r]);
-            if constexpr (NF > 1) img_put_u32<18>(h, (u32)p.fixed[1][r]);
+            if constexpr (NF > 0) img_put_u32<14>(h, (u32)FIX(0, r));
+            if constexpr (NF > 1) img_put_u32<18>(h, (u32)FIX(1, r));
             // private-table entries: offset of the field's length prefix relative to privateStart
             // (13), truncated to u32 (kv.syn.go:664, :671).
             if (MIXED && !isset) {  // GetRequest{Key} (kv.syn.go:119-127)
@@ -404,11 +409,23 @@ __device__ __forceinline__ void encode_body(const EncodeParams& p) {
         }
         if (hw == 0 && lane < SLOT / 4) ((u32*)S.hdr)[lane] = 0;
     }
-    if constexpr (WPT == 1) wave_sync();
-    else __syncthreads();
-    if (!S.ok) return;  // uniform
-    if (DIAG && lane == 0 && (WPT == 1 || wave == 0)) stamp[1] = __builtin_amdgcn_s_memrealtime();
+}
+#undef OFF
+#undef TYP
+#undef FIX
 
+// Phase 2 of a tile: natural-order output chunks.  OW output waves take the steps round-robin;
+// this one is number ow.
+template <int NF, int NV, int kVariant, bool MIXED, int WPT, bool DIAG, int TR, int OW>
+__device__ __forceinline__ void enc_phase2(const EncodeParams& p, EncWaveLds<NV, slot_bytes(14 + 4 * (NF + NV) + 4), TR>& S,
+                                           int cnt, int lane, int wave, int ow, uint8_t* const flg, const MaskTable& masks,
+                                           u64* stamp) {
+    constexpr int HW = TR / kWaveRecs;  // waves that build headers
+    constexpr int NT = NF + NV;
+    constexpr int H0 = 14 + 4 * NT + 4;        // bytes before field 0's payload (the largest, in mixed batches)
+    constexpr i64 OVH = 14 + 4 * NT + 4 * NV;  // fixed bytes per record
+    constexpr int SLOT = slot_bytes(H0);
+    (void)OVH;
     // ---------------- phase 2: natural-order output chunks ----------------
     const i64 T0 = uniform_i64(S.t0);
     const int span = __builtin_amdgcn_readfirstlane(S.span);
@@ -512,7 +529,7 @@ __device__ __forceinline__ void encode_body(const EncodeParams& p) {
 
     if constexpr (kVariant == 1) {  // pipelined: step s+1's loads are in flight across step s's store
         if (!tile_safe) {
-            for (int B = first + 16 * 64 * (WPT == 1 ? 0 : wave); B < span; B += 16 * 64 * WPT) {
+            for (int B = first + 16 * 64 * ow; B < span; B += 16 * 64 * OW) {
                 const int j = locate(B);
                 const int P = B + 16 * lane;
                 if (P < span) chunk(P, j, true);
@@ -524,8 +541,8 @@ __device__ __forceinline__ void encode_body(const EncodeParams& p) {
         // a register set also consumes it and no value of a pending load reaches a join or a loop
         // head (the compiler would copy it there, waiting for every load in flight); steps past
         // kPipe run in a plain loop (the last pipelined fetch is then simply not used).
-        constexpr int kStep = 16 * 64 * WPT, kPipe = 8;
-        int B = first + 16 * 64 * (WPT == 1 ? 0 : wave);  // the next step to store
+        constexpr int kStep = 16 * 64 * OW, kPipe = 8;
+        int B = first + 16 * 64 * ow;  // the next step to store
         if (B < span) {
             u32x4 wa[NV], wb[NV];
             int ja = locate(B);
@@ -560,7 +577,7 @@ __device__ __forceinline__ void encode_body(const EncodeParams& p) {
         return;
     }
     if constexpr (kVariant == 0) {
-        for (int B = first + 16 * 64 * (WPT == 1 ? 0 : wave); B < span; B += 16 * 64 * WPT) {  // wave-uniform loop
+        for (int B = first + 16 * 64 * ow; B < span; B += 16 * 64 * OW) {  // wave-uniform loop
             const int j = locate(B);
             const int P = B + 16 * lane;
             if (P < span) chunk(P, j, !tile_safe);
@@ -628,6 +645,128 @@ __device__ __forceinline__ void encode_body(const EncodeParams& p) {
     }
 }
 
+// A real call from the persistent loop: inlined into the loop, the loop-invariant parts of the
+// unrolled copy steps are hoisted out of it and held in registers (114 VGPRs instead of 54).
+template <int NF, int NV, int kVariant, bool MIXED, int WPT, bool DIAG, int TR, int OW>
+__device__ __attribute__((noinline)) void enc_phase2_call(const EncodeParams& p, EncWaveLds<NV, slot_bytes(14 + 4 * (NF + NV) + 4), TR>& S,
+                                                          int cnt, int lane, int wave, int ow, uint8_t* const flg,
+                                                          const MaskTable& masks, u64* stamp) {
+    enc_phase2<NF, NV, kVariant, MIXED, WPT, DIAG, TR, OW>(p, S, cnt, lane, wave, ow, flg, masks, stamp);
+}
+
+template <int NF, int NV, int kVariant, bool MIXED = false, int WPT = 1, bool DIAG = false, int TR = kWaveRecs,
+          bool PIPE = false, int SSK = 8, bool PF = false>
+__device__ __forceinline__ void encode_body(const EncodeParams& p) {
+    static_assert(!PF || (WPT == kWaves && TR == kWaveRecs && kVariant == 1), "the prefetching encode takes 64-record workgroup tiles");
+    static_assert(!PIPE || (MIXED && WPT == kWaves && TR == kWaveRecs), "the pipelined size scan is for mixed 64-record workgroup tiles");
+    static_assert(!MIXED || (NF == 0 && NV == 2 && kVariant <= 1), "mixed batches are kv Get/Set");
+    static_assert(WPT == 1 || (WPT == kWaves && kVariant <= 1), "whole-workgroup tiles take one step per wave");
+    static_assert(TR == kWaveRecs || (TR == 2 * kWaveRecs && WPT == kWaves), "128-record tiles are workgroup tiles");
+    constexpr int NT = NF + NV;
+    constexpr int H0 = 14 + 4 * NT + 4;        // bytes before field 0's payload (the largest, in mixed batches)
+    constexpr i64 OVH = 14 + 4 * NT + 4 * NV;  // fixed bytes per record
+    constexpr int SLOT = slot_bytes(H0);
+    static_assert(SLOT - 16 >= H0 && OVH >= 16, "layout assumptions");
+
+    __shared__ EncWaveLds<NV, SLOT, TR> lds_all[PF ? 2 : kWaves / WPT];
+    __shared__ EncStage<NF, NV> stg_all[PF ? 2 : 1];
+    __shared__ uint8_t flags_all[kWaves][64];  // record-start marks of one phase-2 step, per wave
+    __shared__ MaskTable masks;
+    u64 blk = blockIdx.x;
+    if constexpr (PIPE) {
+        if (!p.pipe_lookback) {
+            const PipeWords W = pipe_words(p);
+            if (blockIdx.x < p.pipe_sizers) {
+                __shared__ u64 s_tot[kPipeGroup];
+                mixed_sizer(p, W, s_tot);
+                return;
+            }
+            if (blockIdx.x == p.pipe_sizers) {
+                __shared__ pipe::ScanLds SL;
+                pipe::scanner<1, SSK>(W.aw, W.pw, W.ng, p.epoch, SL, DIAG ? p.dbg + W.nt * 8 : nullptr);  // 256 * SSK groups per step
+                return;
+            }
+            blk = blockIdx.x - p.pipe_sizers - 1;
+        }
+    }
+    mask_table_init(masks, threadIdx.x);
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint8_t* const flg = flags_all[wave];
+    flg[lane] = 0;
+    if constexpr (!PF) {
+        (void)stg_all;
+        EncWaveLds<NV, SLOT, TR>& S = lds_all[WPT == 1 ? wave : 0];
+        const u64 r0 = (WPT == 1 ? blk * kWaves + wave : blk) * TR;
+        if (r0 >= p.n) return;  // wave-uniform (workgroup-uniform when WPT > 1)
+        const int cnt = (int)min((u64)TR, p.n - r0);
+        u64* const stamp = DIAG ? p.dbg + (r0 / kWaveRecs) * 8 : nullptr;  // tools/enc_timeline.py
+        if (DIAG && lane == 0 && (WPT == 1 || wave == 0)) {
+            stamp[0] = __builtin_amdgcn_s_memrealtime();
+            stamp[6] = blockIdx.x;
+        }
+        enc_phase1<NF, NV, MIXED, WPT, DIAG, TR, PIPE, false>(p, S, r0, cnt, lane, wave, stamp, nullptr, 0, 0);
+        if constexpr (WPT == 1) wave_sync();
+        else __syncthreads();
+        if (!S.ok) return;  // uniform
+        if (DIAG && lane == 0 && (WPT == 1 || wave == 0)) stamp[1] = __builtin_amdgcn_s_memrealtime();
+        enc_phase2<NF, NV, kVariant, MIXED, WPT, DIAG, TR, WPT>(p, S, cnt, lane, wave, WPT == 1 ? 0 : wave, flg, masks, stamp);
+    } else {
+        // Persistent workgroups, wave-specialised: wave 0 builds tile t (phase 1, from rows staged
+        // one tile ahead) while waves 1-3 copy tile t - G (phase 2); one barrier per tile hands S[b]
+        // over.  S and the stage are double-buffered, so phase 1 of tile t + G may overwrite S[b]
+        // only after that barrier -- by which waves 1-3 have finished tile t - G.
+        const u64 nt = (p.n + kWaveRecs - 1) / kWaveRecs;
+        const u64 G = gridDim.x - (PIPE && !p.pipe_lookback ? p.pipe_sizers + 1 : 0);
+        if (wave == 0) {
+            u64 wg = 0, wl = 0;
+            const auto issue = [&](u64 t, int b) {
+                enc_stage_issue<NF, NV, MIXED>(p, t * kWaveRecs, stg_all[b], lane);
+                if constexpr (PIPE) {
+                    const PipeWords W = pipe_words(p);
+                    wg = pipe::load_word(&W.pw[t / kPipeGroup]);
+                    wl = pipe::load_word(&W.lw[t]);
+                }
+            };
+            if (blk < nt) issue(blk, 0);
+            int b = 0;
+#pragma unroll 1
+            for (u64 t = blk; t < nt; t += G, b ^= 1) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this tile's rows and words have landed
+                const u64 cg = wg, cl = wl;
+                if (t + G < nt) issue(t + G, b ^ 1);  // in flight while this tile is built and copied
+                const u64 r0 = t * kWaveRecs;
+                const int cnt = (int)min((u64)kWaveRecs, p.n - r0);
+                u64* const stamp = DIAG ? p.dbg + t * 8 : nullptr;
+                if (DIAG && lane == 0) {
+                    stamp[0] = __builtin_amdgcn_s_memrealtime();
+                    stamp[6] = blockIdx.x;
+                }
+                int ln = lane;  // opaque per iteration (see the copier loop below)
+                asm volatile("" : "+v"(ln));
+                enc_phase1<NF, NV, MIXED, WPT, DIAG, TR, PIPE, true>(p, lds_all[b], r0, cnt, ln, 0, stamp, &stg_all[b], cg, cl);
+                if (DIAG && lane == 0) stamp[1] = __builtin_amdgcn_s_memrealtime();
+                pipe::lds_barrier();  // S[b] built (LDS writes done; stores and the prefetch stay in flight)
+            }
+        } else {
+            int b = 0;
+#pragma unroll 1
+            for (u64 t = blk; t < nt; t += G, b ^= 1) {
+                pipe::lds_barrier();
+                EncWaveLds<NV, SLOT, TR>& S = lds_all[b];
+                if (!S.ok) continue;  // uniform
+                const int cnt = (int)min((u64)kWaveRecs, p.n - t * kWaveRecs);
+                u64* const stamp = DIAG ? p.dbg + t * 8 : nullptr;
+                int ln = lane;  // opaque per iteration: keeps the lane-derived constants of the copy steps
+                asm volatile("" : "+v"(ln));  // from being hoisted out of the loop (~32 VGPRs held across it)
+                enc_phase2<NF, NV, kVariant, MIXED, WPT, DIAG, TR, kWaves - 1>(p, S, cnt, ln, wave, wave - 1, flg, masks, stamp);
+            }
+        }
+    }
+}
+
+
 template <int NF, int NV, int kVariant, bool MIXED = false, int WPT = 1, bool DIAG = false, int TR = kWaveRecs>
 __global__ __launch_bounds__(256) void encode_kernel(EncodeParams p) {
     encode_body<NF, NV, kVariant, MIXED, WPT, DIAG, TR>(p);
@@ -639,6 +778,40 @@ __global__ __launch_bounds__(256) void encode_kernel(EncodeParams p) {
 template <bool DIAG = false, int SSK = 1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void encode_pipe_kernel(EncodeParams p) {
     encode_body<0, 2, 1, true, kWaves, DIAG, kWaveRecs, true, SSK>(p);
+}
+
+// The prefetching encode (tuning variants 50-53): persistent wave-specialised workgroups, see
+// encode_body PF.  Measured slower than the default (config 2: 174 vs 154 us, config 3: 377 vs
+// 360 us, mixed: 119 vs 111 us; profiles/r03_pf_*): phase 1 drops from ~6 to ~2 us per tile, but
+// the copier loop holds 82-89 VGPRs (occupancy 5-6 instead of 8) and each copier waits for its
+// stores at every tile boundary (vmcnt counts stores; the next tile's loads are issued after them),
+// where a retiring workgroup leaves its stores draining behind it.
+template <int NF, int NV, bool MIXED, bool PIPE, bool DIAG = false>
+__global__ __launch_bounds__(256) void encode_pf_kernel(EncodeParams p) {
+    encode_body<NF, NV, 1, MIXED, kWaves, DIAG, kWaveRecs, PIPE, 1, true>(p);
+}
+
+static int device_cus();
+// Tile workgroups of a persistent launch: all of them resident at once, next to `others` resident
+// workgroups of the same launch (sizers, scanner).
+template <int NF, int NV, bool MIXED, bool PIPE, bool DIAG>
+static u64 pf_tile_groups(u64 ntiles, u64 others) {
+    static int occ[16] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    int& o = occ[dev & 15];
+    if (o == 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, encode_pf_kernel<NF, NV, MIXED, PIPE, DIAG>, 256, 0) != hipSuccess)
+        o = 0;
+    const u64 slots = (u64)device_cus() * (u64)max(o, 1);
+    const u64 g = slots > others + 1 ? slots - others : 1;
+    return min(g, ntiles);
+}
+template <int NF, int NV, bool MIXED, bool PIPE, bool DIAG = false>
+static void launch_pf(EncodeParams p, hipStream_t stream) {
+    const u64 nt = (p.n + kWaveRecs - 1) / kWaveRecs;
+    const u64 others = PIPE && !p.pipe_lookback ? (u64)p.pipe_sizers + 1 : 0;
+    const u64 g = pf_tile_groups<NF, NV, MIXED, PIPE, DIAG>(nt, others);
+    hipLaunchKernelGGL((encode_pf_kernel<NF, NV, MIXED, PIPE, DIAG>), dim3((unsigned)(others + g)), dim3(256), 0, stream, p);
 }
 
 static dim3 encode_grid(u64 n, int wpt) {
@@ -666,6 +839,9 @@ static void launch_layout(const EncodeParams& p, hipStream_t stream) {
         case 10: hipLaunchKernelGGL((encode_kernel<NF, NV, 1, false, kWaves, true>), encode_grid(p.n, kWaves), block, 0, stream, p); return;
         // 21: 128-record workgroup tiles (two header waves)
         case 21: hipLaunchKernelGGL((encode_kernel<NF, NV, 1, false, kWaves, false, 2 * kWaveRecs>), dim3((unsigned)((p.n + 127) / 128)), block, 0, stream, p); return;
+        // 50: the prefetching persistent encode; 53: with timestamps
+        case 50: launch_pf<NF, NV, false, false>(p, stream); return;
+        case 53: launch_pf<NF, NV, false, false, true>(p, stream); return;
         // 15: workgroup tiles, one step at a time (no software pipeline)
         case 15: hipLaunchKernelGGL((encode_kernel<NF, NV, 0, false, kWaves>), encode_grid(p.n, kWaves), block, 0, stream, p); return;
         default: break;
@@ -808,6 +984,7 @@ static void launch_encode_mixed_3(EncodeParams p, void* ws, hipStream_t stream) 
             return;
         case 5: hipLaunchKernelGGL((encode_kernel<0, 2, 0, true>), encode_grid(p.n, 1), dim3(64 * kWaves), 0, stream, p); return;
         case 38: hipLaunchKernelGGL((encode_kernel<0, 2, 1, true, kWaves, true>), encode_grid(p.n, kWaves), dim3(64 * kWaves), 0, stream, p); return;  // + timestamps
+        case 41: hipLaunchKernelGGL((encode_kernel<0, 2, 1, true, 1>), encode_grid(p.n, 1), dim3(64 * kWaves), 0, stream, p); return;  // wave tiles, pipelined steps
         case 15: hipLaunchKernelGGL((encode_kernel<0, 2, 0, true, kWaves>), encode_grid(p.n, kWaves), dim3(64 * kWaves), 0, stream, p); return;
         default: break;
     }
@@ -820,7 +997,7 @@ hipError_t launch_encode_mixed(EncodeParams p, void* ws, hipStream_t stream) {
     if (!p.type || p.lay.nfixed != 0 || p.lay.nvar != 2) return hipErrorInvalidValue;
     int impl = p.impl;
 #ifdef SYMHIP_TUNING
-    if (p.variant == 5 || p.variant == 15 || p.variant == 20 || p.variant == 38 || p.variant == 40) impl = SYM_ENCODE_THREE_KERNEL;  // 40: its default kernel
+    if (p.variant == 5 || p.variant == 15 || p.variant == 20 || p.variant == 38 || p.variant == 40 || p.variant == 41) impl = SYM_ENCODE_THREE_KERNEL;  // 40: its default kernel
 #endif
     if (impl == SYM_ENCODE_THREE_KERNEL) {
         if (!ws) return hipErrorInvalidValue;
@@ -842,6 +1019,15 @@ hipError_t launch_encode_mixed(EncodeParams p, void* ws, hipStream_t stream) {
     const u64 grid = p.pipe_lookback ? nt : P + 1 + nt;
     if (grid > 0xFFFFFFFFull) return hipErrorInvalidValue;
 #ifdef SYMHIP_TUNING
+    if (p.variant == 51) {  // the prefetching persistent encode tiles
+        launch_pf<0, 2, true, true>(p, stream);
+        return hipGetLastError();
+    }
+    if (p.variant == 52) {  // the same with timestamps (tools/mixed_timeline.py --variant 52)
+        if (!p.dbg) return hipErrorInvalidValue;
+        launch_pf<0, 2, true, true, true>(p, stream);
+        return hipGetLastError();
+    }
     if (p.variant == 37) {  // per-tile timestamps (tools/mixed_timeline.py): p.dbg holds 16 u64 per tile
         if (!p.dbg) return hipErrorInvalidValue;
         hipLaunchKernelGGL((encode_pipe_kernel<true>), dim3((unsigned)grid), dim3(64 * kWaves), 0, stream, p);

@@ -668,8 +668,8 @@ def mixed_leg(codec: Codec, dev, reps: int, cfg=None) -> dict:
             "decode_ms": round(dec_ms, 4), "decode_gbps": round(dec_alg / dec_ms / 1e6, 1),
             "gbps_algorithmic": round((enc_alg + dec_alg) / (enc_ms + dec_ms) / 1e6, 1),
             "mrecords_per_s": round(2 * n / (enc_ms + dec_ms) / 1e3, 1),
-            "note": "Get/Set mix at the trace_large.req ratio (9,267 SET / 25,125); encode = size pass + encode "
-                    "kernel and group scan (three launches); client IDs: service 1, Get 1, Set 2"}
+            "note": "Get/Set mix at the trace_large.req ratio (9,267 SET / 25,125); encode = one launch (sizer "
+                    "groups, scanner, encode tiles); client IDs: service 1, Get 1, Set 2"}
 
 
 def config3_leg(codec: Codec, dev, reps: int, cfg=None) -> dict:

@@ -27,7 +27,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--trace", action="store_true")
     ap.add_argument("--records", type=int, default=0)
-    ap.add_argument("--variant", default="37", help="37: one launch; 38: three launches (no sizer/scanner stamps)")
+    ap.add_argument("--variant", default="37", help="37: one launch; 38: three launches (no sizer/scanner stamps); 52: prefetching persistent tiles")
     a = ap.parse_args()
     kw = dict(datagen.config2_trace_mixed() if a.trace else datagen.CONFIG2_MIXED)
     if a.records:
@@ -60,8 +60,8 @@ def main():
     t0 = tile[:, 0].min()
     us = lambda x: (x - t0) / 100.0  # noqa: E731
     st, hdr = us(tile[:, 0]), us(tile[:, 1])
-    pre = us(tile[:, 7]) if a.variant == "37" else st
-    if a.variant != "37":
+    pre = us(tile[:, 7]) if a.variant in ("37", "52") else st
+    if a.variant not in ("37", "52"):
         side[:, 4] = side[:, 5] = t0
     end = us(tile[:, 2:6].max(axis=1))
     grp = np.arange(nt) // 8  # sizer groups (encode.hip kPipeGroup): their stamps sit at the group index
