@@ -973,7 +973,7 @@ def main():
         line["config3_trace"] = t3
         tm = mixed_leg(codec, dev, args.trace_reps, datagen.config2_trace_mixed())
         tm["note"] = ("the kv benchmark's request stream replayed: trace_large.req's GET/SET sequence, key sizes "
-                      "and SET value sizes (clipped to [16, 4096]), cycled to 2^20 requests; three-launch "
+                      "and SET value sizes (clipped to [16, 4096]), cycled to 2^20 requests; one-launch "
                       "encode, pipeline decode")
         line["mixed_trace"] = tm
     if world == 1 and args.host_steps > 0:
