@@ -170,6 +170,9 @@ struct GatherArgs {
 };
 }  // namespace raw
 hipError_t launch_tile_scan(const raw::Pair* agg, raw::Pair* pre, uint64_t ntiles, hipStream_t stream);
+// the same over the tiles of a device-side item count (*nlim) only
+hipError_t launch_tile_scan_limited(const raw::Pair* agg, raw::Pair* pre, uint64_t ntiles, const uint64_t* nlim,
+                                    hipStream_t stream);
 hipError_t launch_tile_scan_gated(const raw::Pair* agg, raw::Pair* pre, uint64_t ntiles, const unsigned* gate,
                                   hipStream_t stream);
 hipError_t launch_segment_gather(const raw::GatherArgs& a, hipStream_t stream);

@@ -20,6 +20,8 @@
 // written with one global_store_dwordx4.  Per-record scan inputs never round-trip through HBM
 // (only 16 bytes per 256-record tile do), which is what a device-wide library scan would cost.
 #include "../../include/symphony_hip.h"
+#include <algorithm>
+
 #include "codec.hpp"
 #include "device_util.hpp"
 
@@ -138,9 +140,12 @@ __global__ __launch_bounds__(256) void firewall_mark_kernel(const uint8_t* in, c
 
 // ---- exclusive scan of the tile totals (one workgroup; pre[ntiles] = grand total).  Each thread
 // takes 4 consecutive tiles, so up to 4096 tiles (2^20 records) take one block-wide scan.
+// nlim (optional): a device count of the scanned items; only its ceil(*nlim / 256) tiles are
+// scanned (an item-capacity launch whose real count is known on the device only).
 __global__ __launch_bounds__(1024) void tile_scan_kernel(const Pair* agg, Pair* pre, u64 ntiles,
-                                                        const unsigned* gate = nullptr) {
+                                                        const unsigned* gate = nullptr, const u64* nlim = nullptr) {
     if (gate && *gate == 0) return;  // a gated launch (reassembly's general path) with nothing to do
+    if (nlim) ntiles = min(ntiles, (*nlim + 255) / 256);
     constexpr int kPer = 4;
     __shared__ u64 wb[16], wc[16];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -193,17 +198,13 @@ __device__ __forceinline__ u64 readlane_u64(u64 v, int l) {
     return (u64)__builtin_amdgcn_readlane((u32)v, l) | ((u64)__builtin_amdgcn_readlane((u32)(v >> 32), l) << 32);
 }
 
+// One 256-segment tile (the workgroup's loop body below).  pre[ntiles] is the total: a scan over
+// the capacity's tiles has it there too, at the exclusive prefix of the first empty tile.
 template <bool FW>
-__global__ __launch_bounds__(kWaves * 64) void gather_kernel(GatherArgs a) {
-    __shared__ WaveLds lds_all[kWaves];
-    __shared__ MaskTable masks;
-    __shared__ u64 wsum_b[kWaves], wsum_c[kWaves];
+__device__ __forceinline__ void gather_tile(const GatherArgs& a, u64 tile, u64 n, u64 ntiles, WaveLds* lds_all,
+                                            const MaskTable& masks, u64* wsum_b, u64* wsum_c) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const u64 ntiles = (a.n + 255) / 256;    // of the tile scan (a.n bounds the segment count)
-    const u64 n = a.n_ptr ? *a.n_ptr : a.n;  // segments
-    const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
-    if ((u64)blockIdx.x * 256 >= n && blockIdx.x > 0) return;  // a tile past the segments writes nothing
-    mask_table_init(masks, threadIdx.x);
+    const u64 i = tile * 256 + threadIdx.x;
 
     // ---- phase 1 (thread = record): length, keep flag, in-tile exclusive scan
     u64 src = 0, len = 0, keep = 0;
@@ -229,7 +230,7 @@ __global__ __launch_bounds__(kWaves * 64) void gather_kernel(GatherArgs a) {
         if (i == 0) atomicOr(a.err, kErrCapacity);
         return;
     }
-    const Pair tp = a.pre[blockIdx.x];
+    const Pair tp = a.pre[tile];
     u64 wb = tp.bytes, wc = tp.count;
     for (int q = 0; q < wave; ++q) {
         wb += wsum_b[q];
@@ -252,7 +253,7 @@ __global__ __launch_bounds__(kWaves * 64) void gather_kernel(GatherArgs a) {
     }
 
     // ---- phase 2 (wave = 64 segments, lane = aligned 16-byte output chunk)
-    const u64 r0 = (u64)blockIdx.x * 256 + (u64)wave * kSegs;
+    const u64 r0 = tile * 256 + (u64)wave * kSegs;
     if (r0 >= n) return;  // wave-uniform
     const int cnt = (int)min((u64)kSegs, n - r0);
     WaveLds& S = lds_all[wave];
@@ -327,6 +328,22 @@ __global__ __launch_bounds__(kWaves * 64) void gather_kernel(GatherArgs a) {
     }
 }
 
+// Grid-stride over the tiles of the segment count (*n_ptr when given, else n): a launch sized for a
+// capacity far above the real count (nested item lists) does not dispatch a workgroup per empty tile.
+template <bool FW>
+__global__ __launch_bounds__(kWaves * 64) void gather_kernel(GatherArgs a) {
+    __shared__ WaveLds lds_all[kWaves];
+    __shared__ MaskTable masks;
+    __shared__ u64 wsum_b[kWaves], wsum_c[kWaves];
+    const u64 n = a.n_ptr ? *a.n_ptr : a.n;  // segments
+    const u64 ntiles = (n + 255) / 256;
+    mask_table_init(masks, threadIdx.x);
+    for (u64 t = blockIdx.x; t < max(ntiles, (u64)1); t += gridDim.x) {  // workgroup-uniform loop
+        gather_tile<FW>(a, t, n, ntiles, lds_all, masks, wsum_b, wsum_c);
+        __syncthreads();  // wsum_* and the wave slots are rewritten by the next tile
+    }
+}
+
 inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 inline u64 tiles_of(u64 n) { return (n + 255) / 256; }
 
@@ -364,7 +381,13 @@ hipError_t launch_tile_scan_gated(const raw::Pair* agg, raw::Pair* pre, u64 ntil
 }
 
 hipError_t launch_segment_gather(const raw::GatherArgs& a, hipStream_t stream) {
-    hipLaunchKernelGGL(raw::gather_kernel<false>, dim3((unsigned)raw::tiles_of(a.n)), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL(raw::gather_kernel<false>, dim3((unsigned)std::min<u64>(raw::tiles_of(a.n), 4096)), dim3(256), 0,
+                       stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_tile_scan_limited(const raw::Pair* agg, raw::Pair* pre, u64 ntiles, const u64* nlim, hipStream_t stream) {
+    hipLaunchKernelGGL(raw::tile_scan_kernel, dim3(1), dim3(1024), 0, stream, agg, pre, ntiles, nullptr, nlim);
     return hipGetLastError();
 }
 

@@ -125,10 +125,22 @@ TEST_FIXED = FlatSchema("Fixed", (FlatField("FInt32", "int32", True), FlatField(
 def encode(codec: Codec, schema: FlatSchema, cols: list, service_id: int = 0, method_id: int = 0,
            stream=None, n: int | None = None, out=None):
     """cols[k] per the module docstring.  -> (stream uint8, offsets int64 [n+1]).  `n` is needed
-    only for a schema without fields (n empty messages).  out=(uint8 buffer, int64 [n+1]) skips
-    the size query (a device sync): the buffer must hold the encoded size.  Message fields are
-    encoded first (their own message fields first), with service / method ids 0 as
-    MarshalSymphony writes for nested messages."""
+    only for a schema without fields (n empty messages).  out=(uint8 buffer, int64 [n+1]): the
+    buffer must hold the encoded size; it is returned whole.  Message fields are encoded first
+    (their own message fields first), with service / method ids 0 as MarshalSymphony writes for
+    nested messages.  The whole tree is launched without a host sync; only the returned stream's
+    length (offsets[n]) is read back at the end."""
+    buf, off = _encode(codec, schema, cols, service_id, method_id, stream, n, out)
+    if out is not None:
+        return buf, off
+    size = int(off[-1].item()) if off.numel() > 1 else 0
+    return buf[:size], off
+
+
+def _encode(codec: Codec, schema: FlatSchema, cols: list, service_id: int, method_id: int, stream, n, out):
+    """encode() without the final read-back: the output buffer is sized from the columns' tensor
+    sizes (an upper bound of the encoded size: sym_flat_encoded_size_ex of every byte / item column
+    taken whole), so no level needs a device value on the host."""
     if len(cols) != len(schema.fields):
         raise ValueError(f"{schema.name}: {len(schema.fields)} columns expected")
     if not schema.fields and n is None:
@@ -140,8 +152,9 @@ def encode(codec: Codec, schema: FlatSchema, cols: list, service_id: int = 0, me
         if f.kind == "message":
             if not isinstance(c, MessageColumn):
                 raise ValueError(f"{f.name}: a MessageColumn expected")
-            m_in = int(c.rec[-1].item() - c.rec[0].item()) if c.rec.numel() > 1 else 0
-            ib, io = encode(codec, f.message, c.cols, stream=stream, n=m_in if not c.cols else None)
+            # a fieldless inner schema needs its record count: the one host read of a level
+            m_in = (int(c.rec[-1].item() - c.rec[0].item()) if c.rec.numel() > 1 else 0) if not c.cols else None
+            ib, io = _encode(codec, f.message, c.cols, 0, 0, stream, m_in, None)
             c = ListColumn(ib, io, c.rec)
             keep.append(c)
         if f.list_like:
@@ -152,11 +165,8 @@ def encode(codec: Codec, schema: FlatSchema, cols: list, service_id: int = 0, me
             ptrs.append(_dptr(c.bytes) or 1)
             offs.append(_dptr(c.rec))
             items.append(_dptr(c.item_off))
-            if out is None:
-                j0, j1 = (int(x) for x in c.rec[[0, -1]].tolist()) if m else (0, 0)
-                o = c.item_off[[j0, j1]].tolist() if c.item_off.numel() else [0, 0]
-                nbytes.append(int(o[1] - o[0]))
-                nitems.append(j1 - j0)
+            nbytes.append(c.bytes.numel())
+            nitems.append(max(0, c.item_off.numel() - 1))
         elif f.width:
             if c.element_size() != f.width or c.device != codec.device or not c.is_contiguous():
                 raise ValueError(f"{f.name}: a contiguous {f.width}-byte column on {codec.device} expected")
@@ -171,8 +181,7 @@ def encode(codec: Codec, schema: FlatSchema, cols: list, service_id: int = 0, me
             _check_col(b, torch.uint8, f.name, codec.device)
             _check_col(o, torch.int64, f.name + " offsets", codec.device)
             m = o.numel() - 1
-            if out is None:
-                nbytes.append(int(o[-1].item() - o[0].item()) if m else 0)
+            nbytes.append(b.numel())
             nitems.append(0)
             ptrs.append(_dptr(b) or 1)
             offs.append(_dptr(o))
@@ -195,14 +204,13 @@ def encode(codec: Codec, schema: FlatSchema, cols: list, service_id: int = 0, me
         _check_col(off, torch.int64, "out offsets", codec.device)
         if off.numel() != n + 1:
             raise ValueError("out offsets: n + 1 entries expected")
-        size = out.numel()
     lists = schema.has_lists
     _native.check(codec._lib.sym_flat_encode_ex(codec._ctx, cf, len(schema.fields), n, _native.ptr_array(ptrs),
                                                _native.ptr_array(offs), _native.ptr_array(items) if lists else None,
                                                service_id, method_id, _dptr(out), _dptr(off),
                                                _stream_handle(codec.device, stream)), "sym_flat_encode_ex")
     del keep
-    return out[:size], off
+    return out, off
 
 
 def decode(codec: Codec, schema: FlatSchema, data: torch.Tensor, rec_off: torch.Tensor, stream=None,
@@ -256,16 +264,27 @@ def decode(codec: Codec, schema: FlatSchema, data: torch.Tensor, rec_off: torch.
                                                _native.ptr_array(offs), _native.ptr_array(items) if lists else None,
                                                _native.u64_array(icaps) if lists else None, _dptr(st), _dptr(fail),
                                                hs), "sym_flat_decode_ex")
+    # every list field's item count and item bytes in ONE read-back per level
+    lk = [k for k, f in enumerate(schema.fields) if f.list_like]
+    sizes = {}
+    if lk and n:
+        parts = []
+        for k in lk:
+            lc = cols[k]
+            m_t = (lc.rec[n] - lc.rec[0]).clamp(0, lc.item_off.numel() - 1).view(1)
+            parts += [m_t, lc.item_off.index_select(0, m_t)]
+        v = torch.cat(parts).tolist()
+        sizes = {k: (int(v[2 * i]), int(v[2 * i + 1])) for i, k in enumerate(lk)}
     for k, f in enumerate(schema.fields):
         if not f.list_like:
             continue
         lc = cols[k]
-        m = int(lc.rec[n].item() - lc.rec[0].item()) if n else 0
+        m, nb = sizes.get(k, (0, 0))
         lc.item_off = lc.item_off[:m + 1]
-        lc.bytes = lc.bytes[:int(lc.item_off[-1].item()) if m else 0]
+        lc.bytes = lc.bytes[:nb if m else 0]
         if f.kind == "message":
             # the items are the inner records (item_off[0] == 0): decode them, fold their statuses in
-            inner_cols, inner_st = decode(codec, f.message, lc.bytes, lc.item_off, stream=stream)
+            inner_cols, inner_st = decode(codec, f.message, lc.bytes, lc.item_off, stream=stream, span=nb if m else 0)
             if n:
                 _native.check(codec._lib.sym_flat_nested_status(codec._ctx, cf, len(schema.fields), k, n,
                                                                  _dptr(lc.rec), _dptr(inner_st) or 1, _dptr(st),
