@@ -75,6 +75,7 @@ SIGNATURES = {
     "sym_flat_encode_ex": (_int, [_ctx, _vp, _int, _u64, _vp, _vp, _vp, _u32, _u32, _u8p, _u64p, _vp]),
     "sym_flat_decode_ex": (_int, [_ctx, _vp, _int, _u64, _u8p, _u64p, _vp, _vp, _vp, _vp, _vp, _u8p, _u8p, _vp]),
     "sym_flat_nested_status": (_int, [_ctx, _vp, _int, _int, _u64, _u64p, _u8p, _u8p, _u8p, _vp]),
+    "sym_flat_list_sizes": (_int, [_ctx, _int, _u64, _vp, _vp, _vp, _u64p, _vp]),
     "sym_raw_set": (_int, [_ctx, _vp, _int, _int, _u8p, _u64p, _u64, _vp, _u64p, _u8p, _u64, _u64p, _u8p, _vp]),
     "sym_batcher_create": (_int, [_int, _int, _u32, _u64, _u32, ctypes.POINTER(ctypes.c_void_p)]),
     "sym_batcher_destroy": (_int, [_vp]),

@@ -742,6 +742,20 @@ int sym_flat_nested_status(sym_ctx* ctx, const sym_field* fields, int nfields, i
     return e == hipSuccess ? SYM_OK : hip_fail(e, "nested status launch");
 }
 
+int sym_flat_list_sizes(sym_ctx* ctx, int nl, uint64_t n, const uint64_t* const* d_recs,
+                        const uint64_t* const* d_items, const uint64_t* item_caps, uint64_t* d_out, void* stream) {
+    if (!ctx) return fail(SYM_ERR_INVALID, "sym_flat_list_sizes: ctx is NULL");
+    if (nl < 0 || nl > SYM_MAX_FLAT_FIELDS) return fail(SYM_ERR_INVALID, "sym_flat_list_sizes: %d lists", nl);
+    if (nl == 0) return SYM_OK;
+    if (!d_recs || !d_items || !item_caps || !d_out) return fail(SYM_ERR_INVALID, "sym_flat_list_sizes: NULL argument");
+    for (int i = 0; i < nl; ++i)
+        if (!d_recs[i] || !d_items[i]) return fail(SYM_ERR_INVALID, "sym_flat_list_sizes: list %d is NULL", i);
+    DeviceGuard g(ctx->device);
+    if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
+    hipError_t e = symhip::launch_list_sizes(nl, n, d_recs, d_items, item_caps, d_out, (hipStream_t)stream);
+    return e == hipSuccess ? SYM_OK : hip_fail(e, "list sizes launch");
+}
+
 int sym_raw_set(sym_ctx* ctx, const sym_field* fields, int nfields, int field, const uint8_t* d_in,
                 const uint64_t* d_rec_off, uint64_t n, const void* d_val, const uint64_t* d_val_off, uint8_t* d_out,
                 uint64_t out_cap, uint64_t* d_out_off, uint8_t* d_status, void* stream) {

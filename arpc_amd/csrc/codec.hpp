@@ -189,6 +189,8 @@ hipError_t launch_flat_decode(const sym_field* f, int nf, uint64_t n, const uint
                               void* const* cols, const uint64_t* caps, uint64_t* const* offs, uint64_t* const* items,
                               const uint64_t* item_caps, uint8_t* status, uint8_t* fail, void* ws, unsigned* err,
                               hipStream_t stream);
+hipError_t launch_list_sizes(int nl, uint64_t n, const uint64_t* const* recs, const uint64_t* const* items,
+                             const uint64_t* caps, uint64_t* out, hipStream_t stream);
 hipError_t launch_nested_status(uint64_t n, uint32_t pos, const uint64_t* rec_items, const uint8_t* item_status,
                                 uint8_t* status, uint8_t* fail, hipStream_t stream);
 

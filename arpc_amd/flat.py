@@ -91,16 +91,22 @@ class MessageColumn:
     n_items: int = 0
 
 
+_C_FIELDS: dict = {}
+
+
 @dataclass(frozen=True)
 class FlatSchema:
     name: str
     fields: tuple
 
     def c_fields(self):
-        arr = (_native.SymField * max(1, len(self.fields)))()
-        for k, f in enumerate(self.fields):
-            arr[k].segment = _native.SYM_SEGMENT_PUBLIC if f.public else _native.SYM_SEGMENT_PRIVATE
-            arr[k].width = f.c_width
+        arr = _C_FIELDS.get(self)
+        if arr is None:  # built once per schema (a tree walk asks for it at every level)
+            arr = (_native.SymField * max(1, len(self.fields)))()
+            for k, f in enumerate(self.fields):
+                arr[k].segment = _native.SYM_SEGMENT_PUBLIC if f.public else _native.SYM_SEGMENT_PRIVATE
+                arr[k].width = f.c_width
+            _C_FIELDS[self] = arr
         return arr
 
     @property
@@ -268,12 +274,13 @@ def decode(codec: Codec, schema: FlatSchema, data: torch.Tensor, rec_off: torch.
     lk = [k for k, f in enumerate(schema.fields) if f.list_like]
     sizes = {}
     if lk and n:
-        parts = []
-        for k in lk:
-            lc = cols[k]
-            m_t = (lc.rec[n] - lc.rec[0]).clamp(0, lc.item_off.numel() - 1).view(1)
-            parts += [m_t, lc.item_off.index_select(0, m_t)]
-        v = torch.cat(parts).tolist()
+        sz = torch.empty(2 * len(lk), dtype=torch.int64, device=codec.device)
+        _native.check(codec._lib.sym_flat_list_sizes(codec._ctx, len(lk), n,
+                                                     _native.ptr_array([_dptr(cols[k].rec) for k in lk]),
+                                                     _native.ptr_array([_dptr(cols[k].item_off) for k in lk]),
+                                                     _native.u64_array([icaps[k] for k in lk]), _dptr(sz), hs),
+                      "sym_flat_list_sizes")
+        v = sz.tolist()
         sizes = {k: (int(v[2 * i]), int(v[2 * i + 1])) for i, k in enumerate(lk)}
     for k, f in enumerate(schema.fields):
         if not f.list_like:

@@ -442,9 +442,9 @@ uint64_t sym_flat_encoded_size(const sym_field* fields, int nfields, uint64_t n,
  *   sym_flat_encoded_size_ex  exact output size: bytes[k] = payload bytes of field k (strings and
  *                    repeated fixed: their column bytes; list-like: item bytes), items[k] = items of a
  *                    list-like field (nested: records where it is set).
- *   sym_flat_encode_ex  as sym_flat_encode; list bodies are written by a second kernel into the
- *                    holes the record kernel leaves.  More than one item for a nested field is
- *                    SYM_ERR_INVALID from sym_ctx_check.
+ *   sym_flat_encode_ex  as sym_flat_encode; list bodies ([count], then [u32 len][item] per item)
+ *                    are written by the same output-stationary kernel.  More than one item for a
+ *                    nested field is SYM_ERR_INVALID from sym_ctx_check.
  *   sym_flat_decode_ex  as sym_flat_decode; list-like field k: item bytes into d_cols[k] (caps[k]),
  *                    item offsets into d_items[k] (item_caps[k] + 1 entries) and record item ranges
  *                    into d_offs[k] (n + 1).  A list keeps the items that fit in the record, in order
@@ -456,7 +456,12 @@ uint64_t sym_flat_encoded_size(const sym_field* fields, int nfields, uint64_t n,
  *                    failed item SYM_STATUS_NESTED (Go returns "failed to unmarshal nested message"
  *                    there); d_fail is updated, so fields can be folded in in any order.  Field
  *                    values of a record with a non-OK status are unspecified beyond the fields
- *                    before the failing one (Go callers discard the struct on error). */
+ *                    before the failing one (Go callers discard the struct on error).
+ *   sym_flat_list_sizes  after sym_flat_decode_ex, for `nl` list-like fields (record item ranges
+ *                    d_recs[i], n + 1 entries; item offsets d_items[i], item_caps[i] + 1): item count
+ *                    m_i = d_recs[i][n] - d_recs[i][0] (clamped to item_caps[i]) and item bytes
+ *                    d_items[i][m_i] into d_out[2i], d_out[2i + 1] (device memory), in one launch,
+ *                    so a host walking a message tree reads back one small array per level. */
 uint64_t sym_flat_encoded_size_ex(const sym_field* fields, int nfields, uint64_t n, const uint64_t* bytes,
                                   const uint64_t* items);
 int sym_flat_encode_ex(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const void* const* d_cols,
@@ -469,6 +474,8 @@ int sym_flat_decode_ex(sym_ctx* ctx, const sym_field* fields, int nfields, uint6
 int sym_flat_nested_status(sym_ctx* ctx, const sym_field* fields, int nfields, int field, uint64_t n,
                            const uint64_t* d_rec_items, const uint8_t* d_item_status, uint8_t* d_status,
                            uint8_t* d_fail, void* stream);
+int sym_flat_list_sizes(sym_ctx* ctx, int nl, uint64_t n, const uint64_t* const* d_recs,
+                        const uint64_t* const* d_items, const uint64_t* item_caps, uint64_t* d_out, void* stream);
 
 /* ---- Batched Raw setters ----------------------------------------------------
  * XxxRaw.SetF(v_i) on buffer i of a flat schema (generator main.go:1038-1093 assertions,
