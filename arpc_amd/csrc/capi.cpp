@@ -143,6 +143,9 @@ int sym_ctx_destroy(sym_ctx* ctx) {
     if (!ctx) return SYM_OK;
     DeviceGuard g(ctx->device);
     host_slots_destroy(ctx);
+    for (hipEvent_t ev : ctx->rx_ev)
+        if (ev) (void)hipEventDestroy(ev);
+    if (ctx->rx_aux) (void)hipStreamDestroy(ctx->rx_aux);
     if (ctx->ws) (void)hipFree(ctx->ws);
     if (ctx->flags) (void)hipFree(ctx->flags);
     if (ctx->frag) (void)hipFree(ctx->frag);
@@ -600,8 +603,18 @@ int sym_reassemble(sym_ctx* ctx, const uint8_t* d_wire, const uint64_t* d_dg_off
     }
     const int rc = ensure_scratch(ctx, symhip::reassemble_ws_bytes(n), "reassembly");
     if (rc != SYM_OK) return rc;
+    if (!ctx->rx_aux) {
+        // high priority: for a single-datagram batch its ~20 launches exit at once, and they should
+        // not queue behind the copy running beside them
+        int least = 0, greatest = 0;
+        hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+        if (e == hipSuccess) e = hipStreamCreateWithPriority(&ctx->rx_aux, hipStreamNonBlocking, greatest);
+        for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&ctx->rx_ev[i], hipEventDisableTiming);
+        if (e != hipSuccess) return hip_fail(e, "reassembly stream / events");
+    }
     hipError_t e = symhip::launch_reassemble(d_wire, d_dg_off, n, d_msg, msg_cap, d_msg_off, d_msg_rpc, d_msg_dg, d_nmsg,
-                                             d_status, ctx->frag, ctx->err, (hipStream_t)stream);
+                                             d_status, ctx->frag, ctx->err, (hipStream_t)stream, ctx->rx_aux,
+                                             ctx->rx_ev[0], ctx->rx_ev[1]);
     return e == hipSuccess ? SYM_OK : hip_fail(e, "reassembly launch");
 }
 

@@ -210,9 +210,12 @@ hipError_t launch_crypt(bool enc, const uint8_t* in, const uint64_t* rec_off, ui
 
 // ---- receive-side reassembly (reassemble.hip)
 size_t reassemble_ws_bytes(uint64_t n);
+// aux / fork / join: a second stream and two events of the ctx: the gated general path runs on
+// aux, beside the single-datagram path on `stream` (nullptr aux: everything on `stream`)
 hipError_t launch_reassemble(const uint8_t* wire, const uint64_t* dg_off, uint64_t n, uint8_t* msg, uint64_t msg_cap,
                              uint64_t* msg_off, uint64_t* msg_rpc, uint64_t* msg_dg, uint64_t* nmsg, uint8_t* status,
-                             void* ws, unsigned* err, hipStream_t stream);
+                             void* ws, unsigned* err, hipStream_t stream, hipStream_t aux = nullptr,
+                             hipEvent_t fork = nullptr, hipEvent_t join = nullptr);
 
 // ---- batched Raw getters and the firewall element (raw_fields.hip)
 hipError_t launch_raw_fixed(const uint8_t* in, const uint64_t* rec_off, uint64_t n, int priv, uint32_t table_off,

@@ -40,6 +40,10 @@ struct sym_ctx {
     int num_cus = 0;
     int decode_impl = SYM_DECODE_PIPELINE;
     int encode_impl = 0;  // SYM_ENCODE_* (mixed batches' size scan)
+    // reassembly: the stream its gated general path runs on beside the caller's, and the fork /
+    // join events (created on first use)
+    hipStream_t rx_aux = nullptr;
+    hipEvent_t rx_ev[2] = {nullptr, nullptr};
     // host-memory entry points: chunk slots (created on first use)
     symhip::host::Slot slots[symhip::host::kSlots];
     bool slots_ready = false;

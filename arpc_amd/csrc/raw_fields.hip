@@ -337,8 +337,9 @@ __global__ __launch_bounds__(kWaves * 64) void gather_kernel(GatherArgs a) {
     __shared__ u64 wsum_b[kWaves], wsum_c[kWaves];
     const u64 n = a.n_ptr ? *a.n_ptr : a.n;  // segments
     const u64 ntiles = (n + 255) / 256;
+    if (n == 0) return;  // nothing to place (and the scan of an empty count may not have run)
     mask_table_init(masks, threadIdx.x);
-    for (u64 t = blockIdx.x; t < max(ntiles, (u64)1); t += gridDim.x) {  // workgroup-uniform loop
+    for (u64 t = blockIdx.x; t < ntiles; t += gridDim.x) {  // workgroup-uniform loop
         gather_tile<FW>(a, t, n, ntiles, lds_all, masks, wsum_b, wsum_c);
         __syncthreads();  // wsum_* and the wave slots are rewritten by the next tile
     }
@@ -381,7 +382,9 @@ hipError_t launch_tile_scan_gated(const raw::Pair* agg, raw::Pair* pre, u64 ntil
 }
 
 hipError_t launch_segment_gather(const raw::GatherArgs& a, hipStream_t stream) {
-    hipLaunchKernelGGL(raw::gather_kernel<false>, dim3((unsigned)std::min<u64>(raw::tiles_of(a.n), 4096)), dim3(256), 0,
+    // a workgroup per tile of the capacity, up to 16384 (a 2^22-segment batch); past that (item
+    // capacities of nested lists, far above their real counts) the workgroups stride over the tiles
+    hipLaunchKernelGGL(raw::gather_kernel<false>, dim3((unsigned)std::min<u64>(raw::tiles_of(a.n), 16384)), dim3(256), 0,
                        stream, a);
     return hipGetLastError();
 }

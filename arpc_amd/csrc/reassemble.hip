@@ -80,8 +80,10 @@ struct Args {
     u32* plen;
     u32* gid;
     u32* idx;
-    const u32* gs;         // sorted group keys / arrival indices
-    const u32* is;
+    const u32* gs;         // sorted group keys / arrival indices (gid / idx themselves when the
+    const u32* is;         // keys came out non-decreasing: *unsorted == 0 and the sort did nothing)
+    unsigned* unsorted;
+    const unsigned* nonmono;  // not every datagram a DataPacket with RPCIDs non-decreasing: hash them
     SeqState* state;
     uint8_t* status;
     Pair* cnt;             // per arrival (n+1): (message bytes, segments << 32 | messages)
@@ -106,6 +108,20 @@ __global__ __launch_bounds__(256) void init_kernel(u64* table, u32* first, u64 t
         if (i < ts) table[i] = kEmpty;
         first[i] = ~0u;
     }
+}
+
+// ---- 1. When every datagram is a DataPacket and the RPCIDs never decrease, each RPCID's datagrams
+// form one contiguous run, so its group is that run and its first arrival the run's head: the hash
+// table (and the sort, the keys being in order) is not needed.  This kernel finds out; the hash
+// and key kernels branch on its word (the packetizer's send order and one client's increasing
+// RPCIDs are this case).
+__global__ __launch_bounds__(256) void order_kernel(Args a, const unsigned* gate, unsigned* nonmono) {
+    if (gated_off(gate)) return;
+    const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
+    bool bad = false;
+    if (i < a.n)
+        bad = a.status[i] != SYM_RX_PENDING || (i > 0 && (a.status[i - 1] != SYM_RX_PENDING || a.rpc[i] < a.rpc[i - 1]));
+    if (__syncthreads_or(bad) && threadIdx.x == 0) atomicOr(nonmono, 1u);
 }
 
 // ---- 2. stable LSD radix sort of (key, value) u32 pairs, 8 key bits per pass, 2048 pairs a tile.
@@ -314,6 +330,8 @@ __global__ __launch_bounds__(256) void hash_kernel(Args a, const unsigned* gate)
     const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
     if (i >= a.n) return;
     a.cnt[i] = Pair{0, 0};
+    a.idx[i] = (u32)i;
+    if (!*a.nonmono) return;  // runs of equal RPCIDs: key_kernel takes the run heads
     u32 g = kNoSlot;  // table slot
     if (a.status[i] == SYM_RX_PENDING) {
         const u64 r = a.rpc[i];
@@ -332,7 +350,6 @@ __global__ __launch_bounds__(256) void hash_kernel(Args a, const unsigned* gate)
     }
     a.slot[i] = g;
     if (g != kNoSlot) atomicMin(&a.first[g], (u32)i);
-    a.idx[i] = (u32)i;
 }
 
 // ---- simple batches: each DataPacket is message number (its rank among the DataPackets).  The
@@ -371,9 +388,22 @@ __global__ __launch_bounds__(256) void emit_simple_kernel(Args a, const Pair* tp
 __global__ __launch_bounds__(256) void key_kernel(Args a, const unsigned* gate) {
     if (gated_off(gate)) return;
     const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
-    if (i >= a.n) return;
-    const u32 s = a.slot[i];
-    a.gid[i] = s == kNoSlot ? a.nodata : a.first[s];
+    bool down = false;  // a key below its predecessor's: the batch needs the sort
+    if (i < a.n && !*a.nonmono) {  // the run head: every datagram is a pending DataPacket here
+        u64 h = i;
+        const u64 r = a.rpc[i];
+        while (h > 0 && a.rpc[h - 1] == r) --h;
+        a.gid[i] = (u32)h;  // non-decreasing
+    } else if (i < a.n) {
+        const u32 s = a.slot[i];
+        const u32 g = s == kNoSlot ? a.nodata : a.first[s];
+        a.gid[i] = g;
+        if (i > 0) {
+            const u32 sp = a.slot[i - 1];
+            down = g < (sp == kNoSlot ? a.nodata : a.first[sp]);
+        }
+    }
+    if (__syncthreads_or(down) && threadIdx.x == 0) atomicOr(a.unsorted, 1u);
 }
 
 __device__ inline bool seq_complete(const SeqState& x) {
@@ -395,12 +425,47 @@ __global__ __launch_bounds__(256) void group_kernel(Args a, const unsigned* gate
     if (gated_off(gate)) return;
     const u64 q0 = (u64)blockIdx.x * 256 + threadIdx.x;
     if (q0 >= a.n) return;
+    if (!*a.unsorted) {  // the keys were in order already: the sort left them in gid / idx
+        a.gs = a.gid;
+        a.is = a.idx;
+    }
     const u32 g = a.gs[q0];
     if (g == a.nodata) return;                   // not a DataPacket (sorted last)
     if (q0 > 0 && a.gs[q0 - 1] == g) return;     // not the first of its group
     u64 e = q0 + 1;
     while (e < a.n && a.gs[e] == g) ++e;
     const u64 k = e - q0;                        // sequence numbers >= k can never complete
+    {  // the run the packetizer sends: one message of k packets, SeqNumber 0..k-1 in order,
+       // TotalPackets k, one fragment each.  The machine below completes it at its last packet
+       // with the packets in arrival order as the segments; say so without the per-sequence state.
+        bool fast = true;
+        u64 bytes = 0;
+        for (u64 t = 0; t < k && fast; ++t) {
+            const u32 j = a.is[q0 + t];
+            const u64 m = a.meta[j];
+            fast = m_seq(m) == t && m_total(m) == k && m_fidx(m) == 0 && !m_more(m);
+            bytes += a.plen[j];
+        }
+        if (fast) {
+            const u32 jl = a.is[e - 1];
+            if constexpr (PASS == 0) {
+                a.cnt[jl] = Pair{bytes, (k << 32) | 1u};
+                for (u64 t = 0; t < k; ++t) a.status[a.is[q0 + t]] = SYM_RX_CONSUMED;
+            } else {
+                const Pair pp = a.pre[jl];
+                const u64 mi = pp.count & 0xffffffffull, sb = pp.count >> 32;
+                a.msg_off[mi] = pp.bytes;
+                a.msg_rpc[mi] = a.rpc[jl];
+                a.msg_dg[mi] = jl;
+                for (u64 t = 0; t < k; ++t) {
+                    const u32 j = a.is[q0 + t];
+                    a.seg_src[sb + t] = a.dg_off[j] + kHdr;
+                    a.seg_len[sb + t] = a.plen[j];
+                }
+            }
+            return;
+        }
+    }
     SeqState* S = a.state + q0;
     for (u64 t = 0; t < k; ++t) S[t] = SeqState{};
     u64 r = q0;  // first datagram of the current message
@@ -549,7 +614,7 @@ inline unsigned key_bits(u64 n) { return log2u(n + 1) + 1; }  // keys in [0, n]
 
 struct Layout {
     size_t table, first, slot, rpc, meta, plen, gid, idx, gs, is, state, cnt, pre, agg, tpre, seg_src, seg_len, agg2,
-        pre2, nseg, nseg2, flag, hist, rowtot, total;
+        pre2, agg3, pre3, nseg, nseg2, flag, unsorted, nonmono, hist, rowtot, total;
 };
 
 inline u64 sort_tiles(u64 n) { return (n + kSortTile - 1) / kSortTile; }
@@ -582,9 +647,13 @@ inline Layout layout(u64 n) {
     L.seg_len = take(n * 8);
     L.agg2 = take((tiles(n) + 1) * sizeof(Pair));
     L.pre2 = take((tiles(n) + 1) * sizeof(Pair));
+    L.agg3 = take((tiles(n) + 1) * sizeof(Pair));  // the single-datagram path's own (it runs beside the general path)
+    L.pre3 = take((tiles(n) + 1) * sizeof(Pair));
     L.nseg = take(8);
-    L.nseg2 = take(16);  // the general path's segment count, then the parse's flag: zeroed together
-    L.flag = L.nseg2 + 8;
+    L.nseg2 = take(32);  // the general path's segment count, the parse's flag, the key order and
+    L.flag = L.nseg2 + 8;  // RPCID order flags: zeroed together
+    L.unsorted = L.nseg2 + 12;
+    L.nonmono = L.nseg2 + 16;
     L.hist = take((size_t)kDigits * sort_tiles(n) * 4);
     L.rowtot = take(kDigits * 4);
     L.total = o;
@@ -597,7 +666,7 @@ size_t reassemble_ws_bytes(u64 n) { return rx::layout(n).total; }
 
 hipError_t launch_reassemble(const uint8_t* wire, const u64* dg_off, u64 n, uint8_t* msg, u64 msg_cap, u64* msg_off,
                              u64* msg_rpc, u64* msg_dg, u64* nmsg, uint8_t* status, void* ws, unsigned* err,
-                             hipStream_t stream) {
+                             hipStream_t stream, hipStream_t aux, hipEvent_t fork, hipEvent_t join) {
     using rx::Pair;
     const rx::Layout L = rx::layout(n);
     char* w = (char*)ws;
@@ -626,6 +695,8 @@ hipError_t launch_reassemble(const uint8_t* wire, const u64* dg_off, u64 n, uint
     a.msg_dg = msg_dg;
     a.seg_src = (u64*)(w + L.seg_src);
     a.seg_len = (u64*)(w + L.seg_len);
+    a.unsorted = (unsigned*)(w + L.unsorted);
+    a.nonmono = (const unsigned*)(w + L.nonmono);
     const dim3 b256(256);
     const unsigned* flag = (const unsigned*)(w + L.flag);
     const dim3 gq((unsigned)rx::tiles(n));
@@ -635,13 +706,13 @@ hipError_t launch_reassemble(const uint8_t* wire, const u64* dg_off, u64 n, uint
     a.agg = agg;
     // the payload segments' tile prefixes, then the gather (segment count on the device); gate:
     // the general path's copy, which does nothing for a simple batch
-    auto seg_tail = [&](u64* nseg, const unsigned* gate) -> hipError_t {
-        Pair* agg2 = (Pair*)(w + L.agg2);
-        Pair* pre2 = (Pair*)(w + L.pre2);
-        hipLaunchKernelGGL(rx::seg_tile_total_kernel, dim3((unsigned)ns), b256, 0, stream, (const u64*)a.seg_len,
+    auto seg_tail = [&](u64* nseg, const unsigned* gate, hipStream_t st) -> hipError_t {
+        Pair* agg2 = (Pair*)(w + (gate ? L.agg2 : L.agg3));
+        Pair* pre2 = (Pair*)(w + (gate ? L.pre2 : L.pre3));
+        hipLaunchKernelGGL(rx::seg_tile_total_kernel, dim3((unsigned)ns), b256, 0, st, (const u64*)a.seg_len,
                            (const u64*)nseg, agg2, gate);
         hipError_t r = hipGetLastError();
-        if (r == hipSuccess) r = launch_tile_scan_gated(agg2, pre2, ns, gate, stream);
+        if (r == hipSuccess) r = launch_tile_scan_gated(agg2, pre2, ns, gate, st);
         if (r != hipSuccess) return r;
         raw::GatherArgs ga{};
         ga.in = wire;
@@ -655,32 +726,44 @@ hipError_t launch_reassemble(const uint8_t* wire, const u64* dg_off, u64 n, uint
         ga.out = msg;
         ga.cap = msg_cap;
         ga.err = err;
-        return launch_segment_gather(ga, stream);
+        return launch_segment_gather(ga, st);
     };
     // Simple batches (every DataPacket one whole message) complete here: parse (with the tile
     // totals of the per-arrival triples), their scan, the messages, the gather.  For other batches
     // the emit writes no message and zero segments, so this gather is empty.
     u64* nseg = (u64*)(w + L.nseg);
     u64* nseg2 = (u64*)(w + L.nseg2);
-    hipError_t e = hipMemsetAsync(w + L.nseg2, 0, 16, stream);  // nseg2 and the flag
+    hipError_t e = hipMemsetAsync(w + L.nseg2, 0, 32, stream);  // nseg2 and the flags
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(rx::parse_kernel, dim3((unsigned)nt), b256, 0, stream, a, (unsigned*)flag);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = launch_tile_scan(agg, tpre, nt, stream)) != hipSuccess) return e;
+    // The general path is queued for every batch; each of its kernels exits at once unless the
+    // parse set the flag (no host read: the call stays asynchronous).  It runs on `aux`, forked
+    // here and joined at the end, so for a simple batch its ~20 empty launches overlap the copy
+    // below.  The two branches share no buffer that both write for the same batch: every write of
+    // the simple branch past this point is for a simple batch (its segment scan excepted, which
+    // has agg3 / pre3 to itself), every write of the general branch for a complex one.
+    hipStream_t gs = stream;
+    if (aux && fork && join) {
+        if ((e = hipEventRecord(fork, stream)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(aux, fork, 0)) != hipSuccess) return e;
+        gs = aux;
+    }
     hipLaunchKernelGGL(rx::emit_simple_kernel, dim3((unsigned)nt), b256, 0, stream, a, (const Pair*)tpre, flag, nmsg,
                        nseg);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    if ((e = seg_tail(nseg, nullptr)) != hipSuccess) return e;
-    // The general path, queued for every batch; each kernel exits at once unless the parse set the
-    // flag (no host read, the stream stays asynchronous).
-    hipLaunchKernelGGL(rx::init_kernel, dim3((unsigned)std::min<u64>(rx::tiles(TS + 1), 4096)), b256, 0, stream, a.table,
-                       a.first, TS, flag);
+    if ((e = seg_tail(nseg, nullptr, stream)) != hipSuccess) return e;
+    hipLaunchKernelGGL(rx::order_kernel, gq, b256, 0, gs, a, flag, (unsigned*)a.nonmono);
+    hipLaunchKernelGGL(rx::init_kernel, dim3((unsigned)std::min<u64>(rx::tiles(TS + 1), 4096)), b256, 0, gs, a.table,
+                       a.first, TS, a.nonmono);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(rx::hash_kernel, gq, b256, 0, stream, a, flag);
+    hipLaunchKernelGGL(rx::hash_kernel, gq, b256, 0, gs, a, flag);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(rx::key_kernel, gq, b256, 0, stream, a, flag);
+    hipLaunchKernelGGL(rx::key_kernel, gq, b256, 0, gs, a, flag);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    {  // 2. the stable radix sort, ping-ponging between (gid, idx) and (gs, is)
+    {  // 2. the stable radix sort, ping-ponging between (gid, idx) and (gs, is); only when the keys
+       // are out of order (set by key_kernel, so only for a batch on the general path)
         u32* kb[2] = {a.gid, (u32*)(w + L.gs)};
         u32* vb[2] = {a.idx, (u32*)(w + L.is)};
         const u64 st = rx::sort_tiles(n);
@@ -689,32 +772,37 @@ hipError_t launch_reassemble(const uint8_t* wire, const u64* dg_off, u64 n, uint
         const unsigned bits = rx::key_bits(n);
         int cur = 0;
         for (unsigned shift = 0; shift < bits; shift += 8, cur ^= 1) {
-            hipLaunchKernelGGL(rx::sort_hist_kernel, dim3((unsigned)st), b256, 0, stream, (const u32*)kb[cur], n,
-                               (int)shift, hist, st, flag);
-            hipLaunchKernelGGL(rx::sort_rowscan_kernel, dim3(rx::kDigits), b256, 0, stream, hist, st, rowtot, flag);
-            hipLaunchKernelGGL(rx::sort_scatter_kernel, dim3((unsigned)st), b256, 0, stream, (const u32*)kb[cur],
+            hipLaunchKernelGGL(rx::sort_hist_kernel, dim3((unsigned)st), b256, 0, gs, (const u32*)kb[cur], n,
+                               (int)shift, hist, st, a.unsorted);
+            hipLaunchKernelGGL(rx::sort_rowscan_kernel, dim3(rx::kDigits), b256, 0, gs, hist, st, rowtot, a.unsorted);
+            hipLaunchKernelGGL(rx::sort_scatter_kernel, dim3((unsigned)st), b256, 0, gs, (const u32*)kb[cur],
                                (const u32*)vb[cur], kb[cur ^ 1], vb[cur ^ 1], n, (int)shift, (const u32*)hist, st,
-                               (const u32*)rowtot, flag);
+                               (const u32*)rowtot, a.unsorted);
             if ((e = hipGetLastError()) != hipSuccess) return e;
         }
         a.gs = kb[cur];
         a.is = vb[cur];
     }
-    hipLaunchKernelGGL(rx::group_kernel<0>, gq, b256, 0, stream, a, flag);
+    hipLaunchKernelGGL(rx::group_kernel<0>, gq, b256, 0, gs, a, flag);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(rx::pair_tile_total_kernel, dim3((unsigned)nt), b256, 0, stream, (const Pair*)a.cnt, n + 1, agg,
+    hipLaunchKernelGGL(rx::pair_tile_total_kernel, dim3((unsigned)nt), b256, 0, gs, (const Pair*)a.cnt, n + 1, agg,
                        flag);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    if ((e = launch_tile_scan_gated(agg, tpre, nt, flag, stream)) != hipSuccess) return e;
-    hipLaunchKernelGGL(rx::pair_scan_apply_kernel, dim3((unsigned)nt), b256, 0, stream, (const Pair*)a.cnt, n + 1,
+    if ((e = launch_tile_scan_gated(agg, tpre, nt, flag, gs)) != hipSuccess) return e;
+    hipLaunchKernelGGL(rx::pair_scan_apply_kernel, dim3((unsigned)nt), b256, 0, gs, (const Pair*)a.cnt, n + 1,
                        (const Pair*)tpre, (Pair*)(w + L.pre), flag);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(rx::finalize_kernel, dim3(1), dim3(1), 0, stream, (const Pair*)(w + L.pre) + n, msg_off, nmsg,
+    hipLaunchKernelGGL(rx::finalize_kernel, dim3(1), dim3(1), 0, gs, (const Pair*)(w + L.pre) + n, msg_off, nmsg,
                        nseg2, flag);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(rx::group_kernel<1>, gq, b256, 0, stream, a, flag);
+    hipLaunchKernelGGL(rx::group_kernel<1>, gq, b256, 0, gs, a, flag);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    return seg_tail(nseg2, flag);
+    if ((e = seg_tail(nseg2, flag, gs)) != hipSuccess) return e;
+    if (gs != stream) {
+        if ((e = hipEventRecord(join, gs)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(stream, join, 0)) != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 }  // namespace symhip

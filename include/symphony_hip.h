@@ -349,7 +349,9 @@ int sym_firewall_filter(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec
  * When every DataPacket is a whole message (TotalPackets 1, one fragment) the messages are the
  * DataPackets in arrival order, found on the device without grouping.  The general path --
  * grouping, sort, the ProcessFragment state machine -- is queued too and its kernels exit at once
- * for such a batch: the call is asynchronous on `stream` like the others (no host read). */
+ * for such a batch: the call is asynchronous on `stream` like the others (no host read).  It runs
+ * on a stream of the ctx forked from `stream` after the parse and joined back before the call's
+ * last operation (events; stream capture follows both). */
 #define SYM_RX_CONSUMED 0   /* part of a returned message */
 #define SYM_RX_PENDING 1    /* still held by the reassembler after the batch */
 #define SYM_RX_NOT_DATA 2   /* not a Request / Response DataPacket: not reassembled */
