@@ -254,3 +254,44 @@ def test_reassembly_one_fragment_makes_batch_general_gpu(gcodec, gdev, where):
     dgs = singles[:pos] + [dgram(999, 2, 1, b"tail"), dgram(999, 2, 0, b"head")] + singles[pos:]
     want = _gpu_vs_oracle(gcodec, gdev, *batch(dgs))
     assert len(want[2]) == 301
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg,mtu", [("config2", 1400), ("config3", 1400), ("config3", 300)])
+def test_reassembly_send_order_gpu(gcodec, gdev, cfg, mtu):
+    """The packetizer's send order: RPCIDs never decrease, so the groups are the runs of equal RPCIDs
+    (no hash table) and each run is one message of packets 0..T-1 (no per-sequence state)."""
+    stream, off, rpc, wire, dg_off = packetized(datagen.CONFIG2 if cfg == "config2" else datagen.CONFIG3, 20000, mtu)
+    want = _gpu_vs_oracle(gcodec, gdev, wire, dg_off)
+    assert len(want[2]) == 20000 and (want[4] == C).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_reassembly_nondecreasing_rpcids_gpu(gcodec, gdev, seed):
+    """RPCIDs that never decrease but whose runs are not one clean message each: an RPCID reused
+    back to back, packets out of order or duplicated inside a run, incomplete runs, extra
+    sequences, fragment indices -- the run-head grouping with the full ProcessFragment machine."""
+    rng = np.random.default_rng(seed)
+    dgs = []
+    r = 10
+    for _ in range(400):
+        r += int(rng.integers(0, 3))  # 0: the previous RPCID again
+        T = int(rng.integers(1, 5))
+        seqs = list(range(T))
+        kind = int(rng.integers(0, 5))
+        if kind == 1:
+            rng.shuffle(seqs)
+        elif kind == 2:
+            seqs = seqs + [int(rng.integers(0, T))]  # a duplicate
+        elif kind == 3 and T > 1:
+            seqs = seqs[:-1]  # incomplete
+        elif kind == 4:
+            seqs = seqs + [T + 1]  # a sequence number past TotalPackets
+        for s in seqs:
+            if kind == 4 and T == 1 and rng.random() < 0.3:
+                dgs.append(dgram(r, T, s, b"-second", fidx=1))
+                dgs.append(dgram(r, T, s, b"first", more=True))
+            else:
+                dgs.append(dgram(r, T, s, bytes(rng.integers(0, 256, int(rng.integers(0, 40)), dtype=np.uint8))))
+    _gpu_vs_oracle(gcodec, gdev, *batch(dgs), misalign=seed)
