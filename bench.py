@@ -718,8 +718,8 @@ def config3_leg(codec: Codec, dev, reps: int, cfg=None) -> dict:
             "encode_ms": round(enc_ms, 4), "encode_gbps": round(enc_b / enc_ms / 1e6, 1),
             "decode_ms": round(dec_ms, 4), "decode_gbps": round(dec_b / dec_ms / 1e6, 1),
             "gbps_algorithmic": round((enc_b + dec_b) / (enc_ms + dec_ms) / 1e6, 1),
-            "kernels": {"encode": "encode_kernel<0, 2, 1, false, 4, false>",
-                        "decode": "decode_pipe_kernel<0, 2, false, 0, 0, 2, 2, 22528, false, 0, false>"},
+            "kernels": {"encode": "encode_kernel<0, 2, 1, false, 4, false, 64>",
+                        "decode": "decode_pipe_kernel<0, 2, false, 0, 0, 2, 2, 22528, false, 0, false, 0>"},
             "note": "config 3 (seed 0x5EED0002), the headline's algorithmic byte definition"}
 
 
@@ -910,9 +910,9 @@ def main():
         glob = {"rank0_base": base, "global_stream_bytes": gtotal, "global_records": n * world}
     # roofline: the dominant single kernel by time (the default decode is one launch)
     if enc_ms >= dec_ms:
-        kname, dom_ms, dom_bytes = f"encode_kernel<{s.nfixed}, {s.nvar}, 1, false, 4, false>", enc_ms, enc_b
+        kname, dom_ms, dom_bytes = f"encode_kernel<{s.nfixed}, {s.nvar}, 1, false, 4, false, 64>", enc_ms, enc_b
     else:
-        kname, dom_ms, dom_bytes = (f"decode_pipe_kernel<{s.nfixed}, {s.nvar}, false, 0, 0, 2, 2, 22528, false, 0, false>",
+        kname, dom_ms, dom_bytes = (f"decode_pipe_kernel<{s.nfixed}, {s.nvar}, false, 0, 0, 2, 2, 22528, false, 0, false, 0>",
                                      dec_ms, dec_b)
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     traffic = load_traffic(kname)
@@ -945,7 +945,7 @@ def main():
                                "gbps": round(enc_b / enc_ms / 1e6, 1)},
                     "decode": {"avg_ms": round(dec_ms, 4), "alg_bytes": dec_b,
                                "gbps": round(dec_b / dec_ms / 1e6, 1),
-                               "kernel": f"decode_pipe_kernel<{s.nfixed}, {s.nvar}, false, 0, 0, 2, 2, 22528, false, 0, false>",
+                               "kernel": f"decode_pipe_kernel<{s.nfixed}, {s.nvar}, false, 0, 0, 2, 2, 22528, false, 0, false, 0>",
                                **refs}},
         "per_gpu_gbps": round((enc_b + dec_b) * args.steps / elapsed / 1e9, 2),
         "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
