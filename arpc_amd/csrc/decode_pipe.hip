@@ -290,7 +290,7 @@ __device__ void lookback(const DecodeParams& p, u64* aw, u64* pw, u64 ntiles, u6
 // when AHEAD % 8 == 0, so the header lines it reads are still in that XCD's L2 when tile t + AHEAD
 // is staged, and the stream is fetched from HBM about once.
 template <int NF, int NV, bool MIX, int MODE = 0, int DIAG = 0, int SK = 4, int PR = 2, int STG = kStage,
-          bool EARLY = false, int PACE = 0, bool XCDP = false, int AHEAD = 0>
+          bool EARLY = false, int PACE = 0, bool XCDP = false, int AHEAD = 0, int NOP = 0>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))) void decode_pipe_kernel(
     DecodeParams p, u64* flags, u32 epoch) {
     static_assert(NV == 1 || NV == 2, "decode handles one or two string columns");
@@ -381,7 +381,15 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
 #pragma unroll
         for (int f = 0; f < NV; ++f) flen[f] = fpos[f] = 0;
         const int nvr = rec_nvar<NV, MIX>(p, live ? r0 + lane : 0);
-        if (live) {
+        if (NOP && live) {  // timing only: the config-2 SetRequest layout assumed, no LDS reads
+            flen[0] = 64;
+            fpos[0] = 26;
+            if constexpr (NV == 2) {
+                flen[1] = L - 94;
+                fpos[1] = 94;
+            }
+            p.status[r0 + lane] = 0;
+        } else if (live) {
             if (L < 13) {
                 st = SYM_STATUS_TOO_SHORT;  // "invalid data: too short" (kv.syn.go:681-683)
             } else if (rd8(0) != 0x01) {
@@ -860,7 +868,7 @@ hipError_t launch_gather_layout(const DecodeParams& p, u64* flags, u32 epoch, hi
 }
 
 template <int NF, int NV, bool MIX, int MODE, int DIAG, int SK = 4, int PR = 2, int STG = kStage, bool EARLY = false,
-          int PACE = 0, bool XCDP = false, int AHEAD = 0>
+          int PACE = 0, bool XCDP = false, int AHEAD = 0, int NOP = 0>
 hipError_t launch(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stream, int pnum = 1, int pden = 1) {
     if (DIAG && !p.dbg) return hipErrorInvalidValue;  // timestamps need SYMHIP_DEBUG_PTR (tuning builds)
     static int cus[16] = {0};
@@ -877,7 +885,7 @@ hipError_t launch(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stre
     DecodeParams q = p;
     q.pipe_parsers = (unsigned)P;
     const u64 grid = kRoles ? P + 1 + nt : nt;
-    hipLaunchKernelGGL((decode_pipe_kernel<NF, NV, MIX, MODE, DIAG, SK, PR, STG, EARLY, PACE, XCDP, AHEAD>), dim3((unsigned)grid),
+    hipLaunchKernelGGL((decode_pipe_kernel<NF, NV, MIX, MODE, DIAG, SK, PR, STG, EARLY, PACE, XCDP, AHEAD, NOP>), dim3((unsigned)grid),
                        dim3(kThreads), 0, stream, q, flags, epoch);
     return hipGetLastError();
 }
@@ -887,11 +895,11 @@ constexpr int kParsersNum = 3;   // parser workgroups = #CUs * 3/4
 constexpr int kParsersDen = 4;
 
 template <int MODE, int DIAG, int SK = kScanPer, int PR = 2, int STG = kStage, bool EARLY = false, int PACE = 0,
-          bool XCDP = false, int AHEAD = 0>
+          bool XCDP = false, int AHEAD = 0, int NOP = 0>
 hipError_t launch_layout(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stream, int pnum = kParsersNum,
                          int pden = kParsersDen) {
 #define SYMHIP_PIPE_LAUNCH(NF, NV, MIX) \
-    launch<NF, NV, MIX, MODE, DIAG, SK, PR, STG, EARLY, PACE, XCDP, AHEAD>(p, flags, epoch, stream, pnum, pden)
+    launch<NF, NV, MIX, MODE, DIAG, SK, PR, STG, EARLY, PACE, XCDP, AHEAD, NOP>(p, flags, epoch, stream, pnum, pden)
     if (p.type)  // mixed kv batch: GetRequest / SetRequest per record
         return p.lay.nfixed == 0 && p.lay.nvar == 2 ? SYMHIP_PIPE_LAUNCH(0, 2, true) : hipErrorInvalidValue;
     if (p.lay.nfixed == 0 && p.lay.nvar == 1) return SYMHIP_PIPE_LAUNCH(0, 1, false);
@@ -966,6 +974,10 @@ hipError_t launch_decode_pipe(const DecodeParams& p, void* flags, unsigned epoch
         case 622: return pipe::launch_layout<0, 0, 2, 2, pipe::kStage, false, 0, false, 1024>(p, fl, epoch, stream);
         case 623: return pipe::launch_layout<0, 0, 2, 2, pipe::kStage, false, 0, false, 2048>(p, fl, epoch, stream);
         case 624: return pipe::launch_layout<0, 0, 2, 2, pipe::kStage, false, 0, false, 4096>(p, fl, epoch, stream);
+        // round 3: the copier's parse replaced by the config-2 layout (timing bound of a parse-free copier)
+        case 700: return pipe::launch_layout<0, 0, 2, 2, pipe::kStage, false, 0, false, 0, 1>(p, fl, epoch, stream);
+        case 701: return pipe::launch_layout<1, 0, 2, 2, pipe::kStage, false, 0, false, 0, 1>(p, fl, epoch, stream);
+        case 702: return pipe::launch_layout<2, 0, 2, 2, pipe::kStage, false, 0, false, 0, 1>(p, fl, epoch, stream);
         // the gather copier (no LDS stage, output-stationary copy); 601: its timing mode (WRONG output)
         case 600: return pipe::launch_gather_layout<0>(p, fl, epoch, stream);
         case 601: return pipe::launch_gather_layout<1>(p, fl, epoch, stream);

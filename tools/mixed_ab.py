@@ -23,6 +23,10 @@ from arpc_amd import datagen  # noqa: E402
 from arpc_amd.codec import Codec, DecodedBatch  # noqa: E402
 
 
+# timing-only decode variants that give wrong output by design (tools/kbench.py)
+WRONG_OUTPUT = {402, 412, 475, 476, 482, 483, 492, 504, 601, 701, 702}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--enc", default="0,20")
@@ -49,6 +53,10 @@ def main():
         sets.append((t, key, val, out, dec))
     enc_alg = n + kb + 8 * (n + 1) + vb + 8 * (n + 1) + total + 8 * (n + 1)
     dec_alg = total + 8 * (n + 1) + n + kb + vb + 16 * (n + 1) + n
+    for t, key, val, out, dec in sets:  # every decode variant reads a valid stream, even with --enc ""
+        codec.encode_kv_mixed(t, key, val, 1, 1, 2, out=out[0], out_off=out[1])
+    torch.cuda.synchronize()
+    codec.check()
     variants = [("enc", int(v)) for v in a.enc.split(",") if v] + [("dec", int(v)) for v in a.dec.split(",") if v]
     times = {v: [] for v in variants}
     ref = {}
@@ -72,7 +80,8 @@ def main():
                     else:
                         dg = tuple(int(x.to(torch.int64).sum().item()) for x in
                                    (dec.var[0][0][:kb], dec.var[0][1], dec.var[1][0][:vb], dec.var[1][1], dec.status))
-                    assert ref.setdefault((kind, k), dg) == dg, f"{kind} variant {v} differs on set {k}"
+                    if not (kind == "dec" and v in WRONG_OUTPUT):
+                        assert ref.setdefault((kind, k), dg) == dg, f"{kind} variant {v} differs on set {k}"
                 else:
                     times[(kind, v)].append(e0.elapsed_time(e1))
     for (kind, v), ts in times.items():
