@@ -82,14 +82,16 @@ int ensure_flags(sym_ctx* ctx, uint64_t n) {
     return SYM_OK;
 }
 
-// The next call's epoch; on wrap-around every word is zeroed again (stream-ordered) first.
-int next_epoch(sym_ctx* ctx, hipStream_t stream, unsigned* epoch) {
-    if (++ctx->epoch >= symhip::kEpochLimit) {
+// The next call's epochs [*epoch, *epoch + span); on wrap-around every word is zeroed again
+// (stream-ordered) first.  A decode takes two: its gate's exact re-decode tags its words epoch + 1.
+int next_epoch(sym_ctx* ctx, hipStream_t stream, unsigned* epoch, unsigned span = 1) {
+    if (ctx->epoch + span >= symhip::kEpochLimit) {
         hipError_t e = hipMemsetAsync(ctx->flags, 0, ctx->flag_bytes, stream);
         if (e != hipSuccess) return hip_fail(e, "zeroing look-back words");
-        ctx->epoch = 1;
+        ctx->epoch = 0;
     }
-    *epoch = ctx->epoch;
+    *epoch = ctx->epoch + 1;
+    ctx->epoch += span;
     return SYM_OK;
 }
 
@@ -294,7 +296,7 @@ int symhip::capi::decode_call(const char* what, sym_ctx* ctx, Layout lay, const 
     int rc = ensure_ws(ctx, lay.nvar, n);
     if (rc == SYM_OK) rc = ensure_flags(ctx, n);
     unsigned epoch = 0;
-    if (rc == SYM_OK) rc = next_epoch(ctx, (hipStream_t)stream, &epoch);
+    if (rc == SYM_OK) rc = next_epoch(ctx, (hipStream_t)stream, &epoch, 2);
     if (rc != SYM_OK) return rc;
     DecodeParams p{};
     p.lay = lay;

@@ -11,6 +11,11 @@
 //   [0, P)      parsers: a wave reads the headers of 64-record tiles (two 16-byte loads per record
 //               into registers, global loads past that window), runs Go's checks for the field
 //               lengths only, and publishes the tile's per-column aggregate word.  They never wait.
+//               kv layouts (no int32 fields) by default parse SPECULATIVELY: the lengths a record
+//               laid out as the generator writes it has, from its length alone and at most one
+//               4-byte load (spec_flen) -- the parsers' header reads were ~10 % of the decode time.
+//               Every copier checks them against Go's exact parse of its staged bytes; a second
+//               launch (the gate) decodes the batch again exactly if any was wrong.
 //   P           scanner: walks the tiles in order, 1024 per step, and publishes every tile's
 //               exclusive prefix word up to the first tile whose aggregate is not yet published.
 //   P + 1 + t   copier of tile t:
@@ -57,6 +62,15 @@ constexpr int kU = 2;           // copy chunks per lane per step
 
 
 __host__ __device__ inline u64 num_tiles(u64 n) { return (n + kRecs - 1) / kRecs; }
+
+// Control words after the aggregate / prefix words and the scanner's 256-byte sink
+// (decode_pipe_flag_bytes): [kCtrlMismatch] tagged with the call's epoch when a copier found a
+// speculative length wrong; [kCtrlSpecErr] tagged when the speculative launch saw a capacity error
+// (value: the kErr bits), merged into p.err by the gate or dropped with a re-decode.  Words of other
+// calls (other tags, or another call's words where a larger batch put them) are ignored.
+constexpr int kCtrlMismatch = 0;
+constexpr int kCtrlSpecErr = 1;
+__device__ __forceinline__ u64* ctrl_words(u64* flags, int nv, u64 ntiles) { return flags + (size_t)2 * nv * ntiles + 32; }
 
 template <int NV, int STG>
 struct alignas(16) Lds {
@@ -186,12 +200,70 @@ __device__ __forceinline__ void parse_tiles(const DecodeParams& p, u64* aw, u64 
     }
 }
 
+// Speculative field lengths of a kv record (NF == 0): in a record laid out as the generator writes it
+// (public version, off2p = 13, ids, private version, table, then the string fields back to back up to
+// the record's end; main.go:439-620), the last string field's length is the bytes left after the
+// others: 14 + 8 * fields bytes of header, table and length prefixes.  So a one-field
+// (GetRequest-shaped) record needs no header read, a two-field one only its first length prefix
+// (bytes 22..25, k0).  The copier checks these against Go's exact parse of its
+// staged bytes (spec_check) and a batch with any difference is decoded again exactly.
+template <int NV>
+__device__ __forceinline__ void spec_flen(u64 L, int nvr, u32 k0, u64 (&flen)[NV]) {
+    flen[0] = 0;
+    if constexpr (NV == 2) flen[1] = 0;
+    if (nvr == 1) {
+        if (L >= 22) flen[0] = L - 22;
+    } else if (NV == 2 && L >= 30 && L - 30 >= (u64)k0) {
+        flen[0] = k0;
+        if constexpr (NV == 2) flen[NV - 1] = L - 30 - k0;
+    }
+}
+
+// parse_tiles with speculative lengths: the record offsets (and types), plus one 4-byte load per
+// two-field record.
+template <int NV, bool MIX, int R>
+__device__ __forceinline__ void parse_tiles_spec(const DecodeParams& p, u64* aw, u64 ntiles, u32 epoch, const u64 (&th)[R]) {
+    const int lane = threadIdx.x & 63;
+    const u64 n = p.n;
+    const uintptr_t in = (uintptr_t)p.in;
+    bool live[R];
+    u64 L[R];
+    int nvr[R];
+    u32 k0[R];
+#pragma unroll
+    for (int h = 0; h < R; ++h) {
+        const u64 r = th[h] * kRecs + lane;
+        live[h] = th[h] < ntiles && r < n;
+        const u64 rc = live[h] ? r : n;
+        const u64 st = p.rec_off[rc];
+        L[h] = p.rec_off[live[h] ? rc + 1 : rc] - st;
+        nvr[h] = rec_nvar<NV, MIX>(p, live[h] ? r : 0);
+        const bool rd = live[h] && nvr[h] == 2 && L[h] >= 30;
+        k0[h] = *(gc_u32*)(rd ? in + st + 22 : (uintptr_t)aw);
+    }
+#pragma unroll
+    for (int h = 0; h < R; ++h) {
+        u64 flen[NV];
+        spec_flen<NV>(live[h] ? L[h] : 0, nvr[h], k0[h], flen);
+        if (th[h] < ntiles) {
+#pragma unroll
+            for (int f = 0; f < NV; ++f) {
+                const u64 inc = wave_incl_scan_u32w_dpp((u32)flen[f]);
+                const u64 agg = (u64)__builtin_amdgcn_readlane((u32)inc, 63) |
+                                ((u64)__builtin_amdgcn_readlane((u32)(inc >> 32), 63) << 32);
+                if (lane == f) store_word(&aw[(size_t)f * ntiles + th[h]], make_word(epoch, kStAgg, agg));
+            }
+        }
+    }
+}
+
 // PACE > 0: a parser wave starts a step only once tile t0 - PACE has its prefix (bounded wait), so
 // the header lines it reads are still cached when that tile's copier stages them.  XCDP: a parser
 // takes only tiles whose copier shares its blockIdx % 8 group (one XCD under round-robin placement),
 // so those lines are in that XCD's L2 (speed only; any placement gives the same results).  tmax:
 // only tiles below it (the copiers parse the others ahead, AHEAD in decode_pipe_kernel).
-template <int NF, int NV, bool MIX, int R = 2, int WB = 32, bool LIGHT = false, int PACE = 0, bool XCDP = false>
+template <int NF, int NV, bool MIX, int R = 2, int WB = 32, bool LIGHT = false, int PACE = 0, bool XCDP = false,
+          bool SPEC = false>
 __device__ void parser(const DecodeParams& p, u64* aw, u64* pw, u64 ntiles, u32 epoch, u32 P, u64 tmax = ~0ull) {
     const int wave = threadIdx.x >> 6;
     const u64 tlim = min(ntiles, tmax);
@@ -219,7 +291,8 @@ __device__ void parser(const DecodeParams& p, u64* aw, u64* pw, u64 ntiles, u32 
                     __builtin_amdgcn_s_sleep(8);
             }
         }
-        parse_tiles<NF, NV, MIX, R, WB, LIGHT>(p, aw, ntiles, epoch, th);
+        if constexpr (SPEC && NF == 0) parse_tiles_spec<NV, MIX, R>(p, aw, ntiles, epoch, th);
+        else parse_tiles<NF, NV, MIX, R, WB, LIGHT>(p, aw, ntiles, epoch, th);
     }
 }
 
@@ -278,24 +351,16 @@ __device__ void lookback(const DecodeParams& p, u64* aw, u64* pw, u64 ntiles, u6
     lookback_with<NV>(aw, pw, ntiles, tile, epoch, pre, [&](u64 t, u64 (&a)[NV]) { tile_agg_global<NF, NV, MIX>(p, t, a); });
 }
 
-// ---------------------------------------------------------------- the kernel
-// MODE 0: the pipeline.  MODE 1: copiers only, every prefix taken as 0 (timing of the data movement
-// alone; wrong output -- tools/kbench.py variant 402).  DIAG: per-tile phase timestamps into p.dbg
-// (8 u64 per tile, s_memrealtime at 100 MHz; tools/fused_timeline.py).
-// STG: staged bytes per tile (LDS: 24.7 KB at kStage -> 6 copiers per CU; below ~21 KB -> 7).
-// EARLY: the prefix word is loaded when the tile starts, so its cross-XCD round trip overlaps the
-// stage instead of following the parse.  PACE, XCDP: see parser().
-// AHEAD > 0: the parsers take only tiles [0, AHEAD); the copier of tile t parses tile t + AHEAD
-// (wave 1, while wave 0 parses its own tile from LDS) -- the same XCD under round-robin placement
-// when AHEAD % 8 == 0, so the header lines it reads are still in that XCD's L2 when tile t + AHEAD
-// is staged, and the stream is fetched from HBM about once.
-template <int NF, int NV, bool MIX, int MODE = 0, int DIAG = 0, int SK = 4, int PR = 2, int STG = kStage,
-          bool EARLY = false, int PACE = 0, bool XCDP = false, int AHEAD = 0, int NOP = 0>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))) void decode_pipe_kernel(
-    DecodeParams p, u64* flags, u32 epoch) {
-    static_assert(NV == 1 || NV == 2, "decode handles one or two string columns");
+// ---------------------------------------------------------------- the copier
+// Tile `tile`: stage, parse (wave 0), prefix, copy.  forced: no parsers / scanner in this launch, so
+// the prefix comes from look-back at once.  SPEC: the parsers published speculative aggregates
+// (parse_tiles_spec); wave 0 compares them record by record with Go's exact parse of the staged
+// bytes and tags ctrl[kCtrlMismatch] on any difference (the gate then decodes the batch again), and
+// a capacity error is tagged in ctrl[kCtrlSpecErr] (it may come from a speculative prefix), merged
+// into p.err by the gate when the speculation held.
+template <int NF, int NV, bool MIX, int MODE, int DIAG, int STG, bool EARLY, int AHEAD, int NOP, bool SPEC>
+__device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 epoch, u64 tile, bool forced, Lds<NV, STG>& S) {
     constexpr int kLoads = (STG / 16 + kThreads - 1) / kThreads;
-    __shared__ Lds<NV, STG> S;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const u64 n = p.n, ntiles = num_tiles(n);
     const uintptr_t in = (uintptr_t)p.in;
@@ -305,22 +370,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
     const uintptr_t safe = (uintptr_t)flags;  // readable filler address for lanes with nothing to load
     u64* aw = flags;                          // aggregate words [NV][ntiles]
     u64* pw = flags + (size_t)NV * ntiles;    // prefix words [NV][ntiles]
-
-    const u32 P = p.pipe_parsers;
-    const bool forced = p.impl == kImplLookback;  // parsers and scanner idle: look-back only
-    // MODE 2 / 3 (timing): roles run, copiers never wait; 3: parsers read only the offsets
-    constexpr bool kRoles = MODE == 0 || MODE == 2 || MODE == 3;
-    if (kRoles && blockIdx.x < P) {
-        if (!forced)
-            parser<NF, NV, MIX, PR, 32, MODE == 3, PACE, XCDP>(p, aw, pw, ntiles, epoch, P, AHEAD > 0 ? (u64)AHEAD : ~0ull);
-        return;
-    }
-    if (kRoles && blockIdx.x == P) {
-        if (!forced) scanner<NV, SK>(aw, pw, ntiles, epoch, S);
-        return;
-    }
-    const u64 tile = kRoles ? blockIdx.x - P - 1 : blockIdx.x;
-    if (tile >= ntiles) return;
     auto stamp = [&](int slot) {
         if constexpr (DIAG)
             if (tid == 0) p.dbg[tile * 8 + slot] = __builtin_amdgcn_s_memrealtime();
@@ -430,6 +479,16 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
 #pragma unroll
             for (int f = 0; f < NF; ++f) p.fixed[f][r0 + lane] = fx[f];
         }
+        u64* const ctrl = ctrl_words(flags, NV, ntiles);
+        if constexpr (SPEC) {  // the parsers' speculative lengths of these records, from the same bytes
+            const u32 k0 = live && nvr == 2 && L >= 30 ? rd32(22) : 0u;
+            u64 sf[NV];
+            spec_flen<NV>(live ? L : 0, nvr, k0, sf);
+            bool mm = false;
+#pragma unroll
+            for (int f = 0; f < NV; ++f) mm |= sf[f] != flen[f];
+            if (__ballot(mm) && lane == 0) store_word(&ctrl[kCtrlMismatch], make_word(epoch, kStAgg, 1));
+        }
         // tile scan of the field lengths (each < 2^32)
         u64 agg[NV], excl[NV];
         u32 nch[NV];
@@ -497,7 +556,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
                 S.dst[f][kRecs] = (int)agg[f];
                 S.pre[f] = pre[f];
                 const i64 cap = (i64)p.cap[f];
-                if (MODE == 0 && agg[f] > 0 && pre[f] + (i64)agg[f] > cap) atomicOr(p.err, kErrCapacity);
+                if (MODE == 0 && agg[f] > 0 && pre[f] + (i64)agg[f] > cap) {
+                    if constexpr (SPEC) store_word(&ctrl[kCtrlSpecErr], make_word(epoch, kStAgg, kErrCapacity));
+                    else atomicOr(p.err, kErrCapacity);
+                }
                 S.lim[f] = max((i64)0, min((i64)agg[f], cap - pre[f]));
             }
             S.total = too_large ? -1 : T;
@@ -574,6 +636,70 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
     stamp(4);
     if constexpr (DIAG)
         if (tid == 0) p.dbg[tile * 8 + 5] = blockIdx.x;
+}
+
+// ---------------------------------------------------------------- the kernel
+// MODE 0: the pipeline.  MODE 1: copiers only, every prefix taken as 0 (timing of the data movement
+// alone; wrong output -- tools/kbench.py variant 402).  DIAG: per-tile phase timestamps into p.dbg
+// (8 u64 per tile, s_memrealtime at 100 MHz; tools/fused_timeline.py).
+// STG: staged bytes per tile (LDS: 24.7 KB at kStage -> 6 copiers per CU; below ~21 KB -> 7).
+// EARLY: the prefix word is loaded when the tile starts, so its cross-XCD round trip overlaps the
+// stage instead of following the parse.  PACE, XCDP: see parser().
+// AHEAD > 0: the parsers take only tiles [0, AHEAD); the copier of tile t parses tile t + AHEAD
+// (wave 1, while wave 0 parses its own tile from LDS) -- the same XCD under round-robin placement
+// when AHEAD % 8 == 0, so the header lines it reads are still in that XCD's L2 when tile t + AHEAD
+// is staged, and the stream is fetched from HBM about once.
+template <int NF, int NV, bool MIX, int MODE = 0, int DIAG = 0, int SK = 4, int PR = 2, int STG = kStage,
+          bool EARLY = false, int PACE = 0, bool XCDP = false, int AHEAD = 0, int NOP = 0, bool SPEC = false, int SPECX = 0>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))) void decode_pipe_kernel(
+    DecodeParams p, u64* flags, u32 epoch) {
+    static_assert(NV == 1 || NV == 2, "decode handles one or two string columns");
+    __shared__ Lds<NV, STG> S;
+    const u64 ntiles = num_tiles(p.n);
+    u64* aw = flags;                        // aggregate words [NV][ntiles]
+    u64* pw = flags + (size_t)NV * ntiles;  // prefix words [NV][ntiles]
+
+    const u32 P = p.pipe_parsers;
+    const bool forced = p.impl == kImplLookback;  // parsers and scanner idle: look-back only
+    // MODE 2 / 3 (timing): roles run, copiers never wait; 3: parsers read only the offsets
+    constexpr bool kRoles = MODE == 0 || MODE == 2 || MODE == 3;
+    if (kRoles && blockIdx.x < P) {
+        if (!forced)
+            parser<NF, NV, MIX, PR, 32, MODE == 3, PACE, XCDP, SPEC>(p, aw, pw, ntiles, epoch, P, AHEAD > 0 ? (u64)AHEAD : ~0ull);
+        return;
+    }
+    if (kRoles && blockIdx.x == P) {
+        if (!forced) scanner<NV, SK>(aw, pw, ntiles, epoch, S);
+        return;
+    }
+    const u64 tile = kRoles ? blockIdx.x - P - 1 : blockIdx.x;
+    if (tile >= ntiles) return;
+    copier<NF, NV, MIX, MODE, DIAG, STG, EARLY, AHEAD, NOP, SPEC && MODE == 0 && SPECX != 1>(p, flags, epoch, tile, forced, S);
+}
+
+// ---------------------------------------------------------------- the gate
+// Runs after every speculative launch (same stream).  When no copier found a speculative length
+// wrong -- every batch the generator's layout produced -- each workgroup reads one word and exits,
+// and workgroup 0 moves the launch's error bits into p.err.  Otherwise the batch is decoded again
+// exactly: a persistent grid takes the tiles in order, each by a forced look-back copier (no
+// parsers, no scanner, no waits) under tag epoch + 1, rewriting every output of the first launch.
+// Progress never depends on which workgroups are resident.
+template <int NF, int NV, bool MIX>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))) void decode_gate_kernel(
+    DecodeParams p, u64* flags, u32 epoch) {
+    __shared__ Lds<NV, kStage> S;
+    const u64 ntiles = num_tiles(p.n);
+    u64* const ctrl = ctrl_words(flags, NV, ntiles);
+    const bool redo = tagged((u64)uniform_i64((i64)load_word(&ctrl[kCtrlMismatch])), epoch);
+    if (!redo && blockIdx.x == 0 && threadIdx.x == 0) {
+        const u64 e = load_word(&ctrl[kCtrlSpecErr]);
+        if (tagged(e, epoch)) atomicOr(p.err, (unsigned)(e & kValMask));
+    }
+    if (!redo) return;
+    for (u64 tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        copier<NF, NV, MIX, 0, 0, kStage, false, 0, 0, false>(p, flags, epoch + 1, tile, true, S);
+        lds_barrier();  // the next tile restages S
+    }
 }
 
 // ---------------------------------------------------------------- the gather copier
@@ -868,7 +994,7 @@ hipError_t launch_gather_layout(const DecodeParams& p, u64* flags, u32 epoch, hi
 }
 
 template <int NF, int NV, bool MIX, int MODE, int DIAG, int SK = 4, int PR = 2, int STG = kStage, bool EARLY = false,
-          int PACE = 0, bool XCDP = false, int AHEAD = 0, int NOP = 0>
+          int PACE = 0, bool XCDP = false, int AHEAD = 0, int NOP = 0, bool SPEC = false, int SPECX = 0>
 hipError_t launch(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stream, int pnum = 1, int pden = 1) {
     if (DIAG && !p.dbg) return hipErrorInvalidValue;  // timestamps need SYMHIP_DEBUG_PTR (tuning builds)
     static int cus[16] = {0};
@@ -885,7 +1011,20 @@ hipError_t launch(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stre
     DecodeParams q = p;
     q.pipe_parsers = (unsigned)P;
     const u64 grid = kRoles ? P + 1 + nt : nt;
-    hipLaunchKernelGGL((decode_pipe_kernel<NF, NV, MIX, MODE, DIAG, SK, PR, STG, EARLY, PACE, XCDP, AHEAD, NOP>), dim3((unsigned)grid),
+    // speculative parsers: only kv layouts (no int32 fields) under the pipeline with its parsers
+    constexpr bool kSpec = SPEC && NF == 0 && MODE == 0;
+    if constexpr (kSpec) {
+        if (p.impl != kImplLookback && P > 0) {
+            hipLaunchKernelGGL((decode_pipe_kernel<NF, NV, MIX, MODE, DIAG, SK, PR, STG, EARLY, PACE, XCDP, AHEAD, NOP, true, SPECX>),
+                               dim3((unsigned)grid), dim3(kThreads), 0, stream, q, flags, epoch);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+            if (SPECX == 1 || SPECX == 2) return hipSuccess;  // timing variants: no gate (WRONG on misfits)
+            const u64 g = min(nt, (u64)ncu * (SPECX == 3 ? 1 : 4));  // one round of resident workgroups
+            hipLaunchKernelGGL((decode_gate_kernel<NF, NV, MIX>), dim3((unsigned)g), dim3(kThreads), 0, stream, q, flags, epoch);
+            return hipGetLastError();
+        }
+    }
+    hipLaunchKernelGGL((decode_pipe_kernel<NF, NV, MIX, MODE, DIAG, SK, PR, STG, EARLY, PACE, XCDP, AHEAD, NOP, false>), dim3((unsigned)grid),
                        dim3(kThreads), 0, stream, q, flags, epoch);
     return hipGetLastError();
 }
@@ -895,11 +1034,11 @@ constexpr int kParsersNum = 3;   // parser workgroups = #CUs * 3/4
 constexpr int kParsersDen = 4;
 
 template <int MODE, int DIAG, int SK = kScanPer, int PR = 2, int STG = kStage, bool EARLY = false, int PACE = 0,
-          bool XCDP = false, int AHEAD = 0, int NOP = 0>
+          bool XCDP = false, int AHEAD = 0, int NOP = 0, bool SPEC = false, int SPECX = 0>
 hipError_t launch_layout(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stream, int pnum = kParsersNum,
                          int pden = kParsersDen) {
 #define SYMHIP_PIPE_LAUNCH(NF, NV, MIX) \
-    launch<NF, NV, MIX, MODE, DIAG, SK, PR, STG, EARLY, PACE, XCDP, AHEAD, NOP>(p, flags, epoch, stream, pnum, pden)
+    launch<NF, NV, MIX, MODE, DIAG, SK, PR, STG, EARLY, PACE, XCDP, AHEAD, NOP, SPEC, SPECX>(p, flags, epoch, stream, pnum, pden)
     if (p.type)  // mixed kv batch: GetRequest / SetRequest per record
         return p.lay.nfixed == 0 && p.lay.nvar == 2 ? SYMHIP_PIPE_LAUNCH(0, 2, true) : hipErrorInvalidValue;
     if (p.lay.nfixed == 0 && p.lay.nvar == 1) return SYMHIP_PIPE_LAUNCH(0, 1, false);
@@ -919,8 +1058,9 @@ hipError_t launch_layout(const DecodeParams& p, u64* flags, u32 epoch, hipStream
 
 size_t decode_pipe_flag_bytes(int nvar, uint64_t n) {
     // aggregate + prefix word per column and tile, then 256 bytes: the scanner's store sink
-    // (pipe_words.hpp); the start doubles as the kernels' filler load address
-    return ((size_t)nvar * 2 * pipe::num_tiles(n) * sizeof(u64) + 256 + 255) & ~(size_t)255;
+    // (pipe_words.hpp), then 256 bytes of control words (pipe::ctrl_words); the start doubles as the
+    // kernels' filler load address
+    return ((size_t)nvar * 2 * pipe::num_tiles(n) * sizeof(u64) + 512 + 255) & ~(size_t)255;
 }
 
 // The pipeline: 512-tile scanner steps, parsers on 3/4 of the CUs (tools/kbench.py sweep).
@@ -978,6 +1118,13 @@ hipError_t launch_decode_pipe(const DecodeParams& p, void* flags, unsigned epoch
         case 700: return pipe::launch_layout<0, 0, 2, 2, pipe::kStage, false, 0, false, 0, 1>(p, fl, epoch, stream);
         case 701: return pipe::launch_layout<1, 0, 2, 2, pipe::kStage, false, 0, false, 0, 1>(p, fl, epoch, stream);
         case 702: return pipe::launch_layout<2, 0, 2, 2, pipe::kStage, false, 0, false, 0, 1>(p, fl, epoch, stream);
+        // round 3: exact parsers (no speculation, no gate): the round-2 default
+        case 710: return pipe::launch_layout<0, 0>(p, fl, epoch, stream);
+        // speculation without the copiers' check and the gate / with the check, no gate / gate on one
+        // workgroup per CU (711 and 712 are WRONG on batches the speculation misses)
+        case 711: return pipe::launch_layout<0, 0, pipe::kScanPer, 2, pipe::kStage, false, 0, false, 0, 0, true, 1>(p, fl, epoch, stream);
+        case 712: return pipe::launch_layout<0, 0, pipe::kScanPer, 2, pipe::kStage, false, 0, false, 0, 0, true, 2>(p, fl, epoch, stream);
+        case 713: return pipe::launch_layout<0, 0, pipe::kScanPer, 2, pipe::kStage, false, 0, false, 0, 0, true, 3>(p, fl, epoch, stream);
         // the gather copier (no LDS stage, output-stationary copy); 601: its timing mode (WRONG output)
         case 600: return pipe::launch_gather_layout<0>(p, fl, epoch, stream);
         case 601: return pipe::launch_gather_layout<1>(p, fl, epoch, stream);
@@ -994,7 +1141,7 @@ hipError_t launch_decode_pipe(const DecodeParams& p, void* flags, unsigned epoch
         default: break;
     }
 #endif
-    return pipe::launch_layout<0, 0>(p, fl, epoch, stream);
+    return pipe::launch_layout<0, 0, pipe::kScanPer, 2, pipe::kStage, false, 0, false, 0, 0, true>(p, fl, epoch, stream);
 }
 
 }  // namespace symhip
