@@ -1019,7 +1019,9 @@ hipError_t launch(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stre
                                dim3((unsigned)grid), dim3(kThreads), 0, stream, q, flags, epoch);
             if ((e = hipGetLastError()) != hipSuccess) return e;
             if (SPECX == 1 || SPECX == 2) return hipSuccess;  // timing variants: no gate (WRONG on misfits)
-            const u64 g = min(nt, (u64)ncu * (SPECX == 3 ? 1 : 4));  // one round of resident workgroups
+            // one workgroup per CU: the gate's cost is mostly the launch after the first kernel (a
+            // 4-per-CU grid measured ~1.3 us slower); a re-decode runs 64 tiles per workgroup
+            const u64 g = min(nt, (u64)ncu * (SPECX == 3 ? 4 : 1));
             hipLaunchKernelGGL((decode_gate_kernel<NF, NV, MIX>), dim3((unsigned)g), dim3(kThreads), 0, stream, q, flags, epoch);
             return hipGetLastError();
         }
@@ -1120,8 +1122,8 @@ hipError_t launch_decode_pipe(const DecodeParams& p, void* flags, unsigned epoch
         case 702: return pipe::launch_layout<2, 0, 2, 2, pipe::kStage, false, 0, false, 0, 1>(p, fl, epoch, stream);
         // round 3: exact parsers (no speculation, no gate): the round-2 default
         case 710: return pipe::launch_layout<0, 0>(p, fl, epoch, stream);
-        // speculation without the copiers' check and the gate / with the check, no gate / gate on one
-        // workgroup per CU (711 and 712 are WRONG on batches the speculation misses)
+        // speculation without the copiers' check and the gate / with the check, no gate / gate on four
+        // workgroups per CU (711 and 712 are WRONG on batches the speculation misses)
         case 711: return pipe::launch_layout<0, 0, pipe::kScanPer, 2, pipe::kStage, false, 0, false, 0, 0, true, 1>(p, fl, epoch, stream);
         case 712: return pipe::launch_layout<0, 0, pipe::kScanPer, 2, pipe::kStage, false, 0, false, 0, 0, true, 2>(p, fl, epoch, stream);
         case 713: return pipe::launch_layout<0, 0, pipe::kScanPer, 2, pipe::kStage, false, 0, false, 0, 0, true, 3>(p, fl, epoch, stream);
