@@ -15,7 +15,9 @@
 //    H^(e-b) for its 64-block window [s, e) with Shoup 4-bit tables of H^1..H^64 in LDS, a wave
 //    XOR-reduction sums the window, and windows chain by Horner (Y := Y * H^len xor window).
 //    Decrypt authenticates both segments (and the private version byte) before any plaintext is
-//    written; a record that fails gets zeros.
+//    written; a record that fails gets zeros.  A record within one GHASH window decrypts in the
+//    hashing pass (plaintext held in registers until the tags check); longer ones take a second
+//    pass.
 #include <cstring>
 
 #include "../../include/symphony_hip.h"
@@ -294,6 +296,13 @@ __device__ void seal_or_open(const Args& a, const Tables& T, const u32* ts, u64 
     const u32 nsp = nbp + 1, nsv = priv ? nbv + 1 : 0, ns = nsp + nsv;  // GHASH slots
     u32x4 y_pub = {0, 0, 0, 0}, y_priv = {0, 0, 0, 0};
     u32 version = 1;  // DEC: first private plaintext byte
+    // DEC of a record whose GHASH slots fit one window (config 2's 350-byte records: 24 slots): pass 1
+    // also runs CTR and keeps the lane's plaintext block in registers until the tags are checked,
+    // so AES overlaps GHASH as in ENC and no second pass re-reads the ciphertext
+    const bool one = !ENC && ns <= (u32)W;
+    u32x4 held = {0, 0, 0, 0};
+    int held_m = 0;
+    uint8_t* held_dst = nullptr;
     // ---- pass 1: ENC encrypts, writes and hashes; DEC hashes the ciphertext (+ private byte 0)
     for (u32 w0 = 0; w0 < ns; w0 += W) {
         const u32 g = w0 + sl;
@@ -306,7 +315,7 @@ __device__ void seal_or_open(const Args& a, const Tables& T, const u32* ts, u64 
         const u32x4 x = load_partial((is_priv ? src_priv : src_pub) + 16 * (u64)i, m);
         const bool ver = !ENC && is_priv && is_data && i == 0;
         u32x4 ks = {0, 0, 0, 0};
-        if (is_len || (ENC && is_data) || ver)  // J0 for the tag, J0 + 1 + i for block i
+        if (is_len || ((ENC || one) && is_data) || ver)  // J0 for the tag, J0 + 1 + i for block i
             ks = aes_block(ts, T.rk[is_priv ? 1 : 0],
                            counter_block(is_priv ? nonce_priv : nonce_pub, is_len ? 1u : i + 2));
         u32x4 c = x;
@@ -315,6 +324,11 @@ __device__ void seal_or_open(const Args& a, const Tables& T, const u32* ts, u64 
             store_bytes((is_priv ? dst_priv : dst_pub) + 16 * (u64)i, c, m);
         }
         if (ver) version = (x.x ^ ks.x) & 0xffu;
+        if (one && is_data) {
+            held = x ^ ks;
+            held_m = m;
+            held_dst = (is_priv ? dst_priv : dst_pub) + 16 * (u64)i;
+        }
         const u64 bits = seg_len * 8;
         const u32x4 X = is_len ? u32x4{0, 0, (u32)(bits >> 32), (u32)bits} : to_be(c);
         const u32 e = min(is_priv ? ns : nsp, w0 + W);
@@ -360,7 +374,8 @@ __device__ void seal_or_open(const Args& a, const Tables& T, const u32* ts, u64 
         for (u64 t = (u64)sl; t < size; t += W) q[t] = 0;
         return;
     }
-    const u32 nb = nbp + nbv;
+    if (one && held_m) store_bytes(held_dst, held, held_m);
+    const u32 nb = one ? 0u : nbp + nbv;
     for (u32 g0 = 0; g0 < nb; g0 += W) {
         const u32 g = g0 + sl;
         if (g >= nb) continue;
