@@ -96,6 +96,10 @@ int sym_ctx_check(sym_ctx* ctx, void* stream);
  *   SYM_DECODE_PIPELINE     (default) one launch: parser, scanner and copier workgroups.  A copier
  *                           whose prefix has not arrived within 1 ms resolves it by a look-back that
  *                           never waits, so progress never depends on which workgroups are resident.
+ *                           For kv schemas the parsers take each record's lengths from the generator's
+ *                           layout and the copiers check them against the exact parse; a second small
+ *                           launch on the same stream (no host sync) merges the error bits, or decodes
+ *                           the batch again exactly when a record did not follow that layout.
  *   SYM_DECODE_THREE_KERNEL parse -> scan -> copy as three stream-ordered launches (no
  *                           inter-workgroup waiting at all).
  *   SYM_DECODE_LOOKBACK     the pipeline with its parsers and scanner idle: every copier takes the
