@@ -696,21 +696,27 @@ int sym_flat_encode(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t
                               d_out_off, stream);
 }
 
-int sym_flat_decode_ex(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const uint8_t* d_in,
-                       const uint64_t* d_rec_off, void* const* d_cols, const uint64_t* caps, uint64_t* const* d_offs,
-                       uint64_t* const* d_items, const uint64_t* item_caps, uint8_t* d_status, uint8_t* d_fail,
-                       void* stream) {
+int sym_flat_decode_ex2(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const uint8_t* d_in,
+                        const uint64_t* d_rec_src, const uint64_t* d_rec_len, const uint64_t* d_lo,
+                        const uint64_t* d_hi, void* const* d_cols, const uint64_t* caps, uint64_t* const* d_offs,
+                        uint64_t* const* d_items, uint64_t* const* d_item_len, const uint64_t* item_caps,
+                        uint8_t* d_status, uint8_t* d_fail, void* stream) {
     if (!ctx) return fail(SYM_ERR_INVALID, "sym_flat_decode: ctx is NULL");
     const bool lists = d_items != nullptr;
     int rc = flat_check("sym_flat_decode", fields, nfields, lists);
     if (rc != SYM_OK) return rc;
-    if (n && (!d_in || !d_rec_off || !d_status || (nfields && (!d_cols || !caps || !d_offs))))
+    if (n && (!d_in || !d_rec_src || !d_status || (nfields && (!d_cols || !caps || !d_offs))))
         return fail(SYM_ERR_INVALID, "sym_flat_decode: NULL argument");
+    if ((d_lo == nullptr) != (d_hi == nullptr)) return fail(SYM_ERR_INVALID, "sym_flat_decode: give both d_lo and d_hi");
+    if (d_rec_len && !d_lo) return fail(SYM_ERR_INVALID, "sym_flat_decode: records in place need d_lo / d_hi");
     for (int k = 0; k < nfields; ++k) {
+        const bool inplace = d_item_len && d_item_len[k];
         if ((n && !d_cols[k] && (flat_scalar(fields[k]) || caps[k])) || (!flat_scalar(fields[k]) && !d_offs[k]))
             return fail(SYM_ERR_INVALID, "sym_flat_decode: field %d has no column", k);
         if (flat_list(fields[k]) && (!item_caps || !d_items[k]))
             return fail(SYM_ERR_INVALID, "sym_flat_decode: list-like field %d needs d_items and item_caps", k);
+        if (inplace && !(fields[k].width & SYM_FIELD_MESSAGE))
+            return fail(SYM_ERR_INVALID, "sym_flat_decode: field %d is not a message field (d_item_len)", k);
     }
     DeviceGuard g(ctx->device);
     if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
@@ -726,9 +732,18 @@ int sym_flat_decode_ex(sym_ctx* ctx, const sym_field* fields, int nfields, uint6
     }
     if ((rc = ensure_scratch(ctx, symhip::flat_ws_bytes(fields, nfields, n, item_caps), "flat decode")) != SYM_OK)
         return rc;
-    hipError_t e = symhip::launch_flat_decode(fields, nfields, n, d_in, d_rec_off, d_cols, caps, d_offs, d_items,
-                                              item_caps, d_status, d_fail, ctx->frag, ctx->err, (hipStream_t)stream);
+    hipError_t e = symhip::launch_flat_decode(fields, nfields, n, d_in, d_rec_src, d_rec_len, d_lo, d_hi, d_cols, caps,
+                                              d_offs, d_items, d_item_len, item_caps, d_status, d_fail, ctx->frag,
+                                              ctx->err, (hipStream_t)stream);
     return e == hipSuccess ? SYM_OK : hip_fail(e, "flat decode launch");
+}
+
+int sym_flat_decode_ex(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const uint8_t* d_in,
+                       const uint64_t* d_rec_off, void* const* d_cols, const uint64_t* caps, uint64_t* const* d_offs,
+                       uint64_t* const* d_items, const uint64_t* item_caps, uint8_t* d_status, uint8_t* d_fail,
+                       void* stream) {
+    return sym_flat_decode_ex2(ctx, fields, nfields, n, d_in, d_rec_off, nullptr, nullptr, nullptr, d_cols, caps, d_offs,
+                               d_items, nullptr, item_caps, d_status, d_fail, stream);
 }
 
 int sym_flat_decode(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const uint8_t* d_in,

@@ -185,10 +185,14 @@ size_t flat_ws_bytes(const sym_field* f, int nf, uint64_t n, const uint64_t* ite
 hipError_t launch_flat_encode(const sym_field* f, int nf, uint64_t n, const void* const* cols,
                               const uint64_t* const* offs, const uint64_t* const* items, uint32_t sid, uint32_t mid,
                               uint8_t* out, uint64_t* out_off, unsigned* err, hipStream_t stream);
+// rec_len non-null: record i is in[rec_off[i], + rec_len[i]) (records in place); lo / hi: device
+// values bounding in's readable extent (null: rec_off[0], rec_off[n]); item_len[k] non-null for a
+// message field k: items[k] / item_len[k] receive each item's (offset into in, length), no bytes
 hipError_t launch_flat_decode(const sym_field* f, int nf, uint64_t n, const uint8_t* in, const uint64_t* rec_off,
-                              void* const* cols, const uint64_t* caps, uint64_t* const* offs, uint64_t* const* items,
-                              const uint64_t* item_caps, uint8_t* status, uint8_t* fail, void* ws, unsigned* err,
-                              hipStream_t stream);
+                              const uint64_t* rec_len, const uint64_t* lo, const uint64_t* hi, void* const* cols,
+                              const uint64_t* caps, uint64_t* const* offs, uint64_t* const* items,
+                              uint64_t* const* item_len, const uint64_t* item_caps, uint8_t* status, uint8_t* fail,
+                              void* ws, unsigned* err, hipStream_t stream);
 hipError_t launch_list_sizes(int nl, uint64_t n, const uint64_t* const* recs, const uint64_t* const* items,
                              const uint64_t* caps, uint64_t* out, hipStream_t stream);
 hipError_t launch_nested_status(uint64_t n, uint32_t pos, const uint64_t* rec_items, const uint8_t* item_status,

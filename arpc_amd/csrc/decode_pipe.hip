@@ -87,19 +87,6 @@ struct alignas(16) Lds {
 };
 
 
-// u32 at byte q (q <= 4*NW-4) of a register window w[0..NW): bit-select the dword pair (a dynamic
-// register index would go to scratch) and align.
-template <int NW>
-__device__ __forceinline__ u32 win_u32(const u32 (&w)[NW], u32 q) {
-    const u32 d = q >> 2;
-    u32 lo = w[0], hi = w[1];
-#pragma unroll
-    for (int k = 1; k < NW; ++k) {
-        lo = d == (u32)k ? w[k] : lo;
-        hi = d == (u32)k ? (k < NW - 1 ? w[k + 1] : 0u) : hi;
-    }
-    return alignbyte(hi, lo, q & 3);
-}
 
 // ---------------------------------------------------------------- parser role
 // Step k covers tiles [k*4PR, (k+1)*4PR): wave (b, w) takes R consecutive tiles, lane = record; every

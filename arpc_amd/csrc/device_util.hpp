@@ -26,6 +26,20 @@ typedef __attribute__((address_space(1))) uint8_t g_u8;
 
 __device__ __forceinline__ u32 alignbyte(u32 hi, u32 lo, u32 sh) { return __builtin_amdgcn_alignbyte(hi, lo, sh); }
 
+// u32 at byte q (q <= 4*NW-4) of a register window w[0..NW): bit-select the dword pair (a dynamic
+// register index would go to scratch) and align.
+template <int NW>
+__device__ __forceinline__ u32 win_u32(const u32 (&w)[NW], u32 q) {
+    const u32 d = q >> 2;
+    u32 lo = w[0], hi = w[1];
+#pragma unroll
+    for (int k = 1; k < NW; ++k) {
+        lo = d == (u32)k ? w[k] : lo;
+        hi = d == (u32)k ? (k < NW - 1 ? w[k + 1] : 0u) : hi;
+    }
+    return alignbyte(hi, lo, q & 3);
+}
+
 // Mask selecting chunk bytes [lo, hi) inside dword k (lo, hi in [-inf, +inf], clamped).
 __device__ __forceinline__ u32 dword_mask(int lo, int hi, int k) {
     const int a = min(max(lo - 4 * k, 0), 4);

@@ -220,17 +220,27 @@ def _encode(codec: Codec, schema: FlatSchema, cols: list, service_id: int, metho
 
 
 def decode(codec: Codec, schema: FlatSchema, data: torch.Tensor, rec_off: torch.Tensor, stream=None,
-           span: int | None = None, with_fail: bool = False):
+           span: int | None = None, with_fail: bool = False, rec_len: torch.Tensor | None = None,
+           extent: tuple | None = None):
     """UnmarshalSymphony into fresh structs -> (cols, status) (with_fail: (cols, status, fail)); cols
     per the module docstring, message fields decoded recursively with their items' statuses folded
     into `status` (SYM_STATUS_NESTED).  span = rec_off[n] - rec_off[0] when the caller knows it
-    (skips a device sync)."""
+    (skips a device sync).  Inner levels are decoded in place (sym_flat_decode_ex2): a message
+    field's items stay where they are in `data` -- rec_off holds their offsets, rec_len their
+    lengths, extent the device pointers bounding data's readable bytes, span an upper bound of their
+    bytes -- so no level copies its inner messages out."""
     _check_col(data, torch.uint8, "data", codec.device)
     _check_col(rec_off, torch.int64, "rec_off", codec.device)
-    n = rec_off.numel() - 1
+    if rec_len is not None:
+        _check_col(rec_len, torch.int64, "rec_len", codec.device)
+        if extent is None or span is None:
+            raise ValueError("records in place need extent and span")
+    n = rec_off.numel() - 1 if rec_len is None else rec_len.numel()
     if span is None:
         span = int(rec_off[-1].item() - rec_off[0].item()) if n else 0
-    cols, ptrs, caps, offs, items, icaps = [], [], [], [], [], []
+    if extent is None and n:  # data's readable extent: rec_off[0], rec_off[n] (device values)
+        extent = (_dptr(rec_off), _dptr(rec_off) + 8 * n)
+    cols, ptrs, caps, offs, items, ilens, icaps = [], [], [], [], [], [], []
     for f in schema.fields:
         if f.width:
             c = torch.empty(max(1, n), dtype=DTYPE[f.kind], device=codec.device)
@@ -239,17 +249,23 @@ def decode(codec: Codec, schema: FlatSchema, data: torch.Tensor, rec_off: torch.
             caps.append(0)
             offs.append(0)
             items.append(0)
+            ilens.append(0)
             icaps.append(0)
         elif f.list_like:
             icap = n if (f.kind == "message" and not f.repeated) else span // 4 + 1  # items hold a [u32 len] each
-            b = torch.empty(max(1, span), dtype=torch.uint8, device=codec.device)
+            msg = f.kind == "message"  # items left in place: (offset into data, length)
+            b = torch.empty(1 if msg else max(1, span), dtype=torch.uint8, device=codec.device)
             io = torch.empty(icap + 1, dtype=torch.int64, device=codec.device)
+            il = torch.empty(max(1, icap), dtype=torch.int64, device=codec.device) if msg else None
             rec = torch.empty(n + 1, dtype=torch.int64, device=codec.device)
-            cols.append(ListColumn(b, io, rec))
+            lc = ListColumn(b, io, rec)
+            lc.item_len = il
+            cols.append(lc)
             ptrs.append(_dptr(b))
-            caps.append(span)
+            caps.append(0 if msg else span)
             offs.append(_dptr(rec))
             items.append(_dptr(io))
+            ilens.append(_dptr(il) if msg else 0)
             icaps.append(icap)
         else:
             b = torch.empty(max(1, span), dtype=torch.uint8, device=codec.device)
@@ -259,17 +275,21 @@ def decode(codec: Codec, schema: FlatSchema, data: torch.Tensor, rec_off: torch.
             caps.append(span)
             offs.append(_dptr(o))
             items.append(0)
+            ilens.append(0)
             icaps.append(0)
     st = torch.empty(max(1, n), dtype=torch.uint8, device=codec.device)
     fail = torch.empty(max(1, n), dtype=torch.uint8, device=codec.device)
     cf = schema.c_fields()
     lists = schema.has_lists
     hs = _stream_handle(codec.device, stream)
-    _native.check(codec._lib.sym_flat_decode_ex(codec._ctx, cf, len(schema.fields), n, _dptr(data) or 1,
-                                               _dptr(rec_off), _native.ptr_array(ptrs), _native.u64_array(caps),
-                                               _native.ptr_array(offs), _native.ptr_array(items) if lists else None,
-                                               _native.u64_array(icaps) if lists else None, _dptr(st), _dptr(fail),
-                                               hs), "sym_flat_decode_ex")
+    lo, hi = extent if (extent is not None and (rec_len is not None)) else (0, 0)
+    _native.check(codec._lib.sym_flat_decode_ex2(codec._ctx, cf, len(schema.fields), n, _dptr(data) or 1,
+                                                _dptr(rec_off), _dptr(rec_len) if rec_len is not None else 0, lo, hi,
+                                                _native.ptr_array(ptrs), _native.u64_array(caps),
+                                                _native.ptr_array(offs), _native.ptr_array(items) if lists else None,
+                                                _native.ptr_array(ilens) if lists else None,
+                                                _native.u64_array(icaps) if lists else None, _dptr(st), _dptr(fail),
+                                                hs), "sym_flat_decode_ex2")
     # every list field's item count and item bytes in ONE read-back per level
     lk = [k for k, f in enumerate(schema.fields) if f.list_like]
     sizes = {}
@@ -287,16 +307,18 @@ def decode(codec: Codec, schema: FlatSchema, data: torch.Tensor, rec_off: torch.
             continue
         lc = cols[k]
         m, nb = sizes.get(k, (0, 0))
-        lc.item_off = lc.item_off[:m + 1]
-        lc.bytes = lc.bytes[:nb if m else 0]
         if f.kind == "message":
-            # the items are the inner records (item_off[0] == 0): decode them, fold their statuses in
-            inner_cols, inner_st = decode(codec, f.message, lc.bytes, lc.item_off, stream=stream, span=nb if m else 0)
+            # the items are the inner records, in place in `data`: decode them, fold their statuses in
+            inner_cols, inner_st = decode(codec, f.message, data, lc.item_off[:m], stream=stream, span=span,
+                                          rec_len=lc.item_len[:m], extent=extent)
             if n:
                 _native.check(codec._lib.sym_flat_nested_status(codec._ctx, cf, len(schema.fields), k, n,
                                                                  _dptr(lc.rec), _dptr(inner_st) or 1, _dptr(st),
                                                                  _dptr(fail), hs), "sym_flat_nested_status")
             cols[k] = MessageColumn(inner_cols, lc.rec, inner_st, m)
+            continue
+        lc.item_off = lc.item_off[:m + 1]
+        lc.bytes = lc.bytes[:nb if m else 0]
     out = [c[:n] if isinstance(c, torch.Tensor) else c for c in cols]
     return (out, st[:n], fail[:n]) if with_fail else (out, st[:n])
 

@@ -480,7 +480,7 @@ def boutique_leg(codec: Codec, dev, reps: int, n: int = 1 << 18) -> dict:
         return float(np.median(ts)) * 1e3
 
     enc_ms = timed(lambda: flat.encode(codec, sch, cols))
-    dec_ms = timed(lambda: flat.decode(codec, sch, data, off))
+    dec_ms = timed(lambda: flat.decode(codec, sch, data, off, span=data.numel()))
     sb = int(off[-1].item())
     msgs = 4 * n + 3 * inner  # PlaceOrderResponse, OrderResult, Money, Address; per item OrderItem, CartItem, Money
     return {"schema": sch.name, "records": n, "order_items": inner, "messages_per_batch": msgs, "stream_bytes": sb,

@@ -463,6 +463,14 @@ uint64_t sym_flat_encoded_size(const sym_field* fields, int nfields, uint64_t n,
  *                    there); d_fail is updated, so fields can be folded in in any order.  Field
  *                    values of a record with a non-OK status are unspecified beyond the fields
  *                    before the failing one (Go callers discard the struct on error).
+ *   sym_flat_decode_ex2  sym_flat_decode_ex over records in place and with message fields left in
+ *                    place, so a tree decodes without copying inner messages out: record i is
+ *                    d_in[d_rec_src[i], d_rec_src[i] + d_rec_len[i]) (d_rec_len NULL: contiguous, d_rec_src
+ *                    is d_rec_off), and d_in's readable extent is [*d_lo, *d_hi) (device values; both NULL:
+ *                    d_rec_src[0], d_rec_src[n]; required with d_rec_len).  For a message field k with
+ *                    d_item_len[k] non-NULL no item bytes are written: d_items[k][j] receives item j's
+ *                    offset into d_in and d_item_len[k][j] its length, and the inner level is decoded
+ *                    from there (d_rec_src = d_items[k], d_rec_len = d_item_len[k], the same d_in).
  *   sym_flat_list_sizes  after sym_flat_decode_ex, for `nl` list-like fields (record item ranges
  *                    d_recs[i], n + 1 entries; item offsets d_items[i], item_caps[i] + 1): item count
  *                    m_i = d_recs[i][n] - d_recs[i][0] (clamped to item_caps[i]) and item bytes
@@ -477,6 +485,11 @@ int sym_flat_decode_ex(sym_ctx* ctx, const sym_field* fields, int nfields, uint6
                        const uint64_t* d_rec_off, void* const* d_cols, const uint64_t* caps, uint64_t* const* d_offs,
                        uint64_t* const* d_items, const uint64_t* item_caps, uint8_t* d_status, uint8_t* d_fail,
                        void* stream);
+int sym_flat_decode_ex2(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const uint8_t* d_in,
+                        const uint64_t* d_rec_src, const uint64_t* d_rec_len, const uint64_t* d_lo,
+                        const uint64_t* d_hi, void* const* d_cols, const uint64_t* caps, uint64_t* const* d_offs,
+                        uint64_t* const* d_items, uint64_t* const* d_item_len, const uint64_t* item_caps,
+                        uint8_t* d_status, uint8_t* d_fail, void* stream);
 int sym_flat_nested_status(sym_ctx* ctx, const sym_field* fields, int nfields, int field, uint64_t n,
                            const uint64_t* d_rec_items, const uint8_t* d_item_status, uint8_t* d_status,
                            uint8_t* d_fail, void* stream);

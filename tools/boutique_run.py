@@ -38,7 +38,7 @@ def main():
         d2, o2 = flat.encode(codec, sch, cols)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        flat.decode(codec, sch, data, off)
+        flat.decode(codec, sch, data, off, span=data.numel())
         torch.cuda.synchronize()
         t2 = time.perf_counter()
         te.append(t1 - t0)
