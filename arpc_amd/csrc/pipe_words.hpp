@@ -15,8 +15,10 @@ constexpr int kEpochShift = 44;
 constexpr u64 kStAgg = 1ull << 42;
 constexpr u64 kStPre = 2ull << 42;
 constexpr u64 kValMask = (1ull << 42) - 1;
-// Bounded waits, in wall time (s_memrealtime runs at 100 MHz): a wait that outlives this reports
-// kErrTimeout (SYM_ERR_DEVICE from sym_ctx_check) and gives up, so the grid always drains.
+// Bounded waits, in wall time (s_memrealtime runs at 100 MHz).  No wait is needed for progress: a
+// scanner idle for kWaitTicks exits (its consumers look back instead), and a consumer whose word has
+// not come after kFallbackTicks resolves it itself, so the grid always drains with correct results
+// (kErrTimeout is therefore never set).
 constexpr u64 kWaitTicks = 25000000;  // 250 ms: the scanner gives up (copiers fall back) after this idle time
 constexpr u64 kFallbackTicks = 100000; // 1 ms: a copier waits this long for its prefix before looking back
 __device__ __forceinline__ u64 now_ticks() { return __builtin_amdgcn_s_memrealtime(); }
