@@ -1114,6 +1114,16 @@ hipError_t launch_decode_pipe(const DecodeParams& p, void* flags, unsigned epoch
         case 711: return pipe::launch_layout<0, 0, pipe::kScanPer, 2, pipe::kStage, false, 0, false, 0, 0, true, 1>(p, fl, epoch, stream);
         case 712: return pipe::launch_layout<0, 0, pipe::kScanPer, 2, pipe::kStage, false, 0, false, 0, 0, true, 2>(p, fl, epoch, stream);
         case 713: return pipe::launch_layout<0, 0, pipe::kScanPer, 2, pipe::kStage, false, 0, false, 0, 0, true, 3>(p, fl, epoch, stream);
+        // round 3: the speculative default with an early prefix load and / or a 20992-byte stage
+        case 720: return pipe::launch_layout<0, 0, pipe::kScanPer, 2, pipe::kStage, true, 0, false, 0, 0, true>(p, fl, epoch, stream);
+        case 721: return pipe::launch_layout<0, 0, pipe::kScanPer, 2, 20992, true, 0, false, 0, 0, true>(p, fl, epoch, stream);
+        case 722: return pipe::launch_layout<0, 0, pipe::kScanPer, 2, 20992, false, 0, false, 0, 0, true>(p, fl, epoch, stream);
+        case 723: return pipe::launch_layout<0, 0, pipe::kScanPer, 2, pipe::kStage, false, 0, false, 0, 0, true>(p, fl, epoch, stream, 1, 2);
+        case 724: return pipe::launch_layout<0, 0, pipe::kScanPer, 2, pipe::kStage, false, 0, false, 0, 0, true>(p, fl, epoch, stream, 1, 1);
+        case 725: return pipe::launch_layout<0, 0, pipe::kScanPer, 2, pipe::kStage, false, 0, false, 0, 0, true>(p, fl, epoch, stream, 1, 4);
+        case 726: return pipe::launch_layout<0, 0, pipe::kScanPer, 2, pipe::kStage, false, 0, false, 0, 0, true>(p, fl, epoch, stream, 3, 8);
+        case 727: return pipe::launch_layout<0, 0, pipe::kScanPer, 2, pipe::kStage, false, 0, false, 0, 0, true>(p, fl, epoch, stream, 5, 8);
+        case 728: return pipe::launch_layout<0, 0, pipe::kScanPer, 2, pipe::kStage, false, 0, false, 0, 0, true>(p, fl, epoch, stream, 1, 8);
         // the gather copier (no LDS stage, output-stationary copy); 601: its timing mode (WRONG output)
         case 600: return pipe::launch_gather_layout<0>(p, fl, epoch, stream);
         case 601: return pipe::launch_gather_layout<1>(p, fl, epoch, stream);
@@ -1130,6 +1140,10 @@ hipError_t launch_decode_pipe(const DecodeParams& p, void* flags, unsigned epoch
         default: break;
     }
 #endif
+    // speculative parsers are lighter: half the CUs' worth of them keeps ahead of the copiers (sweep of
+    // 1/8 .. 3/4 with configs 2, 3 and the mixed batch); exact parsers (int32 fields) keep 3/4
+    if (p.lay.nfixed == 0)
+        return pipe::launch_layout<0, 0, pipe::kScanPer, 2, pipe::kStage, false, 0, false, 0, 0, true>(p, fl, epoch, stream, 1, 2);
     return pipe::launch_layout<0, 0, pipe::kScanPer, 2, pipe::kStage, false, 0, false, 0, 0, true>(p, fl, epoch, stream);
 }
 
