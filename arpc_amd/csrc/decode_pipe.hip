@@ -285,6 +285,7 @@ __device__ void parser(const DecodeParams& p, u64* aw, u64* pw, u64 ntiles, u32 
 
 // ---------------------------------------------------------------- scanner role: pipe_words.hpp scanner()
 constexpr int kScanPerG = 2;  // the gather copier's scanner: tiles per thread per step
+constexpr int kScanPer = 2;   // the pipeline's scanner: tiles per thread per step (512-tile steps)
 
 // ---------------------------------------------------------------- look-back (the fallback)
 // Field lengths of record r with Go's checks (kv.syn.go:681-745, echo.syn.go:223-231), read straight
@@ -474,7 +475,9 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
             bool mm = false;
 #pragma unroll
             for (int f = 0; f < NV; ++f) mm |= sf[f] != flen[f];
-            if (__ballot(mm) && lane == 0) store_word(&ctrl[kCtrlMismatch], make_word(epoch, kStAgg, 1));
+            // (tag once: when every record misses, 16k copiers storing to one word contend)
+            if (__ballot(mm) && lane == 0 && !tagged(load_word(&ctrl[kCtrlMismatch]), epoch))
+                store_word(&ctrl[kCtrlMismatch], make_word(epoch, kStAgg, 1));
         }
         // tile scan of the field lengths (each < 2^32)
         u64 agg[NV], excl[NV];
@@ -668,9 +671,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
 // Runs after every speculative launch (same stream).  When no copier found a speculative length
 // wrong -- every batch the generator's layout produced -- each workgroup reads one word and exits,
 // and workgroup 0 moves the launch's error bits into p.err.  Otherwise the batch is decoded again
-// exactly: a persistent grid takes the tiles in order, each by a forced look-back copier (no
-// parsers, no scanner, no waits) under tag epoch + 1, rewriting every output of the first launch.
-// Progress never depends on which workgroups are resident.
+// exactly under tag epoch + 1, rewriting every output of the first launch: the pipeline's roles on
+// a persistent grid (exact parsers, the scanner, copiers taking tiles in turn).  Progress never
+// depends on which workgroups are resident.
 template <int NF, int NV, bool MIX>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))) void decode_gate_kernel(
     DecodeParams p, u64* flags, u32 epoch) {
@@ -683,8 +686,23 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
         if (tagged(e, epoch)) atomicOr(p.err, (unsigned)(e & kValMask));
     }
     if (!redo) return;
-    for (u64 tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        copier<NF, NV, MIX, 0, 0, kStage, false, 0, 0, false>(p, flags, epoch + 1, tile, true, S);
+    // the exact pipeline on a persistent grid: a quarter of the workgroups parse every tile exactly,
+    // one scans, the rest copy tiles c, c + C, ... (a copier whose prefix is late looks back, so no
+    // role waits on residency)
+    u64* aw = flags;
+    u64* pw = flags + (size_t)NV * ntiles;
+    const u32 G = gridDim.x, P = G >= 8 ? G / 4 : 0;
+    if (blockIdx.x < P) {
+        parser<NF, NV, MIX, 2, 32>(p, aw, pw, ntiles, epoch + 1, P);
+        return;
+    }
+    if (P && blockIdx.x == P) {
+        scanner<NV, kScanPer>(aw, pw, ntiles, epoch + 1, S);
+        return;
+    }
+    const u32 c0 = P ? P + 1 : 0;
+    for (u64 tile = blockIdx.x - c0; tile < ntiles; tile += G - c0) {
+        copier<NF, NV, MIX, 0, 0, kStage, false, 0, 0, false>(p, flags, epoch + 1, tile, P == 0, S);
         lds_barrier();  // the next tile restages S
     }
 }
@@ -1006,9 +1024,9 @@ hipError_t launch(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stre
                                dim3((unsigned)grid), dim3(kThreads), 0, stream, q, flags, epoch);
             if ((e = hipGetLastError()) != hipSuccess) return e;
             if (SPECX == 1 || SPECX == 2) return hipSuccess;  // timing variants: no gate (WRONG on misfits)
-            // one workgroup per CU: the gate's cost is mostly the launch after the first kernel (a
-            // 4-per-CU grid measured ~1.3 us slower); a re-decode runs 64 tiles per workgroup
-            const u64 g = min(nt, (u64)ncu * (SPECX == 3 ? 4 : 1));
+            // four workgroups per CU (the gate's cost is the launch behind the first kernel, the same
+            // for 1 or 4 per CU); a re-decode is the exact pipeline on them
+            const u64 g = min(nt + 1 + ncu, (u64)ncu * (SPECX == 3 ? 1 : 4));
             hipLaunchKernelGGL((decode_gate_kernel<NF, NV, MIX>), dim3((unsigned)g), dim3(kThreads), 0, stream, q, flags, epoch);
             return hipGetLastError();
         }
@@ -1018,7 +1036,6 @@ hipError_t launch(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stre
     return hipGetLastError();
 }
 
-constexpr int kScanPer = 2;      // scanner tiles per thread per step (512-tile steps)
 constexpr int kParsersNum = 3;   // parser workgroups = #CUs * 3/4
 constexpr int kParsersDen = 4;
 
@@ -1109,8 +1126,8 @@ hipError_t launch_decode_pipe(const DecodeParams& p, void* flags, unsigned epoch
         case 702: return pipe::launch_layout<2, 0, 2, 2, pipe::kStage, false, 0, false, 0, 1>(p, fl, epoch, stream);
         // round 3: exact parsers (no speculation, no gate): the round-2 default
         case 710: return pipe::launch_layout<0, 0>(p, fl, epoch, stream);
-        // speculation without the copiers' check and the gate / with the check, no gate / gate on four
-        // workgroups per CU (711 and 712 are WRONG on batches the speculation misses)
+        // speculation without the copiers' check and the gate / with the check, no gate / gate on one
+        // workgroup per CU (711 and 712 are WRONG on batches the speculation misses)
         case 711: return pipe::launch_layout<0, 0, pipe::kScanPer, 2, pipe::kStage, false, 0, false, 0, 0, true, 1>(p, fl, epoch, stream);
         case 712: return pipe::launch_layout<0, 0, pipe::kScanPer, 2, pipe::kStage, false, 0, false, 0, 0, true, 2>(p, fl, epoch, stream);
         case 713: return pipe::launch_layout<0, 0, pipe::kScanPer, 2, pipe::kStage, false, 0, false, 0, 0, true, 3>(p, fl, epoch, stream);
