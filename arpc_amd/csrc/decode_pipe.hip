@@ -1141,6 +1141,11 @@ hipError_t launch_decode_pipe(const DecodeParams& p, void* flags, unsigned epoch
         case 726: return pipe::launch_layout<0, 0, pipe::kScanPer, 2, pipe::kStage, false, 0, false, 0, 0, true>(p, fl, epoch, stream, 3, 8);
         case 727: return pipe::launch_layout<0, 0, pipe::kScanPer, 2, pipe::kStage, false, 0, false, 0, 0, true>(p, fl, epoch, stream, 5, 8);
         case 728: return pipe::launch_layout<0, 0, pipe::kScanPer, 2, pipe::kStage, false, 0, false, 0, 0, true>(p, fl, epoch, stream, 1, 8);
+        // speculative parsers on half the CUs: scanner tiles per thread 1 / 4, parser tiles per wave step 4 / 1
+        case 730: return pipe::launch_layout<0, 0, 1, 2, pipe::kStage, false, 0, false, 0, 0, true>(p, fl, epoch, stream, 1, 2);
+        case 731: return pipe::launch_layout<0, 0, 4, 2, pipe::kStage, false, 0, false, 0, 0, true>(p, fl, epoch, stream, 1, 2);
+        case 732: return pipe::launch_layout<0, 0, pipe::kScanPer, 4, pipe::kStage, false, 0, false, 0, 0, true>(p, fl, epoch, stream, 1, 2);
+        case 733: return pipe::launch_layout<0, 0, pipe::kScanPer, 1, pipe::kStage, false, 0, false, 0, 0, true>(p, fl, epoch, stream, 1, 2);
         // the gather copier (no LDS stage, output-stationary copy); 601: its timing mode (WRONG output)
         case 600: return pipe::launch_gather_layout<0>(p, fl, epoch, stream);
         case 601: return pipe::launch_gather_layout<1>(p, fl, epoch, stream);
@@ -1157,10 +1162,11 @@ hipError_t launch_decode_pipe(const DecodeParams& p, void* flags, unsigned epoch
         default: break;
     }
 #endif
-    // speculative parsers are lighter: half the CUs' worth of them keeps ahead of the copiers (sweep of
-    // 1/8 .. 3/4 with configs 2, 3 and the mixed batch); exact parsers (int32 fields) keep 3/4
+    // speculative parsers are lighter: half the CUs' worth of them keeps ahead of the copiers, and the
+    // scanner's 256-tile steps publish sooner (sweeps with configs 2, 3 and the mixed batch,
+    // DESIGN.md); exact parsers (int32 fields) keep 3/4 of the CUs and 512-tile steps
     if (p.lay.nfixed == 0)
-        return pipe::launch_layout<0, 0, pipe::kScanPer, 2, pipe::kStage, false, 0, false, 0, 0, true>(p, fl, epoch, stream, 1, 2);
+        return pipe::launch_layout<0, 0, 1, 2, pipe::kStage, false, 0, false, 0, 0, true>(p, fl, epoch, stream, 1, 2);
     return pipe::launch_layout<0, 0, pipe::kScanPer, 2, pipe::kStage, false, 0, false, 0, 0, true>(p, fl, epoch, stream);
 }
 
