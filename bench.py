@@ -197,8 +197,8 @@ def cpu_baseline(kw: dict, seconds: float) -> dict:
 def decode_kernel_name(s) -> str:
     """rocprof's name of the default decode's main launch for schema s: kv layouts (no int32 fields)
     run the speculative parsers (decode_pipe.hip), followed by the small gate launch."""
-    spec = "true" if s.nfixed == 0 else "false"
-    return f"decode_pipe_kernel<{s.nfixed}, {s.nvar}, false, 0, 0, 2, 2, 22528, false, 0, false, 0, 0, {spec}, 0>"
+    spec, sk = ("true", 1) if s.nfixed == 0 else ("false", 2)  # scanner tiles per thread (decode_pipe.hip)
+    return f"decode_pipe_kernel<{s.nfixed}, {s.nvar}, false, 0, 0, {sk}, 2, 22528, false, 0, false, 0, 0, {spec}, 0>"
 
 
 def load_traffic(kernel: str):
