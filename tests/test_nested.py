@@ -331,3 +331,97 @@ def test_gpu_online_boutique(codec, dev):
     codec.check()
     assert (st.cpu().numpy() == 0).all()
     assert from_columns(sch, cols, n) == [full(sch, r) for r in recs]
+
+
+@pytest.mark.gpu
+def test_gpu_in_place_level_matches_packed_items(codec, dev):
+    """sym_flat_decode_ex2 leaves a message field's items in place ((offset, length) into the input);
+    sym_flat_decode_ex's packed form gathers them into an item column.  The inner level decoded from
+    either is the same (boutique OrderResults -> their repeated OrderItems)."""
+    from arpc_amd import _native, datagen, flat
+    from arpc_amd.codec import _dptr
+    outer = flat.OB_ORDER_RESULT
+    n = 700
+    tree = datagen.ob_place_order(n, seed=9)
+    ob, oo = flat.encode(codec, outer, flat.columns_from_tree(outer, tree[1][0][1], dev))
+    codec.check()
+    k = [f.name for f in outer.fields].index("Items")
+    span = ob.numel()
+    icap = span // 4 + 1
+
+    def run(inplace):
+        cols, caps, offs, items, ilens, icaps, t = [], [], [], [], [], [], {}
+        for j, f in enumerate(outer.fields):
+            if f.list_like:
+                msg = inplace and j == k
+                t[j] = dict(b=torch.empty(1 if msg else span, dtype=torch.uint8, device=dev),
+                            io=torch.empty(icap + 1, dtype=torch.int64, device=dev),
+                            il=torch.empty(icap, dtype=torch.int64, device=dev),
+                            rec=torch.empty(n + 1, dtype=torch.int64, device=dev))
+                cols.append(_dptr(t[j]["b"]))
+                caps.append(0 if msg else span)
+                offs.append(_dptr(t[j]["rec"]))
+                items.append(_dptr(t[j]["io"]))
+                ilens.append(_dptr(t[j]["il"]) if msg else 0)
+                icaps.append(icap)
+            else:
+                t[j] = dict(b=torch.empty(span, dtype=torch.uint8, device=dev),
+                            o=torch.empty(n + 1, dtype=torch.int64, device=dev))
+                cols.append(_dptr(t[j]["b"]))
+                caps.append(span)
+                offs.append(_dptr(t[j]["o"]))
+                items.append(0)
+                ilens.append(0)
+                icaps.append(0)
+        st = torch.empty(n, dtype=torch.uint8, device=dev)
+        _native.check(codec._lib.sym_flat_decode_ex2(
+            codec._ctx, outer.c_fields(), len(outer.fields), n, _dptr(ob), _dptr(oo), 0, 0, 0,
+            _native.ptr_array(cols), _native.u64_array(caps), _native.ptr_array(offs), _native.ptr_array(items),
+            _native.ptr_array(ilens), _native.u64_array(icaps), _dptr(st), 0, 0), "sym_flat_decode_ex2")
+        codec.check()
+        assert (st.cpu().numpy() == 0).all()
+        it = t[k]
+        m = int((it["rec"][n] - it["rec"][0]).item())
+        if inplace:
+            icols, ist = flat.decode(codec, outer.fields[k].message, ob, it["io"][:m], span=span,
+                                     rec_len=it["il"][:m], extent=(_dptr(oo), _dptr(oo) + 8 * n))
+        else:
+            nb = int(it["io"][m].item())
+            icols, ist = flat.decode(codec, outer.fields[k].message, it["b"][:nb], it["io"][:m + 1])
+        codec.check()
+        return m, icols, ist
+
+    m1, c1, s1 = run(True)
+    m2, c2, s2 = run(False)
+    assert m1 == m2 > n
+    assert torch.equal(s1, s2) and (s1.cpu().numpy() == 0).all()
+    assert from_columns(outer.fields[k].message, c1, m1) == from_columns(outer.fields[k].message, c2, m2)
+
+
+@pytest.mark.gpu
+def test_gpu_decode_ex2_argument_checks(codec, dev):
+    from arpc_amd import _native, flat
+    from arpc_amd.codec import _dptr
+    sch = flat.OB_MONEY  # no message field
+    data = torch.zeros(64, dtype=torch.uint8, device=dev)
+    off = torch.tensor([0, 20], dtype=torch.int64, device=dev)
+    ln = torch.tensor([20], dtype=torch.int64, device=dev)
+    b = torch.empty(64, dtype=torch.uint8, device=dev)
+    o = torch.empty(2, dtype=torch.int64, device=dev)
+    v = torch.empty(8, dtype=torch.uint8, device=dev)
+    st = torch.empty(1, dtype=torch.uint8, device=dev)
+    cf = sch.c_fields()
+    args = dict(cols=_native.ptr_array([_dptr(b), _dptr(v), _dptr(v)]), caps=_native.u64_array([64, 0, 0]),
+                offs=_native.ptr_array([_dptr(o), 0, 0]))
+    # records in place need the input's extent
+    rc = codec._lib.sym_flat_decode_ex2(codec._ctx, cf, 3, 1, _dptr(data), _dptr(off), _dptr(ln), 0, 0, args["cols"],
+                                        args["caps"], args["offs"], None, None, None, _dptr(st), 0, 0)
+    assert rc == _native.SYM_ERR_INVALID
+    # an in-place item column only for a message field
+    io = torch.empty(2, dtype=torch.int64, device=dev)
+    sch2 = flat.FlatSchema("L", (flat.FlatField("S", "string", repeated=True),))
+    rc = codec._lib.sym_flat_decode_ex2(codec._ctx, sch2.c_fields(), 1, 1, _dptr(data), _dptr(off), 0, 0, 0,
+                                        _native.ptr_array([_dptr(b)]), _native.u64_array([64]),
+                                        _native.ptr_array([_dptr(o)]), _native.ptr_array([_dptr(io)]),
+                                        _native.ptr_array([_dptr(io)]), _native.u64_array([1]), _dptr(st), 0, 0)
+    assert rc == _native.SYM_ERR_INVALID
