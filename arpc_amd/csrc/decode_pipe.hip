@@ -72,15 +72,13 @@ constexpr int kCtrlMismatch = 0;
 constexpr int kCtrlSpecErr = 1;
 __device__ __forceinline__ u64* ctrl_words(u64* flags, int nv, u64 ntiles) { return flags + (size_t)2 * nv * ntiles + 32; }
 
-template <int NV, int STG, int H = 1>
+template <int NV, int STG>
 struct alignas(16) Lds {
     uint8_t stage[STG + 16];
-    u64 src[NV][kRecs * H];      // field payload position (stream offset)
-    int dst[NV][kRecs * H + 1];  // field start in the tile's column range; [cnt..] = aggregate
-    int cs[kRecs * H + 1];       // record's first copy chunk (record-major chunk sequence)
-    int nch0[kRecs * H];         // chunks of the record's first string field
-    u64 hagg[NV];                // H == 2: the second half's aggregate
-    int hbig;                    // H == 2: the second half's lengths reach 2^31
+    u64 src[NV][kRecs];      // field payload position (stream offset)
+    int dst[NV][kRecs + 1];  // field start in the tile's column range; [cnt..] = aggregate
+    int cs[kRecs + 1];       // record's first copy chunk (record-major chunk sequence)
+    int nch0[kRecs];         // chunks of the record's first string field
     i64 pre[NV];             // tile prefix per column
     i64 lim[NV];             // bytes of the tile's column range that fit the output capacity
     int total;               // chunks in the tile (-1: tile skipped, error reported)
@@ -348,9 +346,8 @@ __device__ void lookback(const DecodeParams& p, u64* aw, u64* pw, u64 ntiles, u6
 // bytes and tags ctrl[kCtrlMismatch] on any difference (the gate then decodes the batch again), and
 // a capacity error is tagged in ctrl[kCtrlSpecErr] (it may come from a speculative prefix), merged
 // into p.err by the gate when the speculation held.
-// H: 64-record halves per copier tile (2: 128 records, for batches of short records).
-template <int NF, int NV, bool MIX, int MODE, int DIAG, int STG, bool EARLY, int AHEAD, int NOP, bool SPEC, int H = 1>
-__device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 epoch, u64 tile, bool forced, Lds<NV, STG, H>& S) {
+template <int NF, int NV, bool MIX, int MODE, int DIAG, int STG, bool EARLY, int AHEAD, int NOP, bool SPEC>
+__device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 epoch, u64 tile, bool forced, Lds<NV, STG>& S) {
     constexpr int kLoads = (STG / 16 + kThreads - 1) / kThreads;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const u64 n = p.n, ntiles = num_tiles(n);
@@ -366,9 +363,8 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
             if (tid == 0) p.dbg[tile * 8 + slot] = __builtin_amdgcn_s_memrealtime();
     };
     stamp(0);
-    const u64 t0 = tile * H;  // the copier's first 64-record tile (the words stay per 64 records)
-    const u64 r0 = t0 * kRecs;
-    const int cnt = (int)min((u64)kRecs * H, n - r0);
+    const u64 r0 = tile * kRecs;
+    const int cnt = (int)min((u64)kRecs, n - r0);
     const u64 s0 = p.rec_off[r0], s1 = p.rec_off[r0 + cnt];
     const uintptr_t base = (in + s0) & ~(uintptr_t)15;
     const uintptr_t stop = min((in + s1 + 15) & ~(uintptr_t)15, in_end16);
@@ -376,10 +372,10 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
 
     // ---- 1. stage (and wave 0's record offsets, and with EARLY its prefix words) ----
     u64 start = 0, endv = 0, wv_early = 0;
-    if (wave < H) {
-        start = p.rec_off[r0 + min(kRecs * wave + lane, cnt)];
-        endv = p.rec_off[r0 + min(kRecs * wave + lane + 1, cnt)];
-        if (EARLY && MODE == 0 && wave == 0 && lane < NV) wv_early = load_word(&pw[(size_t)lane * ntiles + t0]);
+    if (wave == 0) {
+        start = p.rec_off[r0 + min(lane, cnt)];
+        endv = p.rec_off[r0 + min(lane + 1, cnt)];
+        if (EARLY && MODE == 0 && lane < NV) wv_early = load_word(&pw[(size_t)lane * ntiles + tile]);
     }
     {
         u32x4 sv[kLoads];
@@ -404,15 +400,8 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
             parse_tiles<NF, NV, MIX, 1, 32>(p, aw, ntiles, epoch, ta);
         }
     }
-    // Waves [0, H) parse one 64-record half each (lane = record); wave 0 then takes the tile's
-    // prefix and combines the halves.  With H == 1 it is one wave's straight-line code.
-    u64 agg[NV], excl[NV];
-    u32 nch[NV], nrec = 0;
-    bool too_large = false, live = false;
-    u64* const ctrl = ctrl_words(flags, NV, ntiles);
-    const int rb = kRecs * wave;  // the wave's half
-    if (wave < H) {
-        live = rb + lane < cnt;
+    if (wave == 0) {
+        const bool live = lane < cnt;
         const u64 L = endv - start;
         const uintptr_t A = in + start;
         auto rd8 = [&](u64 q) -> u32 {
@@ -428,7 +417,7 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
         u64 flen[NV], fpos[NV];
 #pragma unroll
         for (int f = 0; f < NV; ++f) flen[f] = fpos[f] = 0;
-        const int nvr = rec_nvar<NV, MIX>(p, live ? r0 + rb + lane : 0);
+        const int nvr = rec_nvar<NV, MIX>(p, live ? r0 + lane : 0);
         if (NOP && live) {  // timing only: the config-2 SetRequest layout assumed, no LDS reads
             flen[0] = 64;
             fpos[0] = 26;
@@ -436,7 +425,7 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
                 flen[1] = L - 94;
                 fpos[1] = 94;
             }
-            p.status[r0 + rb + lane] = 0;
+            p.status[r0 + lane] = 0;
         } else if (live) {
             if (L < 13) {
                 st = SYM_STATUS_TOO_SHORT;  // "invalid data: too short" (kv.syn.go:681-683)
@@ -474,10 +463,11 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
                     }
                 }
             }
-            p.status[r0 + rb + lane] = (uint8_t)st;
+            p.status[r0 + lane] = (uint8_t)st;
 #pragma unroll
-            for (int f = 0; f < NF; ++f) p.fixed[f][r0 + rb + lane] = fx[f];
+            for (int f = 0; f < NF; ++f) p.fixed[f][r0 + lane] = fx[f];
         }
+        u64* const ctrl = ctrl_words(flags, NV, ntiles);
         if constexpr (SPEC) {  // the parsers' speculative lengths of these records, from the same bytes
             const u32 k0 = live && nvr == 2 && L >= 30 ? rd32(22) : 0u;
             u64 sf[NV];
@@ -489,7 +479,10 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
             if (__ballot(mm) && lane == 0 && !tagged(load_word(&ctrl[kCtrlMismatch]), epoch))
                 store_word(&ctrl[kCtrlMismatch], make_word(epoch, kStAgg, 1));
         }
-        // half-tile scan of the field lengths (each < 2^32)
+        // tile scan of the field lengths (each < 2^32)
+        u64 agg[NV], excl[NV];
+        u32 nch[NV];
+        bool too_large = false;
 #pragma unroll
         for (int f = 0; f < NV; ++f) {
             const u64 inc = wave_incl_scan_u32w_dpp((u32)flen[f]);
@@ -498,33 +491,18 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
             excl[f] = inc - flen[f];
             too_large |= agg[f] >= ((u64)1 << 31);  // positions inside a tile's range are 32-bit
             nch[f] = (u32)((flen[f] + 15) >> 4);
-            S.src[f][rb + lane] = start + fpos[f];
-            S.dst[f][rb + lane] = (int)excl[f];  // lanes >= cnt hold the aggregate
+            S.src[f][lane] = start + fpos[f];
+            S.dst[f][lane] = (int)excl[f];  // lanes >= cnt hold the aggregate
         }
-        nrec = nch[0] + (NV == 2 ? nch[NV - 1] : 0u);
-        S.nch0[rb + lane] = (int)nch[0];
-        // the half's aggregate (a parser may have published the same value)
-        if ((MODE == 0 || MODE == 2 || MODE == 3) && lane < NV && t0 + wave < ntiles)
-            store_word(&aw[(size_t)lane * ntiles + t0 + wave], make_word(epoch, kStAgg, lane == 0 ? agg[0] : agg[NV - 1]));
-        if (H > 1 && wave > 0) {  // handed to wave 0
-            S.cs[rb + lane] = (int)nrec;
-            if (lane < NV) S.hagg[lane] = lane == 0 ? agg[0] : agg[NV - 1];
-            if (lane == 0) S.hbig = too_large;
-        }
-    }
-    if constexpr (H > 1) lds_barrier();
-    if (wave == 0) {
-        u64 aggT[NV];  // the tile's (both halves') aggregate
-#pragma unroll
-        for (int f = 0; f < NV; ++f) aggT[f] = agg[f] + (H > 1 ? S.hagg[f] : 0);
-        if constexpr (H > 1) too_large |= S.hbig != 0 || aggT[0] >= ((u64)1 << 31) || aggT[NV - 1] >= ((u64)1 << 31);
         stamp(2);
         i64 pre[NV];
         if constexpr (MODE == 0) {
             u64 wv = 0;
             bool got = true;
-            if (lane < NV) {  // the tile's prefix (its first half's)
-                u64* a = &pw[(size_t)lane * ntiles + t0];
+            if (lane < NV) {
+                // this tile's aggregate (a parser may have published the same value), then its prefix
+                store_word(&aw[(size_t)lane * ntiles + tile], make_word(epoch, kStAgg, lane == 0 ? agg[0] : agg[NV - 1]));
+                u64* a = &pw[(size_t)lane * ntiles + tile];
                 wv = EARLY && tagged(wv_early, epoch) ? wv_early : load_word(a);
                 if (!forced) {
                     for (const u64 t0 = now_ticks(); !tagged(wv, epoch) && now_ticks() - t0 <= kFallbackTicks;) {
@@ -535,15 +513,17 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
                 got = tagged(wv, epoch);
             }
             if (__ballot(!got)) {  // no prefix from the scanner: resolve it here (never waits)
-                lookback<NF, NV, MIX>(p, aw, pw, ntiles, t0, epoch, pre);
+                lookback<NF, NV, MIX>(p, aw, pw, ntiles, tile, epoch, pre);
 #pragma unroll
                 for (int f = 0; f < NV; ++f)
-                    if (lane == 0) store_word(&pw[(size_t)f * ntiles + t0], make_word(epoch, kStPre, (u64)pre[f]));
+                    if (lane == 0) store_word(&pw[(size_t)f * ntiles + tile], make_word(epoch, kStPre, (u64)pre[f]));
             } else {
                 pre[0] = (i64)((u64)__shfl((long long)wv, 0, 64) & kValMask);
                 if constexpr (NV == 2) pre[1] = (i64)((u64)__shfl((long long)wv, 1, 64) & kValMask);
             }
         } else {  // timing only: spread the tiles over the columns in proportion to their stream offset
+            if ((MODE == 2 || MODE == 3) && lane < NV)
+                store_word(&aw[(size_t)lane * ntiles + tile], make_word(epoch, kStAgg, lane == 0 ? agg[0] : agg[NV - 1]));
             const double frac = (double)(s0 - p.rec_off[0]) / (double)(p.rec_off[n] - p.rec_off[0] + 1);
 #pragma unroll
             for (int f = 0; f < NV; ++f) pre[f] = (i64)(frac * (double)p.cap[f]);
@@ -552,34 +532,25 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
 #pragma unroll
         for (int f = 0; f < NV; ++f) {
             if (live) p.offs[f][r0 + lane] = (u64)pre[f] + excl[f];
-            if constexpr (H > 1) {  // the second half's records follow the first half's bytes
-                const int d1 = S.dst[f][kRecs + lane] + (int)agg[f];
-                S.dst[f][kRecs + lane] = d1;
-                if (kRecs + lane < cnt) p.offs[f][r0 + kRecs + lane] = (u64)pre[f] + (u64)d1;
-            }
-            if (lane == 0 && r0 + cnt == n) p.offs[f][n] = (u64)pre[f] + aggT[f];
+            if (lane == 0 && r0 + cnt == n) p.offs[f][n] = (u64)pre[f] + agg[f];
         }
+        const u32 nrec = nch[0] + (NV == 2 ? nch[NV - 1] : 0u);
         const u32 cinc = wave_incl_scan_u32_dpp(nrec);
         S.cs[lane] = (int)(cinc - nrec);
-        int T = (int)__builtin_amdgcn_readlane(cinc, 63);
-        if constexpr (H > 1) {
-            const u32 n1 = (u32)S.cs[kRecs + lane];
-            const u32 c1 = wave_incl_scan_u32_dpp(n1) + (u32)T;
-            S.cs[kRecs + lane] = (int)(c1 - n1);
-            T = (int)__builtin_amdgcn_readlane(c1, 63);
-        }
+        S.nch0[lane] = (int)nch[0];
         if (lane == 0) {
-            S.cs[kRecs * H] = T;
+            const int T = (int)__builtin_amdgcn_readlane(cinc, 63);
+            S.cs[kRecs] = T;
 #pragma unroll
             for (int f = 0; f < NV; ++f) {
-                S.dst[f][kRecs * H] = (int)aggT[f];
+                S.dst[f][kRecs] = (int)agg[f];
                 S.pre[f] = pre[f];
                 const i64 cap = (i64)p.cap[f];
-                if (MODE == 0 && aggT[f] > 0 && pre[f] + (i64)aggT[f] > cap) {
+                if (MODE == 0 && agg[f] > 0 && pre[f] + (i64)agg[f] > cap) {
                     if constexpr (SPEC) store_word(&ctrl[kCtrlSpecErr], make_word(epoch, kStAgg, kErrCapacity));
                     else atomicOr(p.err, kErrCapacity);
                 }
-                S.lim[f] = max((i64)0, min((i64)aggT[f], cap - pre[f]));
+                S.lim[f] = max((i64)0, min((i64)agg[f], cap - pre[f]));
             }
             S.total = too_large ? -1 : T;
         }
@@ -603,7 +574,7 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
         for (int u = 0; u < kU; ++u) {
             const int c = c0 + kThreads * u + tid;
             const bool has = c < T;
-            const int k = has ? lds_search_pow2<kRecs * H>(S.cs, cnt, c) : 0;
+            const int k = has ? lds_search_64(S.cs, cnt, c) : 0;
             int q = c - S.cs[k];
             const int n0 = S.nch0[k];
             const bool second = NV == 2 && q >= n0;
@@ -669,13 +640,11 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
 // when AHEAD % 8 == 0, so the header lines it reads are still in that XCD's L2 when tile t + AHEAD
 // is staged, and the stream is fetched from HBM about once.
 template <int NF, int NV, bool MIX, int MODE = 0, int DIAG = 0, int SK = 4, int PR = 2, int STG = kStage,
-          bool EARLY = false, int PACE = 0, bool XCDP = false, int AHEAD = 0, int NOP = 0, bool SPEC = false, int SPECX = 0,
-          int H = 1>
+          bool EARLY = false, int PACE = 0, bool XCDP = false, int AHEAD = 0, int NOP = 0, bool SPEC = false, int SPECX = 0>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))) void decode_pipe_kernel(
     DecodeParams p, u64* flags, u32 epoch) {
     static_assert(NV == 1 || NV == 2, "decode handles one or two string columns");
-    static_assert(H == 1 || (H == 2 && AHEAD == 0), "128-record copier tiles: no parse-ahead");
-    __shared__ Lds<NV, STG, H> S;
+    __shared__ Lds<NV, STG> S;
     const u64 ntiles = num_tiles(p.n);
     u64* aw = flags;                        // aggregate words [NV][ntiles]
     u64* pw = flags + (size_t)NV * ntiles;  // prefix words [NV][ntiles]
@@ -694,8 +663,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
         return;
     }
     const u64 tile = kRoles ? blockIdx.x - P - 1 : blockIdx.x;
-    if (tile * H >= ntiles) return;
-    copier<NF, NV, MIX, MODE, DIAG, STG, EARLY, AHEAD, NOP, SPEC && MODE == 0 && SPECX != 1, H>(p, flags, epoch, tile, forced, S);
+    if (tile >= ntiles) return;
+    copier<NF, NV, MIX, MODE, DIAG, STG, EARLY, AHEAD, NOP, SPEC && MODE == 0 && SPECX != 1>(p, flags, epoch, tile, forced, S);
 }
 
 // ---------------------------------------------------------------- the gate
@@ -1030,7 +999,7 @@ hipError_t launch_gather_layout(const DecodeParams& p, u64* flags, u32 epoch, hi
 }
 
 template <int NF, int NV, bool MIX, int MODE, int DIAG, int SK = 4, int PR = 2, int STG = kStage, bool EARLY = false,
-          int PACE = 0, bool XCDP = false, int AHEAD = 0, int NOP = 0, bool SPEC = false, int SPECX = 0, int H = 1>
+          int PACE = 0, bool XCDP = false, int AHEAD = 0, int NOP = 0, bool SPEC = false, int SPECX = 0>
 hipError_t launch(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stream, int pnum = 1, int pden = 1) {
     if (DIAG && !p.dbg) return hipErrorInvalidValue;  // timestamps need SYMHIP_DEBUG_PTR (tuning builds)
     static int cus[16] = {0};
@@ -1046,12 +1015,12 @@ hipError_t launch(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stre
     if (AHEAD > 0 && P > (u64)(AHEAD + 4 * PR - 1) / (4 * PR)) P = (AHEAD + 4 * PR - 1) / (4 * PR);  // tiles [0, AHEAD)
     DecodeParams q = p;
     q.pipe_parsers = (unsigned)P;
-    const u64 grid = (kRoles ? P + 1 : 0) + (nt + H - 1) / H;  // a copier per H tiles
+    const u64 grid = kRoles ? P + 1 + nt : nt;
     // speculative parsers: only kv layouts (no int32 fields) under the pipeline with its parsers
     constexpr bool kSpec = SPEC && NF == 0 && MODE == 0;
     if constexpr (kSpec) {
         if (p.impl != kImplLookback && P > 0) {
-            hipLaunchKernelGGL((decode_pipe_kernel<NF, NV, MIX, MODE, DIAG, SK, PR, STG, EARLY, PACE, XCDP, AHEAD, NOP, true, SPECX, H>),
+            hipLaunchKernelGGL((decode_pipe_kernel<NF, NV, MIX, MODE, DIAG, SK, PR, STG, EARLY, PACE, XCDP, AHEAD, NOP, true, SPECX>),
                                dim3((unsigned)grid), dim3(kThreads), 0, stream, q, flags, epoch);
             if ((e = hipGetLastError()) != hipSuccess) return e;
             if (SPECX == 1 || SPECX == 2) return hipSuccess;  // timing variants: no gate (WRONG on misfits)
@@ -1062,7 +1031,7 @@ hipError_t launch(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stre
             return hipGetLastError();
         }
     }
-    hipLaunchKernelGGL((decode_pipe_kernel<NF, NV, MIX, MODE, DIAG, SK, PR, STG, EARLY, PACE, XCDP, AHEAD, NOP, false, 0, H>), dim3((unsigned)grid),
+    hipLaunchKernelGGL((decode_pipe_kernel<NF, NV, MIX, MODE, DIAG, SK, PR, STG, EARLY, PACE, XCDP, AHEAD, NOP, false>), dim3((unsigned)grid),
                        dim3(kThreads), 0, stream, q, flags, epoch);
     return hipGetLastError();
 }
@@ -1071,11 +1040,11 @@ constexpr int kParsersNum = 3;   // parser workgroups = #CUs * 3/4
 constexpr int kParsersDen = 4;
 
 template <int MODE, int DIAG, int SK = kScanPer, int PR = 2, int STG = kStage, bool EARLY = false, int PACE = 0,
-          bool XCDP = false, int AHEAD = 0, int NOP = 0, bool SPEC = false, int SPECX = 0, int H = 1>
+          bool XCDP = false, int AHEAD = 0, int NOP = 0, bool SPEC = false, int SPECX = 0>
 hipError_t launch_layout(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stream, int pnum = kParsersNum,
                          int pden = kParsersDen) {
 #define SYMHIP_PIPE_LAUNCH(NF, NV, MIX) \
-    launch<NF, NV, MIX, MODE, DIAG, SK, PR, STG, EARLY, PACE, XCDP, AHEAD, NOP, SPEC, SPECX, H>(p, flags, epoch, stream, pnum, pden)
+    launch<NF, NV, MIX, MODE, DIAG, SK, PR, STG, EARLY, PACE, XCDP, AHEAD, NOP, SPEC, SPECX>(p, flags, epoch, stream, pnum, pden)
     if (p.type)  // mixed kv batch: GetRequest / SetRequest per record
         return p.lay.nfixed == 0 && p.lay.nvar == 2 ? SYMHIP_PIPE_LAUNCH(0, 2, true) : hipErrorInvalidValue;
     if (p.lay.nfixed == 0 && p.lay.nvar == 1) return SYMHIP_PIPE_LAUNCH(0, 1, false);
@@ -1177,10 +1146,6 @@ hipError_t launch_decode_pipe(const DecodeParams& p, void* flags, unsigned epoch
         case 731: return pipe::launch_layout<0, 0, 4, 2, pipe::kStage, false, 0, false, 0, 0, true>(p, fl, epoch, stream, 1, 2);
         case 732: return pipe::launch_layout<0, 0, pipe::kScanPer, 4, pipe::kStage, false, 0, false, 0, 0, true>(p, fl, epoch, stream, 1, 2);
         case 733: return pipe::launch_layout<0, 0, pipe::kScanPer, 1, pipe::kStage, false, 0, false, 0, 0, true>(p, fl, epoch, stream, 1, 2);
-        // 128-record copier tiles (two 64-record halves; the words stay per 64 records): 750 the
-        // speculative default so, 751 its copiers-only timing (WRONG output)
-        case 750: return pipe::launch_layout<0, 0, 1, 2, pipe::kStage, false, 0, false, 0, 0, true, 0, 2>(p, fl, epoch, stream, 1, 2);
-        case 751: return pipe::launch_layout<1, 0, 1, 2, pipe::kStage, false, 0, false, 0, 0, true, 0, 2>(p, fl, epoch, stream, 1, 2);
         // the gather copier (no LDS stage, output-stationary copy); 601: its timing mode (WRONG output)
         case 600: return pipe::launch_gather_layout<0>(p, fl, epoch, stream);
         case 601: return pipe::launch_gather_layout<1>(p, fl, epoch, stream);

@@ -267,18 +267,6 @@ __device__ __forceinline__ u32 wave_incl_scan_u32(u32 v, int lane) {
 }
 
 // Largest j in [0, cnt) with a[j] <= key (a ascending, a[0] <= key); cnt <= 64.
-// The same over up to N entries (N a power of two).
-template <int N, typename T>
-__device__ __forceinline__ int lds_search_pow2(const T* a, int cnt, T key) {
-    int j = 0;
-#pragma unroll
-    for (int step = N / 2; step > 0; step >>= 1) {
-        const int c = j + step;
-        if (c < cnt && a[c] <= key) j = c;
-    }
-    return j;
-}
-
 template <typename T>
 __device__ __forceinline__ int lds_search_64(const T* a, int cnt, T key) {
     int j = 0;
