@@ -191,7 +191,11 @@ int sym_ctx_set_decode_impl(sym_ctx* ctx, int impl) {
     if (impl != SYM_DECODE_PIPELINE && impl != SYM_DECODE_THREE_KERNEL && impl != SYM_DECODE_LOOKBACK)
         return fail(SYM_ERR_INVALID, "sym_ctx_set_decode_impl: unknown implementation %d", impl);
     ctx->decode_impl = impl;
-    return SYM_OK;
+    // a new choice starts without a speculation hold (decode_pipe.hip spec_held: err[2..3])
+    DeviceGuard g(ctx->device);
+    if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
+    hipError_t e = hipMemset(ctx->err + 2, 0, sizeof(uint64_t));
+    return e == hipSuccess ? SYM_OK : hip_fail(e, "clearing the speculation hold");
 }
 
 int sym_ctx_set_encode_impl(sym_ctx* ctx, int impl) {

@@ -29,7 +29,8 @@ struct sym_ctx {
     void* flags = nullptr;  // default decode's aggregate / prefix words (epoch-tagged)
     size_t flag_bytes = 0;
     unsigned epoch = 0;     // tag of the last decode call's look-back words
-    unsigned* err = nullptr;  // [0] device error word (kErr* bits); [1] unused
+    unsigned* err = nullptr;  // [0] device error word (kErr* bits); [1] unused; [2..3] the decode's
+                              // speculation hold (decode_pipe.hip spec_held), a u64 epoch
     // scan workspace of the packetizer, the field getters, the flat decode and the mixed encode
     // (stream-ordered, so calls on one stream share it)
     void* frag = nullptr;

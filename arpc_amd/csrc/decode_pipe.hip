@@ -206,6 +206,17 @@ __device__ __forceinline__ void spec_flen(u64 L, int nvr, u32 k0, u64 (&flen)[NV
     }
 }
 
+// Speculation hold: after a batch whose speculative lengths missed, the gate stores in the ctx's
+// error block (bytes 8..15, next to the error word) an epoch kSpecHold calls ahead; until the calls
+// reach it the parsers parse exactly and the copiers skip the check, so a producer whose records do
+// not follow the generator layout pays the re-decode once per kSpecHold calls, not on every batch.
+constexpr u64 kSpecHold = 2 * 64;  // epochs (a decode call takes two)
+__device__ __forceinline__ u64* spec_hold_word(const DecodeParams& p) { return (u64*)(p.err + 2); }
+__device__ __forceinline__ bool spec_held(const DecodeParams& p, u32 epoch) {
+    const u64 h = *spec_hold_word(p);  // written by an earlier launch: visible at this launch's start
+    return (u64)epoch < h && h - (u64)epoch <= kSpecHold;  // (a hold from before an epoch wrap is stale)
+}
+
 // parse_tiles with speculative lengths: the record offsets (and types), plus one 4-byte load per
 // two-field record.
 template <int NV, bool MIX, int R>
@@ -254,6 +265,7 @@ template <int NF, int NV, bool MIX, int R = 2, int WB = 32, bool LIGHT = false, 
 __device__ void parser(const DecodeParams& p, u64* aw, u64* pw, u64 ntiles, u32 epoch, u32 P, u64 tmax = ~0ull) {
     const int wave = threadIdx.x >> 6;
     const u64 tlim = min(ntiles, tmax);
+    const bool held = SPEC && NF == 0 && spec_held(p, epoch);  // exact parsing this call (wave-uniform)
     // tile of (sequence index j, slot h) = tb + ts * (j + h)
     u64 tb = 0, ts = 1, j0 = ((u64)blockIdx.x * 4 + wave) * R, jstep = (u64)P * 4 * R;
     if (XCDP && P % 8 == 0) {
@@ -278,7 +290,7 @@ __device__ void parser(const DecodeParams& p, u64* aw, u64* pw, u64 ntiles, u32 
                     __builtin_amdgcn_s_sleep(8);
             }
         }
-        if constexpr (SPEC && NF == 0) parse_tiles_spec<NV, MIX, R>(p, aw, ntiles, epoch, th);
+        if (SPEC && NF == 0 && !held) parse_tiles_spec<NV, MIX, R>(p, aw, ntiles, epoch, th);
         else parse_tiles<NF, NV, MIX, R, WB, LIGHT>(p, aw, ntiles, epoch, th);
     }
 }
@@ -372,6 +384,7 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
 
     // ---- 1. stage (and wave 0's record offsets, and with EARLY its prefix words) ----
     u64 start = 0, endv = 0, wv_early = 0;
+    const bool held = SPEC && spec_held(p, epoch);  // loaded beside the stage, used after the parse
     if (wave == 0) {
         start = p.rec_off[r0 + min(lane, cnt)];
         endv = p.rec_off[r0 + min(lane + 1, cnt)];
@@ -468,7 +481,7 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
             for (int f = 0; f < NF; ++f) p.fixed[f][r0 + lane] = fx[f];
         }
         u64* const ctrl = ctrl_words(flags, NV, ntiles);
-        if constexpr (SPEC) {  // the parsers' speculative lengths of these records, from the same bytes
+        if (SPEC && !held) {  // the parsers' speculative lengths of these records, from the same bytes
             const u32 k0 = live && nvr == 2 && L >= 30 ? rd32(22) : 0u;
             u64 sf[NV];
             spec_flen<NV>(live ? L : 0, nvr, k0, sf);
@@ -686,6 +699,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
         if (tagged(e, epoch)) atomicOr(p.err, (unsigned)(e & kValMask));
     }
     if (!redo) return;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *spec_hold_word(p) = (u64)epoch + kSpecHold;  // parse exactly for a while
     // the exact pipeline on a persistent grid: a quarter of the workgroups parse every tile exactly,
     // one scans, the rest copy tiles c, c + C, ... (a copier whose prefix is late looks back, so no
     // role waits on residency)

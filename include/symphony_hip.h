@@ -99,7 +99,9 @@ int sym_ctx_check(sym_ctx* ctx, void* stream);
  *                           For kv schemas the parsers take each record's lengths from the generator's
  *                           layout and the copiers check them against the exact parse; a second small
  *                           launch on the same stream (no host sync) merges the error bits, or decodes
- *                           the batch again exactly when a record did not follow that layout.
+ *                           the batch again exactly when a record did not follow that layout; the
+ *                           ctx then parses exactly for its next 64 decode calls (setting the impl
+ *                           clears that hold).
  *   SYM_DECODE_THREE_KERNEL parse -> scan -> copy as three stream-ordered launches (no
  *                           inter-workgroup waiting at all).
  *   SYM_DECODE_LOOKBACK     the pipeline with its parsers and scanner idle: every copier takes the

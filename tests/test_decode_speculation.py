@@ -40,6 +40,7 @@ def codec(dev):
 
 @pytest.fixture(autouse=True, params=sorted(DECODE_IMPLS))
 def decode_impl(request, codec):
+    """Setting the impl also clears the ctx's speculation hold, so every test starts speculating."""
     codec.set_decode_impl(DECODE_IMPLS[request.param])
     yield request.param
     codec.set_decode_impl(0)
@@ -159,3 +160,18 @@ def test_small_decode_after_large_mixed_encode(codec, dev):
         stream, off = oracle.encode_batch(b.fixed, b.var)
         got = decode_gpu(codec, "kv_set_request", stream, off, dev)  # checks the error word
         assert_decode_equal(got, oracle.decode_batch(0, 2, stream, off), f"n={n}")
+
+
+def test_hold_after_a_miss_then_speculation_again(codec, dev):
+    """After a batch the speculation missed, the ctx parses exactly for a while (the gate's hold);
+    batches decoded in that time -- clean ones and ones with misfits -- and after it are all exact."""
+    n = 6000
+    b = datagen.make_batch(schema="kv_set_request", n=n, lens=(("uniform", 0, 40), ("uniform", 0, 200)), seed=21)
+    stream, off = oracle.encode_batch(b.fixed, b.var)
+    bad, bad_off = _with_trailers(stream, off, [7, 4000], extra=2, seed=3)
+    want_bad = oracle.decode_batch(0, 2, bad, bad_off)
+    want_ok = oracle.decode_batch(0, 2, stream, off)
+    seq = [True, False, True] + [False] * 70 + [True, False]  # past the hold (64 calls) and a miss again
+    for i, misfit in enumerate(seq):
+        got = decode_gpu(codec, "kv_set_request", bad if misfit else stream, bad_off if misfit else off, dev)
+        assert_decode_equal(got, want_bad if misfit else want_ok, f"call {i}")
