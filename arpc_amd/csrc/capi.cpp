@@ -712,7 +712,7 @@ int sym_flat_decode_ex2(sym_ctx* ctx, const sym_field* fields, int nfields, uint
     if (n && (!d_in || !d_rec_src || !d_status || (nfields && (!d_cols || !caps || !d_offs))))
         return fail(SYM_ERR_INVALID, "sym_flat_decode: NULL argument");
     if ((d_lo == nullptr) != (d_hi == nullptr)) return fail(SYM_ERR_INVALID, "sym_flat_decode: give both d_lo and d_hi");
-    if (d_rec_len && !d_lo) return fail(SYM_ERR_INVALID, "sym_flat_decode: records in place need d_lo / d_hi");
+    if (n && d_rec_len && !d_lo) return fail(SYM_ERR_INVALID, "sym_flat_decode: records in place need d_lo / d_hi");
     for (int k = 0; k < nfields; ++k) {
         const bool inplace = d_item_len && d_item_len[k];
         if ((n && !d_cols[k] && (flat_scalar(fields[k]) || caps[k])) || (!flat_scalar(fields[k]) && !d_offs[k]))

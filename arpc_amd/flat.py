@@ -233,9 +233,10 @@ def decode(codec: Codec, schema: FlatSchema, data: torch.Tensor, rec_off: torch.
     _check_col(rec_off, torch.int64, "rec_off", codec.device)
     if rec_len is not None:
         _check_col(rec_len, torch.int64, "rec_len", codec.device)
-        if extent is None or span is None:
+        if rec_len.numel() and (extent is None or span is None):
             raise ValueError("records in place need extent and span")
     n = rec_off.numel() - 1 if rec_len is None else rec_len.numel()
+    in_place = rec_len is not None and n > 0
     if span is None:
         span = int(rec_off[-1].item() - rec_off[0].item()) if n else 0
     if extent is None and n:  # data's readable extent: rec_off[0], rec_off[n] (device values)
@@ -282,9 +283,9 @@ def decode(codec: Codec, schema: FlatSchema, data: torch.Tensor, rec_off: torch.
     cf = schema.c_fields()
     lists = schema.has_lists
     hs = _stream_handle(codec.device, stream)
-    lo, hi = extent if (extent is not None and (rec_len is not None)) else (0, 0)
+    lo, hi = extent if in_place else (0, 0)
     _native.check(codec._lib.sym_flat_decode_ex2(codec._ctx, cf, len(schema.fields), n, _dptr(data) or 1,
-                                                _dptr(rec_off), _dptr(rec_len) if rec_len is not None else 0, lo, hi,
+                                                _dptr(rec_off) or 1, _dptr(rec_len) if in_place else 0, lo, hi,
                                                 _native.ptr_array(ptrs), _native.u64_array(caps),
                                                 _native.ptr_array(offs), _native.ptr_array(items) if lists else None,
                                                 _native.ptr_array(ilens) if lists else None,

@@ -425,3 +425,12 @@ def test_gpu_decode_ex2_argument_checks(codec, dev):
                                         _native.ptr_array([_dptr(o)]), _native.ptr_array([_dptr(io)]),
                                         _native.ptr_array([_dptr(io)]), _native.u64_array([1]), _dptr(st), 0, 0)
     assert rc == _native.SYM_ERR_INVALID
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("recs", [[], [{"RootId": i32(5)}, {"RootId": i32(6)}, {"RootId": i32(7)}]],
+                         ids=["no records", "every nested message nil"])
+def test_gpu_empty_levels(codec, dev, recs):
+    """A batch of no records, and one whose nested fields are all nil: the inner levels (decoded in
+    place) have no records."""
+    gpu_round_trip(codec, ROOT, recs, dev)
