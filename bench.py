@@ -12,8 +12,8 @@ one: step s encodes set s%4 and decodes the stream encoded two steps earlier.
 Prints ONE JSON line on rank 0.  `value` = algorithmic GB/s over all ranks (SURVEY.md
 section 8d: 694 B encode + 695 B decode per 64/256 record), timed with a barrier +
 device sync on both sides, max over ranks.  `roofline` reports the dominant single kernel
-(encode_kernel, or the one-launch decode_pipe_kernel) from HIP events on the stream the kernels
-run on; `cpu_baseline` times the C restatement of the Go codec (oracle/) on a bounded sample on
+(encode_kernel, or decode_pipe_kernel) from HIP events on the stream the kernels run on (the
+decode's events also cover its small gate launch, so `achieved` is conservative); `cpu_baseline` times the C restatement of the Go codec (oracle/) on a bounded sample on
 this host, at 1 thread and at the host's core share, plus config 1's echo record.
 --config 4 is SURVEY 8d config 4: 2^23 SetRequests per GPU (seed 0x5EED0003 + rank), the shards
 of a 2^26-record batch on 8 GPUs.  Legs beside the headline (outside the timed region): the mixed
