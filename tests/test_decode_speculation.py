@@ -175,3 +175,21 @@ def test_hold_after_a_miss_then_speculation_again(codec, dev):
     for i, misfit in enumerate(seq):
         got = decode_gpu(codec, "kv_set_request", bad if misfit else stream, bad_off if misfit else off, dev)
         assert_decode_equal(got, want_bad if misfit else want_ok, f"call {i}")
+
+
+@pytest.mark.parametrize("seed", [31, 32, 33, 34])
+def test_random_batches_with_random_misfits(codec, dev, seed):
+    """Random kv schema, record count (ragged: not a multiple of 64), value sizes and misfit density
+    (none, one, a few, every record), each checked bit for bit against the oracle."""
+    rng = np.random.default_rng(seed)
+    schema = ["kv_get_request", "kv_set_request", "kv_get_response"][seed % 3]
+    s = schemas.BY_NAME[schema]
+    n = int(rng.integers(1000, 120000))
+    lens = tuple(("uniform", 0, int(rng.choice([16, 64, 300, 2000]))) for _ in range(s.nvar))
+    b = datagen.make_batch(schema=schema, n=n, lens=lens, seed=seed)
+    stream, off = oracle.encode_batch(b.fixed, b.var)
+    density = [0, 1, 7, n][seed % 4]
+    which = sorted(set(int(x) for x in rng.integers(0, n, density))) if density < n else range(n)
+    data, rec_off = _with_trailers(stream, off, which, extra=int(rng.integers(1, 9)), seed=seed)
+    got = decode_gpu(codec, s, data, rec_off, dev, misalign=int(rng.integers(0, 16)))
+    assert_decode_equal(got, oracle.decode_batch(s.nfixed, s.nvar, data, rec_off), f"{schema}/{n}/{density}")
