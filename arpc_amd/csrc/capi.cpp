@@ -191,11 +191,11 @@ int sym_ctx_set_decode_impl(sym_ctx* ctx, int impl) {
     if (impl != SYM_DECODE_PIPELINE && impl != SYM_DECODE_THREE_KERNEL && impl != SYM_DECODE_LOOKBACK)
         return fail(SYM_ERR_INVALID, "sym_ctx_set_decode_impl: unknown implementation %d", impl);
     ctx->decode_impl = impl;
-    // a new choice starts without a speculation hold (decode_pipe.hip spec_held: err[2..3])
-    DeviceGuard g(ctx->device);
-    if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
-    hipError_t e = hipMemset(ctx->err + 2, 0, sizeof(uint64_t));
-    return e == hipSuccess ? SYM_OK : hip_fail(e, "clearing the speculation hold");
+    // A new choice starts without a speculation hold: every hold an earlier call set (or a call still
+    // running sets) names a call number below the ones from now on, so it is stale (decode_pipe.hip
+    // spec_held).  Host-side only: nothing to order against decodes still on the caller's streams.
+    ctx->decode_seq += symhip::kSpecHoldCalls + 1;
+    return SYM_OK;
 }
 
 int sym_ctx_set_encode_impl(sym_ctx* ctx, int impl) {
@@ -318,6 +318,7 @@ int symhip::capi::decode_call(const char* what, sym_ctx* ctx, Layout lay, const 
     p.ws = ctx->ws;
     p.flags = ctx->flags;
     p.epoch = epoch;
+    p.seq = ++ctx->decode_seq;
     p.err = ctx->err;
     p.impl = ctx->decode_impl;
 #ifdef SYMHIP_TUNING

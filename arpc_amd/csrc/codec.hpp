@@ -83,6 +83,8 @@ struct DecodeParams {
     void* ws;       // decode_workspace_bytes() bytes (three-kernel decode)
     void* flags;    // decode_pipe_flag_bytes() bytes of aggregate / prefix words (default decode)
     unsigned epoch; // word tag of this call, in [1, kEpochLimit)
+    uint64_t seq;   // this decode call's number in its ctx (1, 2, ...; never reset): the speculation
+                    // hold counts decode calls with it (decode_pipe.hip spec_held)
     u64_t* dbg;     // tuning builds only (tools/fused_timeline.py): per-tile timestamps, else null
     unsigned pipe_parsers;  // set by launch_decode_pipe: parser workgroups of the launch
     unsigned* err;  // persistent device error word (kErr* bits), cleared by the host
@@ -112,6 +114,8 @@ size_t decode_workspace_bytes(int nvar, uint64_t n);
 // they need zeroing only when allocated and when the epoch wraps.
 size_t decode_pipe_flag_bytes(int nvar, uint64_t n);
 constexpr unsigned kEpochLimit = 1u << 20;
+// Decode calls that parse exactly after a batch whose speculative lengths missed (decode_pipe.hip).
+constexpr uint64_t kSpecHoldCalls = 64;
 hipError_t launch_decode_pipe(const DecodeParams& p, void* flags, unsigned epoch, hipStream_t stream);
 
 #ifdef SYMHIP_TUNING

@@ -40,6 +40,7 @@ struct sym_ctx {
     uint8_t crypt_keys[64] = {0};
     int num_cus = 0;
     int decode_impl = SYM_DECODE_PIPELINE;
+    uint64_t decode_seq = 0;  // decode calls so far (DecodeParams::seq): the speculation hold counts them
     int encode_impl = 0;  // SYM_ENCODE_* (mixed batches' size scan)
     // reassembly: the stream its gated general path runs on beside the caller's, and the fork /
     // join events (created on first use)

@@ -207,14 +207,17 @@ __device__ __forceinline__ void spec_flen(u64 L, int nvr, u32 k0, u64 (&flen)[NV
 }
 
 // Speculation hold: after a batch whose speculative lengths missed, the gate stores in the ctx's
-// error block (bytes 8..15, next to the error word) an epoch kSpecHold calls ahead; until the calls
-// reach it the parsers parse exactly and the copiers skip the check, so a producer whose records do
-// not follow the generator layout pays the re-decode once per kSpecHold calls, not on every batch.
-constexpr u64 kSpecHold = 2 * 64;  // epochs (a decode call takes two)
+// error block (bytes 8..15, next to the error word) the number of the decode call kSpecHold calls
+// ahead (p.seq counts a ctx's decode calls and is never reset); until the calls reach it the parsers
+// parse exactly and the copiers skip the check, so a producer whose records do not follow the
+// generator layout pays the re-decode once per kSpecHold calls, not on every batch.  The host makes a
+// hold stale without touching the device: sym_ctx_set_decode_impl advances the ctx's call number past
+// any hold an earlier call could have set.
+constexpr u64 kSpecHold = kSpecHoldCalls;  // decode calls (codec.hpp)
 __device__ __forceinline__ u64* spec_hold_word(const DecodeParams& p) { return (u64*)(p.err + 2); }
-__device__ __forceinline__ bool spec_held(const DecodeParams& p, u32 epoch) {
+__device__ __forceinline__ bool spec_held(const DecodeParams& p) {
     const u64 h = *spec_hold_word(p);  // written by an earlier launch: visible at this launch's start
-    return (u64)epoch < h && h - (u64)epoch <= kSpecHold;  // (a hold from before an epoch wrap is stale)
+    return p.seq < h && h - p.seq <= kSpecHold;
 }
 
 // parse_tiles with speculative lengths: the record offsets (and types), plus one 4-byte load per
@@ -265,7 +268,7 @@ template <int NF, int NV, bool MIX, int R = 2, int WB = 32, bool LIGHT = false, 
 __device__ void parser(const DecodeParams& p, u64* aw, u64* pw, u64 ntiles, u32 epoch, u32 P, u64 tmax = ~0ull) {
     const int wave = threadIdx.x >> 6;
     const u64 tlim = min(ntiles, tmax);
-    const bool held = SPEC && NF == 0 && spec_held(p, epoch);  // exact parsing this call (wave-uniform)
+    const bool held = SPEC && NF == 0 && spec_held(p);  // exact parsing this call (wave-uniform)
     // tile of (sequence index j, slot h) = tb + ts * (j + h)
     u64 tb = 0, ts = 1, j0 = ((u64)blockIdx.x * 4 + wave) * R, jstep = (u64)P * 4 * R;
     if (XCDP && P % 8 == 0) {
@@ -384,7 +387,7 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
 
     // ---- 1. stage (and wave 0's record offsets, and with EARLY its prefix words) ----
     u64 start = 0, endv = 0, wv_early = 0;
-    const bool held = SPEC && spec_held(p, epoch);  // loaded beside the stage, used after the parse
+    const bool held = SPEC && spec_held(p);  // loaded beside the stage, used after the parse
     if (wave == 0) {
         start = p.rec_off[r0 + min(lane, cnt)];
         endv = p.rec_off[r0 + min(lane + 1, cnt)];
@@ -653,8 +656,9 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
 // when AHEAD % 8 == 0, so the header lines it reads are still in that XCD's L2 when tile t + AHEAD
 // is staged, and the stream is fetched from HBM about once.
 template <int NF, int NV, bool MIX, int MODE = 0, int DIAG = 0, int SK = 4, int PR = 2, int STG = kStage,
-          bool EARLY = false, int PACE = 0, bool XCDP = false, int AHEAD = 0, int NOP = 0, bool SPEC = false, int SPECX = 0>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))) void decode_pipe_kernel(
+          bool EARLY = false, int PACE = 0, bool XCDP = false, int AHEAD = 0, int NOP = 0, bool SPEC = false, int SPECX = 0,
+          int WPE = 6>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void decode_pipe_kernel(
     DecodeParams p, u64* flags, u32 epoch) {
     static_assert(NV == 1 || NV == 2, "decode handles one or two string columns");
     __shared__ Lds<NV, STG> S;
@@ -699,7 +703,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
         if (tagged(e, epoch)) atomicOr(p.err, (unsigned)(e & kValMask));
     }
     if (!redo) return;
-    if (blockIdx.x == 0 && threadIdx.x == 0) *spec_hold_word(p) = (u64)epoch + kSpecHold;  // parse exactly for a while
+    if (blockIdx.x == 0 && threadIdx.x == 0) *spec_hold_word(p) = p.seq + kSpecHold + 1;  // the next kSpecHold calls parse exactly
     // the exact pipeline on a persistent grid: a quarter of the workgroups parse every tile exactly,
     // one scans, the rest copy tiles c, c + C, ... (a copier whose prefix is late looks back, so no
     // role waits on residency)
@@ -1013,7 +1017,7 @@ hipError_t launch_gather_layout(const DecodeParams& p, u64* flags, u32 epoch, hi
 }
 
 template <int NF, int NV, bool MIX, int MODE, int DIAG, int SK = 4, int PR = 2, int STG = kStage, bool EARLY = false,
-          int PACE = 0, bool XCDP = false, int AHEAD = 0, int NOP = 0, bool SPEC = false, int SPECX = 0>
+          int PACE = 0, bool XCDP = false, int AHEAD = 0, int NOP = 0, bool SPEC = false, int SPECX = 0, int WPE = 6>
 hipError_t launch(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stream, int pnum = 1, int pden = 1) {
     if (DIAG && !p.dbg) return hipErrorInvalidValue;  // timestamps need SYMHIP_DEBUG_PTR (tuning builds)
     static int cus[16] = {0};
@@ -1034,7 +1038,7 @@ hipError_t launch(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stre
     constexpr bool kSpec = SPEC && NF == 0 && MODE == 0;
     if constexpr (kSpec) {
         if (p.impl != kImplLookback && P > 0) {
-            hipLaunchKernelGGL((decode_pipe_kernel<NF, NV, MIX, MODE, DIAG, SK, PR, STG, EARLY, PACE, XCDP, AHEAD, NOP, true, SPECX>),
+            hipLaunchKernelGGL((decode_pipe_kernel<NF, NV, MIX, MODE, DIAG, SK, PR, STG, EARLY, PACE, XCDP, AHEAD, NOP, true, SPECX, WPE>),
                                dim3((unsigned)grid), dim3(kThreads), 0, stream, q, flags, epoch);
             if ((e = hipGetLastError()) != hipSuccess) return e;
             if (SPECX == 1 || SPECX == 2) return hipSuccess;  // timing variants: no gate (WRONG on misfits)
@@ -1045,7 +1049,7 @@ hipError_t launch(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stre
             return hipGetLastError();
         }
     }
-    hipLaunchKernelGGL((decode_pipe_kernel<NF, NV, MIX, MODE, DIAG, SK, PR, STG, EARLY, PACE, XCDP, AHEAD, NOP, false>), dim3((unsigned)grid),
+    hipLaunchKernelGGL((decode_pipe_kernel<NF, NV, MIX, MODE, DIAG, SK, PR, STG, EARLY, PACE, XCDP, AHEAD, NOP, false, 0, WPE>), dim3((unsigned)grid),
                        dim3(kThreads), 0, stream, q, flags, epoch);
     return hipGetLastError();
 }
@@ -1054,11 +1058,11 @@ constexpr int kParsersNum = 3;   // parser workgroups = #CUs * 3/4
 constexpr int kParsersDen = 4;
 
 template <int MODE, int DIAG, int SK = kScanPer, int PR = 2, int STG = kStage, bool EARLY = false, int PACE = 0,
-          bool XCDP = false, int AHEAD = 0, int NOP = 0, bool SPEC = false, int SPECX = 0>
+          bool XCDP = false, int AHEAD = 0, int NOP = 0, bool SPEC = false, int SPECX = 0, int WPE = 6>
 hipError_t launch_layout(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stream, int pnum = kParsersNum,
                          int pden = kParsersDen) {
 #define SYMHIP_PIPE_LAUNCH(NF, NV, MIX) \
-    launch<NF, NV, MIX, MODE, DIAG, SK, PR, STG, EARLY, PACE, XCDP, AHEAD, NOP, SPEC, SPECX>(p, flags, epoch, stream, pnum, pden)
+    launch<NF, NV, MIX, MODE, DIAG, SK, PR, STG, EARLY, PACE, XCDP, AHEAD, NOP, SPEC, SPECX, WPE>(p, flags, epoch, stream, pnum, pden)
     if (p.type)  // mixed kv batch: GetRequest / SetRequest per record
         return p.lay.nfixed == 0 && p.lay.nvar == 2 ? SYMHIP_PIPE_LAUNCH(0, 2, true) : hipErrorInvalidValue;
     if (p.lay.nfixed == 0 && p.lay.nvar == 1) return SYMHIP_PIPE_LAUNCH(0, 1, false);
@@ -1160,6 +1164,12 @@ hipError_t launch_decode_pipe(const DecodeParams& p, void* flags, unsigned epoch
         case 731: return pipe::launch_layout<0, 0, 4, 2, pipe::kStage, false, 0, false, 0, 0, true>(p, fl, epoch, stream, 1, 2);
         case 732: return pipe::launch_layout<0, 0, pipe::kScanPer, 4, pipe::kStage, false, 0, false, 0, 0, true>(p, fl, epoch, stream, 1, 2);
         case 733: return pipe::launch_layout<0, 0, pipe::kScanPer, 1, pipe::kStage, false, 0, false, 0, 0, true>(p, fl, epoch, stream, 1, 2);
+        // round 4: 8 waves per SIMD (<= 64 VGPRs) with a 16 KiB stage (8 copiers per CU by LDS), with the
+        // speculative default's geometry; 742: copiers only at 8 per CU (WRONG output); 743: the 16 KiB
+        // stage at 6 waves per SIMD
+        case 740: return pipe::launch_layout<0, 0, 1, 2, 16384, false, 0, false, 0, 0, true, 0, 8>(p, fl, epoch, stream, 1, 2);
+        case 742: return pipe::launch_layout<1, 0, 1, 2, 16384, false, 0, false, 0, 0, true, 0, 8>(p, fl, epoch, stream, 1, 2);
+        case 743: return pipe::launch_layout<0, 0, 1, 2, 16384, false, 0, false, 0, 0, true, 0, 6>(p, fl, epoch, stream, 1, 2);
         // the gather copier (no LDS stage, output-stationary copy); 601: its timing mode (WRONG output)
         case 600: return pipe::launch_gather_layout<0>(p, fl, epoch, stream);
         case 601: return pipe::launch_gather_layout<1>(p, fl, epoch, stream);

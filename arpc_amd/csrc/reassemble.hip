@@ -390,9 +390,30 @@ __global__ __launch_bounds__(256) void key_kernel(Args a, const unsigned* gate) 
     const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
     bool down = false;  // a key below its predecessor's: the batch needs the sort
     if (i < a.n && !*a.nonmono) {  // the run head: every datagram is a pending DataPacket here
-        u64 h = i;
+        // The RPCIDs never decrease on this path, so the head is the first index holding r: one load
+        // when i starts its run (the common case), else a gallop back (steps 1, 2, 4, ...) to an index
+        // below the run, then a binary search -- O(log run) loads, so one RPCID repeated over a whole
+        // batch costs 2^20 * ~40 loads, not a walk of the run per datagram.
         const u64 r = a.rpc[i];
-        while (h > 0 && a.rpc[h - 1] == r) --h;
+        u64 h = i;
+        if (i > 0 && a.rpc[i - 1] == r) {
+            i64 lo = -1, hi = (i64)i - 1;  // rpc[lo] < r (lo = -1: none), rpc[hi] == r
+            for (i64 step = 1;; step <<= 1) {
+                const i64 c = hi - step;
+                if (c < 0) break;
+                if (a.rpc[c] != r) {
+                    lo = c;
+                    break;
+                }
+                hi = c;
+            }
+            while (hi - lo > 1) {
+                const i64 mid = lo + (hi - lo) / 2;
+                if (a.rpc[mid] == r) hi = mid;
+                else lo = mid;
+            }
+            h = (u64)hi;
+        }
         a.gid[i] = (u32)h;  // non-decreasing
     } else if (i < a.n) {
         const u32 s = a.slot[i];

@@ -244,8 +244,10 @@ class BatchingSerializer:
     marshal / unmarshal call is one record (as Go's Call goroutines make them, pkg/rpc/client.go:233-310,
     server.go:152 / :173), coalesced with the calls other threads make meanwhile into one device
     batch by the C ABI's batcher (sym_batcher_*, arpc_amd/csrc/batcher.cpp).  Same results and
-    errors as SymphonySerializer; safe to share across threads (ctypes releases the GIL while a
-    call waits for its batch)."""
+    errors as SymphonySerializer, for records of any size: a record larger than the batcher's slot
+    (max_bytes) goes through a SymphonySerializer of its own, as the reference's Serializer has no
+    size limit.  Safe to share across threads (ctypes releases the GIL while a call waits for its
+    batch)."""
 
     def __init__(self, device: int = 0, service_id: int = 0, method_id: int = 0, max_records: int = 4096,
                  max_bytes: int = 8 << 20, max_wait_us: int = 0):
@@ -253,6 +255,7 @@ class BatchingSerializer:
         self._cfg = (max_records, max_bytes, max_wait_us)
         self._batchers: dict = {}
         self._lock = threading.Lock()
+        self._direct = SymphonySerializer(device, service_id, method_id)  # records over max_bytes
 
     def _batcher(self, s: schemas.Schema):
         b = self._batchers.get(s.schema_id)
@@ -274,6 +277,8 @@ class BatchingSerializer:
         ptrs = (ctypes.c_void_p * max(1, s.nvar))(*[ctypes.addressof(b) for b in bufs])
         lens = (ctypes.c_uint64 * max(1, s.nvar))(*[len(v) for v in vals])
         size = s.overhead + sum(len(v) for v in vals)
+        if size > self._cfg[1]:
+            return self._direct.marshal(msg)
         out = ctypes.create_string_buffer(max(1, size))
         n = ctypes.c_uint64()
         _native.check(_native.lib().sym_batcher_encode_one(self._batcher(s), fixed, ptrs, lens, self.service_id,
@@ -284,6 +289,8 @@ class BatchingSerializer:
     def unmarshal(self, data: bytes, out) -> None:
         s = _schema_of(out)
         data = bytes(data)
+        if len(data) > self._cfg[1]:
+            return self._direct.unmarshal(data, out)
         cap = max(1, len(data))
         fixed = (ctypes.c_int32 * max(1, s.nfixed))()
         bufs = [ctypes.create_string_buffer(cap) for _ in range(s.nvar)]

@@ -181,3 +181,21 @@ def test_batcher_capacity_and_size_limits(gpu):
     assert L.sym_batcher_decode_one(h, rec, len(rec), None, outs, caps, got, ctypes.byref(st)) == _native.SYM_ERR_CAPACITY
     assert list(got) == [10, 100] and kb.raw[:10] == key and vb.raw == val[:16]
     L.sym_batcher_destroy(h)
+
+
+@pytest.mark.gpu
+def test_batching_serializer_records_over_the_slot_size(gpu):
+    """A record larger than the batcher's slot (max_bytes) still marshals and unmarshals exactly:
+    the reference Serializer has no size limit, so it takes the direct path."""
+    from arpc_amd.serializer import BatchingSerializer, SetRequest
+    ser = BatchingSerializer(gpu, service_id=1, method_id=2, max_bytes=4096)
+    for vlen in (100, 4096 - 30 - 8, 5000, 70000):
+        m = SetRequest(b"k" * 8, bytes(range(256)) * (vlen // 256) + bytes(vlen % 256))
+        data = ser.marshal(m)
+        want = bytearray(oracle.marshal([], [m.Key, m.Value]))
+        want[5:13] = struct.pack("<II", 1, 2)
+        assert data == bytes(want), vlen
+        out = SetRequest()
+        ser.unmarshal(data, out)
+        assert out == m, vlen
+    ser.close()

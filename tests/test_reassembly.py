@@ -295,3 +295,21 @@ def test_reassembly_nondecreasing_rpcids_gpu(gcodec, gdev, seed):
             else:
                 dgs.append(dgram(r, T, s, bytes(rng.integers(0, 256, int(rng.integers(0, 40)), dtype=np.uint8))))
     _gpu_vs_oracle(gcodec, gdev, *batch(dgs), misalign=seed)
+
+
+@pytest.mark.gpu
+def test_reassembly_one_rpcid_over_a_large_batch_gpu(gcodec, gdev):
+    """One RPCID repeated over 2^17 datagrams (non-decreasing, so the run-head path): pairs of
+    packets 0, 1 of TotalPackets 2, each pair completing a message (RPCID reuse after completion,
+    fragmentation.go:62-181), a duplicate and an incomplete tail.  The run head is found by a gallop
+    and a binary search (the one-step walk back was O(run^2))."""
+    n = 1 << 17
+    dgs = []
+    for k in range(n // 2):
+        dgs.append(dgram(42, 2, 0, bytes([k & 255]) * (k % 23)))
+        if k == 777:
+            dgs.append(dgram(42, 2, 0, b"dup"))
+        dgs.append(dgram(42, 2, 1, b"#"))
+    dgs.append(dgram(42, 2, 0, b"left open"))
+    want = _gpu_vs_oracle(gcodec, gdev, *batch(dgs))
+    assert len(want[2]) == n // 2

@@ -3,7 +3,7 @@
 #   pass 0: --kernel-trace --stats      (per-kernel durations)
 #   pass 1: --pmc FETCH_SIZE            (HBM read side; x2 on gfx950, MI355X_MICROARCH.md HBM)
 #   pass 2: --pmc WRITE_SIZE            (HBM write side)
-#   pass 3+: extra counter sets given as arguments, one pass each
+#   pass 3+: extra counter sets given as arguments (counters of one set joined by commas), one pass each
 # Each pass under its own timeout; stop at the first failure.
 set -u
 OUT=${OUT:-gpurun_out/prof}
@@ -26,5 +26,5 @@ run write --pmc WRITE_SIZE || exit 1
 i=0
 for set in "$@"; do
   i=$((i+1))
-  run "pmc$i" --pmc $set || exit 1
+  run "pmc$i" --pmc ${set//,/ } || exit 1
 done
