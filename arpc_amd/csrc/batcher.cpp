@@ -24,8 +24,18 @@
 // allocated with hipHostMalloc is mapped into the device's address space), so a batch is one
 // launch plus one hipStreamSynchronize and no copies.  The encode and decode queues each own a
 // sym_ctx (only the current leader uses it) and a non-blocking stream.
+//
+// Records up to kRingRecordMax bytes (every kv / echo request an RPC carries in practice) take the
+// ring instead (record_worker.hip): no launch per record or batch, one persistent single-workgroup
+// worker per queue serving tickets in place in coherent pinned slots; a record is published with one
+// store, served within a few microseconds, and read back as soon as its own flag is set.  Larger
+// records keep the batched path above.  Both give the same bytes and statuses.
 #include <hip/hip_runtime.h>
 
+#include <immintrin.h>
+#include <sched.h>
+
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
@@ -36,6 +46,7 @@
 #include "../../include/symphony_hip.h"
 #include "codec.hpp"
 #include "ctx.hpp"
+#include "record_worker.hpp"
 
 using namespace symhip::capi;
 using symhip::Layout;
@@ -68,6 +79,17 @@ struct BSlot {
     std::condition_variable cv;  // the slot's callers: DONE, or "lead me"
 };
 
+// The ring of one queue (record_worker.hpp): coherent mapped pinned memory, the callers' ticket
+// counter, and the worker's generation (relaunched under `mu` when one has exited).
+struct Ring {
+    symhip::RingCtl* ctl = nullptr;
+    uint8_t* slots = nullptr;
+    std::atomic<uint64_t> ticket{0};
+    std::atomic<uint64_t> gen{0};
+    std::mutex mu;
+    hipStream_t stream = nullptr;
+};
+
 struct Queue {
     sym_ctx* ctx = nullptr;
     hipStream_t stream = nullptr;
@@ -90,6 +112,7 @@ struct sym_batcher {
     uint64_t B = 0;  // record bytes per batch
     uint32_t wait_us = 0;
     Queue q[2];      // 0 encode, 1 decode
+    Ring ring[2];    // 0 encode, 1 decode: records up to kRingRecordMax bytes
 };
 
 namespace {
@@ -245,6 +268,109 @@ void release(Queue& q, std::unique_lock<std::mutex>& lk, BSlot& s) {
     }
 }
 
+// ---- the ring path (record_worker.hip) ----
+int ring_launch(sym_batcher* b, int dir, Ring& r, uint64_t gen) {
+    DeviceGuard g(b->device);
+    if (g.err != hipSuccess) return hip_fail(g.err, "sym_batcher: hipSetDevice");
+    hipError_t e = symhip::launch_record_worker(r.ctl, r.slots, b->lay, dir, gen, r.stream);
+    return e == hipSuccess ? SYM_OK : hip_fail(e, "sym_batcher: record worker launch");
+}
+
+int ring_create(sym_batcher* b, int dir, Ring& r) {
+    DeviceGuard g(b->device);
+    if (g.err != hipSuccess) return hip_fail(g.err, "sym_batcher_create: hipSetDevice");
+    const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
+    hipError_t e = hipHostMalloc((void**)&r.ctl, sizeof(symhip::RingCtl), fl);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&r.slots, (size_t)symhip::kRingSlots * symhip::kSlotBytes, fl);
+    if (e != hipSuccess) return fail(SYM_ERR_NOMEM, "sym_batcher_create: ring of %d slots: %s", symhip::kRingSlots,
+                                     hipGetErrorString(e));
+    memset(r.ctl, 0, sizeof(symhip::RingCtl));
+    memset(r.slots, 0, (size_t)symhip::kRingSlots * symhip::kSlotBytes);
+    for (int k = 0; k < symhip::kRingSlots; ++k)
+        ((symhip::SlotCtl*)(r.slots + (size_t)k * symhip::kSlotBytes))->turn = (uint64_t)k;
+    if ((e = hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking)) != hipSuccess)
+        return hip_fail(e, "sym_batcher_create: worker stream");
+    r.gen = 1;
+    return ring_launch(b, dir, r, 1);
+}
+
+void ring_destroy(Ring& r) {
+    if (r.ctl && r.stream) {  // tell the worker to leave, wait until it has
+        __atomic_store_n(&r.ctl->stop, 1, __ATOMIC_SEQ_CST);
+        (void)hipStreamSynchronize(r.stream);
+    }
+    if (r.stream) (void)hipStreamDestroy(r.stream);
+    if (r.slots) (void)hipHostFree(r.slots);
+    if (r.ctl) (void)hipHostFree(r.ctl);
+    r.stream = nullptr;
+    r.slots = nullptr;
+    r.ctl = nullptr;
+}
+
+// After a record is published: a worker that announced its exit (ctl->quit == its generation) and did
+// not see the record is replaced.  `waited`: the caller has waited long for its record -- a worker
+// that has gone (or whose launch ended) without serving it is replaced as well.
+int ring_ensure_worker(sym_batcher* b, int dir, Ring& r, bool waited) {
+    const uint64_t gen = r.gen.load(std::memory_order_acquire);
+    const uint64_t q = __atomic_load_n(&r.ctl->quit, __ATOMIC_SEQ_CST);
+    bool gone = __atomic_load_n(&r.ctl->gone, __ATOMIC_ACQUIRE) == gen;
+    if (q != gen && !gone && !waited) return SYM_OK;
+    std::lock_guard<std::mutex> lk(r.mu);
+    if (r.gen.load(std::memory_order_acquire) != gen) return SYM_OK;  // another caller relaunched it
+    if (!gone && waited && q != gen) {  // a long wait: has the worker's launch ended anyway?
+        DeviceGuard g(b->device);
+        const hipError_t e = hipStreamQuery(r.stream);
+        if (e == hipErrorNotReady) return SYM_OK;
+        if (e != hipSuccess) return hip_fail(e, "sym_batcher: record worker");
+        gone = true;
+    }
+    // the worker either takes the announcement back (it saw a record) or leaves
+    while (!gone && __atomic_load_n(&r.ctl->quit, __ATOMIC_ACQUIRE) == gen)
+        gone = __atomic_load_n(&r.ctl->gone, __ATOMIC_ACQUIRE) == gen;
+    if (!gone) return SYM_OK;
+    r.gen.store(gen + 1, std::memory_order_release);
+    return ring_launch(b, dir, r, gen + 1);
+}
+
+// Spin until *p == want (a pause first, then yielding the CPU: there may be more callers than cores);
+// every ~10 ms make sure a worker runs.
+int ring_wait(sym_batcher* b, int dir, Ring& r, const uint64_t* p, uint64_t want) {
+    for (uint64_t i = 0; __atomic_load_n(p, __ATOMIC_ACQUIRE) != want; ++i) {
+        if (i < 256) {
+            _mm_pause();
+            continue;
+        }
+        sched_yield();
+        if ((i & 4095) == 0) {
+            const int rc = ring_ensure_worker(b, dir, r, true);
+            if (rc != SYM_OK) return rc;
+        }
+    }
+    return SYM_OK;
+}
+
+// One record through the ring: take a ticket and its slot, `fill` the in area, publish, wait for the
+// worker, `drain` the out area, free the slot.
+template <typename Fill, typename Drain>
+int ring_call(sym_batcher* b, int dir, uint64_t in_len, Fill&& fill, Drain&& drain) {
+    Ring& r = b->ring[dir];
+    const uint64_t t = r.ticket.fetch_add(1, std::memory_order_relaxed);
+    uint8_t* slot = r.slots + (size_t)(t % symhip::kRingSlots) * symhip::kSlotBytes;
+    symhip::SlotCtl* sc = (symhip::SlotCtl*)slot;
+    int rc = ring_wait(b, dir, r, &sc->turn, t);
+    if (rc != SYM_OK) return rc;
+    fill(slot + symhip::kSlotInAt);
+    sc->in_len = in_len;
+    __atomic_store_n(&sc->req, t + 1, __ATOMIC_RELEASE);
+    __atomic_fetch_add(&r.ctl->posted, 1, __ATOMIC_SEQ_CST);  // then look at quit (the worker's hand-shake)
+    rc = ring_ensure_worker(b, dir, r, false);
+    if (rc == SYM_OK) rc = ring_wait(b, dir, r, &sc->done, t + 1);
+    if (rc != SYM_OK) return rc;  // (the slot stays taken: the device failed)
+    drain(slot + symhip::kSlotOutAt);
+    __atomic_store_n(&sc->turn, t + symhip::kRingSlots, __ATOMIC_RELEASE);
+    return SYM_OK;
+}
+
 void destroy_queue(Queue& q) {
     if (q.stream) (void)hipStreamDestroy(q.stream);
     for (BSlot& s : q.slot) {
@@ -293,6 +419,7 @@ int sym_batcher_create(int device, int schema, uint32_t max_records, uint64_t ma
         }
         if (rc != SYM_OK) break;
         for (BSlot& s : q.slot) slot_reset(s, b->lay.nvar);
+        rc = ring_create(b, dir, b->ring[dir]);
     }
     if (rc != SYM_OK) {
         sym_batcher_destroy(b);
@@ -304,6 +431,7 @@ int sym_batcher_create(int device, int schema, uint32_t max_records, uint64_t ma
 
 int sym_batcher_destroy(sym_batcher* b) {
     if (!b) return SYM_OK;
+    for (Ring& r : b->ring) ring_destroy(r);
     for (Queue& q : b->q) destroy_queue(q);
     delete b;
     return SYM_OK;
@@ -328,6 +456,23 @@ int sym_batcher_encode_one(sym_batcher* b, const int32_t* fixed, const uint8_t* 
                                  (unsigned long long)size);
     if (!out || out_cap < size) return fail(SYM_ERR_CAPACITY, "sym_batcher_encode_one: out needs %llu bytes",
                                             (unsigned long long)size);
+    if (var <= symhip::kRingRecordMax) {  // the ring: the worker writes the record, IDs included
+        return ring_call(
+            b, 0, var,
+            [&](uint8_t* in) {
+                symhip::EncIn* h = (symhip::EncIn*)in;
+                for (int f = 0; f < symhip::kMaxFixed; ++f) h->fixed[f] = f < L.nfixed ? fixed[f] : 0;
+                h->service_id = service_id;
+                h->method_id = method_id;
+                uint8_t* p = in + sizeof(symhip::EncIn);
+                for (int f = 0; f < symhip::kMaxVar; ++f) {
+                    h->len[f] = f < L.nvar ? lens[f] : 0;
+                    if (f < L.nvar && lens[f]) memcpy(p, fields[f], lens[f]);
+                    p += f < L.nvar ? lens[f] : 0;
+                }
+            },
+            [&](const uint8_t* o) { memcpy(out, o, size); });
+    }
     Queue& q = b->q[0];
     std::unique_lock<std::mutex> lk(q.mu);
     BSlot& s = *reserve(b, q, lk, size);
@@ -368,6 +513,24 @@ int sym_batcher_decode_one(sym_batcher* b, const uint8_t* data, uint64_t len, in
         return fail(SYM_ERR_INVALID, "sym_batcher_decode_one: NULL argument");
     if (len > b->B) return fail(SYM_ERR_INVALID, "sym_batcher_decode_one: a %llu-byte record exceeds max_bytes",
                                 (unsigned long long)len);
+    if (len <= symhip::kRingRecordMax) {
+        bool short_cap = false;
+        const int rc = ring_call(
+            b, 1, len, [&](uint8_t* in) { if (len) memcpy(in, data, len); },
+            [&](const uint8_t* o) {
+                const symhip::DecOut* d = (const symhip::DecOut*)o;
+                *status = (uint8_t)d->status;
+                for (int f = 0; f < L.nfixed; ++f) fixed[f] = d->fixed[f];
+                for (int f = 0; f < L.nvar; ++f) {
+                    lens[f] = d->len[f];
+                    const uint64_t c = lens[f] < caps[f] ? lens[f] : caps[f];
+                    short_cap |= c < lens[f];
+                    if (c) memcpy(fields[f], o + symhip::kDecData + (f ? d->at1 : 0), c);
+                }
+            });
+        if (rc != SYM_OK) return rc;
+        return short_cap ? fail(SYM_ERR_CAPACITY, "sym_batcher_decode_one: a field exceeds its cap") : SYM_OK;
+    }
     Queue& q = b->q[1];
     std::unique_lock<std::mutex> lk(q.mu);
     BSlot& s = *reserve(b, q, lk, len);
@@ -402,10 +565,11 @@ int sym_batcher_stats(sym_batcher* b, uint64_t* enc_batches, uint64_t* enc_recor
                       uint64_t* dec_records) {
     if (!b) return fail(SYM_ERR_INVALID, "sym_batcher_stats: NULL batcher");
     uint64_t v[4];
-    for (int dir = 0; dir < 2; ++dir) {
+    for (int dir = 0; dir < 2; ++dir) {  // batches: the batched path's launches + the ring worker's passes
         std::lock_guard<std::mutex> lk(b->q[dir].mu);
-        v[2 * dir] = b->q[dir].batches;
-        v[2 * dir + 1] = b->q[dir].records;
+        const symhip::RingCtl* c = b->ring[dir].ctl;
+        v[2 * dir] = b->q[dir].batches + (c ? __atomic_load_n(&c->passes, __ATOMIC_ACQUIRE) : 0);
+        v[2 * dir + 1] = b->q[dir].records + (c ? __atomic_load_n(&c->served, __ATOMIC_ACQUIRE) : 0);
     }
     if (enc_batches) *enc_batches = v[0];
     if (enc_records) *enc_records = v[1];

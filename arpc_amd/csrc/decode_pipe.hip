@@ -361,7 +361,7 @@ __device__ void lookback(const DecodeParams& p, u64* aw, u64* pw, u64 ntiles, u6
 // bytes and tags ctrl[kCtrlMismatch] on any difference (the gate then decodes the batch again), and
 // a capacity error is tagged in ctrl[kCtrlSpecErr] (it may come from a speculative prefix), merged
 // into p.err by the gate when the speculation held.
-template <int NF, int NV, bool MIX, int MODE, int DIAG, int STG, bool EARLY, int AHEAD, int NOP, bool SPEC>
+template <int NF, int NV, bool MIX, int MODE, int DIAG, int STG, bool EARLY, int AHEAD, int NOP, bool SPEC, int UK = kU>
 __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 epoch, u64 tile, bool forced, Lds<NV, STG>& S) {
     constexpr int kLoads = (STG / 16 + kThreads - 1) / kThreads;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -580,14 +580,14 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
     const i64 pre0 = uniform_i64(S.pre[0]), pre1 = uniform_i64(S.pre[NV - 1]);
     const i64 lim0 = uniform_i64(S.lim[0]), lim1 = uniform_i64(S.lim[NV - 1]);
     const uintptr_t stage_end = base + (uintptr_t)nst;
-    for (int c0 = 0; c0 < T; c0 += kThreads * kU) {  // uniform loop
-        u32x4 v[kU];
-        int P_[kU], code[kU];
-        uintptr_t X[kU];
-        bool glob[kU];
+    for (int c0 = 0; c0 < T; c0 += kThreads * UK) {  // uniform loop
+        u32x4 v[UK];
+        int P_[UK], code[UK];
+        uintptr_t X[UK];
+        bool glob[UK];
         bool anyg = false;
 #pragma unroll
-        for (int u = 0; u < kU; ++u) {
+        for (int u = 0; u < UK; ++u) {
             const int c = c0 + kThreads * u + tid;
             const bool has = c < T;
             const int k = has ? lds_search_64(S.cs, cnt, c) : 0;
@@ -606,15 +606,15 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
             v[u] = has && !glob[u] ? lds16u(S.stage, (int)(X[u] - base)) : u32x4{0, 0, 0, 0};
         }
         if (__ballot(anyg)) {  // past the staged span: HBM loads, all issued before any use
-            u32x4 g[kU];
+            u32x4 g[UK];
 #pragma unroll
-            for (int u = 0; u < kU; ++u) {
+            for (int u = 0; u < UK; ++u) {
                 const uintptr_t Xc = X[u] < in_last ? X[u] : in_last;
                 g[u] = ld16u(glob[u] ? Xc : safe);
                 code[u] |= glob[u] ? (int)((X[u] - Xc) << 5) : 0;
             }
 #pragma unroll
-            for (int u = 0; u < kU; ++u) {
+            for (int u = 0; u < UK; ++u) {
                 const u32 sh = ((u32)code[u] >> 5) & 31u;
                 if (sh) {  // a short field read from the stream's last block: shift down
                     u32 t[4];
@@ -625,7 +625,7 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
             }
         }
 #pragma unroll
-        for (int u = 0; u < kU; ++u) {
+        for (int u = 0; u < UK; ++u) {
             const bool second = (code[u] >> 10) & 1;
             const int nb = code[u] & 31;
             const i64 hi = min((i64)(P_[u] + nb), second ? lim1 : lim0);
@@ -657,7 +657,7 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
 // is staged, and the stream is fetched from HBM about once.
 template <int NF, int NV, bool MIX, int MODE = 0, int DIAG = 0, int SK = 4, int PR = 2, int STG = kStage,
           bool EARLY = false, int PACE = 0, bool XCDP = false, int AHEAD = 0, int NOP = 0, bool SPEC = false, int SPECX = 0,
-          int WPE = 6>
+          int WPE = 6, int UK = kU>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void decode_pipe_kernel(
     DecodeParams p, u64* flags, u32 epoch) {
     static_assert(NV == 1 || NV == 2, "decode handles one or two string columns");
@@ -681,7 +681,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(WPE, 8
     }
     const u64 tile = kRoles ? blockIdx.x - P - 1 : blockIdx.x;
     if (tile >= ntiles) return;
-    copier<NF, NV, MIX, MODE, DIAG, STG, EARLY, AHEAD, NOP, SPEC && MODE == 0 && SPECX != 1>(p, flags, epoch, tile, forced, S);
+    copier<NF, NV, MIX, MODE, DIAG, STG, EARLY, AHEAD, NOP, SPEC && MODE == 0 && SPECX != 1, UK>(p, flags, epoch, tile, forced, S);
 }
 
 // ---------------------------------------------------------------- the gate
@@ -1017,7 +1017,8 @@ hipError_t launch_gather_layout(const DecodeParams& p, u64* flags, u32 epoch, hi
 }
 
 template <int NF, int NV, bool MIX, int MODE, int DIAG, int SK = 4, int PR = 2, int STG = kStage, bool EARLY = false,
-          int PACE = 0, bool XCDP = false, int AHEAD = 0, int NOP = 0, bool SPEC = false, int SPECX = 0, int WPE = 6>
+          int PACE = 0, bool XCDP = false, int AHEAD = 0, int NOP = 0, bool SPEC = false, int SPECX = 0, int WPE = 6,
+          int UK = kU>
 hipError_t launch(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stream, int pnum = 1, int pden = 1) {
     if (DIAG && !p.dbg) return hipErrorInvalidValue;  // timestamps need SYMHIP_DEBUG_PTR (tuning builds)
     static int cus[16] = {0};
@@ -1038,7 +1039,7 @@ hipError_t launch(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stre
     constexpr bool kSpec = SPEC && NF == 0 && MODE == 0;
     if constexpr (kSpec) {
         if (p.impl != kImplLookback && P > 0) {
-            hipLaunchKernelGGL((decode_pipe_kernel<NF, NV, MIX, MODE, DIAG, SK, PR, STG, EARLY, PACE, XCDP, AHEAD, NOP, true, SPECX, WPE>),
+            hipLaunchKernelGGL((decode_pipe_kernel<NF, NV, MIX, MODE, DIAG, SK, PR, STG, EARLY, PACE, XCDP, AHEAD, NOP, true, SPECX, WPE, UK>),
                                dim3((unsigned)grid), dim3(kThreads), 0, stream, q, flags, epoch);
             if ((e = hipGetLastError()) != hipSuccess) return e;
             if (SPECX == 1 || SPECX == 2) return hipSuccess;  // timing variants: no gate (WRONG on misfits)
@@ -1049,7 +1050,7 @@ hipError_t launch(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stre
             return hipGetLastError();
         }
     }
-    hipLaunchKernelGGL((decode_pipe_kernel<NF, NV, MIX, MODE, DIAG, SK, PR, STG, EARLY, PACE, XCDP, AHEAD, NOP, false, 0, WPE>), dim3((unsigned)grid),
+    hipLaunchKernelGGL((decode_pipe_kernel<NF, NV, MIX, MODE, DIAG, SK, PR, STG, EARLY, PACE, XCDP, AHEAD, NOP, false, 0, WPE, UK>), dim3((unsigned)grid),
                        dim3(kThreads), 0, stream, q, flags, epoch);
     return hipGetLastError();
 }
@@ -1058,11 +1059,11 @@ constexpr int kParsersNum = 3;   // parser workgroups = #CUs * 3/4
 constexpr int kParsersDen = 4;
 
 template <int MODE, int DIAG, int SK = kScanPer, int PR = 2, int STG = kStage, bool EARLY = false, int PACE = 0,
-          bool XCDP = false, int AHEAD = 0, int NOP = 0, bool SPEC = false, int SPECX = 0, int WPE = 6>
+          bool XCDP = false, int AHEAD = 0, int NOP = 0, bool SPEC = false, int SPECX = 0, int WPE = 6, int UK = kU>
 hipError_t launch_layout(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stream, int pnum = kParsersNum,
                          int pden = kParsersDen) {
 #define SYMHIP_PIPE_LAUNCH(NF, NV, MIX) \
-    launch<NF, NV, MIX, MODE, DIAG, SK, PR, STG, EARLY, PACE, XCDP, AHEAD, NOP, SPEC, SPECX, WPE>(p, flags, epoch, stream, pnum, pden)
+    launch<NF, NV, MIX, MODE, DIAG, SK, PR, STG, EARLY, PACE, XCDP, AHEAD, NOP, SPEC, SPECX, WPE, UK>(p, flags, epoch, stream, pnum, pden)
     if (p.type)  // mixed kv batch: GetRequest / SetRequest per record
         return p.lay.nfixed == 0 && p.lay.nvar == 2 ? SYMHIP_PIPE_LAUNCH(0, 2, true) : hipErrorInvalidValue;
     if (p.lay.nfixed == 0 && p.lay.nvar == 1) return SYMHIP_PIPE_LAUNCH(0, 1, false);
@@ -1170,6 +1171,10 @@ hipError_t launch_decode_pipe(const DecodeParams& p, void* flags, unsigned epoch
         case 740: return pipe::launch_layout<0, 0, 1, 2, 16384, false, 0, false, 0, 0, true, 0, 8>(p, fl, epoch, stream, 1, 2);
         case 742: return pipe::launch_layout<1, 0, 1, 2, 16384, false, 0, false, 0, 0, true, 0, 8>(p, fl, epoch, stream, 1, 2);
         case 743: return pipe::launch_layout<0, 0, 1, 2, 16384, false, 0, false, 0, 0, true, 0, 6>(p, fl, epoch, stream, 1, 2);
+        // round 4: copy chunks per lane per step 3 / 4 (default stage), and with the 8-wave 16 KiB stage
+        case 744: return pipe::launch_layout<0, 0, 1, 2, pipe::kStage, false, 0, false, 0, 0, true, 0, 6, 3>(p, fl, epoch, stream, 1, 2);
+        case 745: return pipe::launch_layout<0, 0, 1, 2, pipe::kStage, false, 0, false, 0, 0, true, 0, 6, 4>(p, fl, epoch, stream, 1, 2);
+        case 746: return pipe::launch_layout<0, 0, 1, 2, 16384, false, 0, false, 0, 0, true, 0, 8, 3>(p, fl, epoch, stream, 1, 2);
         // the gather copier (no LDS stage, output-stationary copy); 601: its timing mode (WRONG output)
         case 600: return pipe::launch_gather_layout<0>(p, fl, epoch, stream);
         case 601: return pipe::launch_gather_layout<1>(p, fl, epoch, stream);

@@ -1,0 +1,65 @@
+// record_worker.hpp -- the ring of record slots shared by batcher.cpp (host) and record_worker.hip
+// (the persistent per-record worker).  All of it lives in pinned host memory allocated coherent and
+// mapped (hipHostMallocCoherent | hipHostMallocMapped): the callers write and read it with plain
+// stores / loads and C11 atomics, the worker with system-scope 8-byte atomics.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "codec.hpp"
+
+namespace symhip {
+
+constexpr int kRingSlots = 256;            // tickets in flight per queue (= the worker's window)
+constexpr size_t kSlotBytes = 16384;       // one slot: control words, in area, out area
+constexpr size_t kSlotInAt = 64;
+constexpr size_t kSlotIn = 4096 - 64;      // in area bytes
+constexpr size_t kSlotOutAt = 4096;
+constexpr size_t kSlotOut = kSlotBytes - kSlotOutAt;
+constexpr uint64_t kRingRecordMax = 4000;  // records (encode: field bytes; decode: record bytes) up to
+                                           // this go through the ring; larger ones through batches
+constexpr uint64_t kIdleTicks = 2000000;   // 20 ms without a record (s_memrealtime, 100 MHz): the worker exits
+
+struct RingCtl {          // one per queue, written as commented
+    uint64_t posted;      // callers: records published so far (atomic add after the slot's req store)
+    uint64_t stop;        // host: leave now (sym_batcher_destroy)
+    uint64_t quit;        // worker: the generation that is about to exit (0: none)
+    uint64_t gone;        // worker: the generation that has exited
+    uint64_t e, nproc;    // worker, at exit: its window base and records served (the next one resumes)
+    uint64_t served;      // worker: records served so far, every pass (sym_batcher_stats)
+    uint64_t passes;      // worker: passes that served records, every pass (sym_batcher_stats)
+};
+
+struct SlotCtl {          // the first 64 bytes of a slot
+    uint64_t req;         // caller: ticket + 1 once the in area is written
+    uint64_t done;        // worker: ticket + 1 once the out area is written
+    uint64_t turn;        // caller: the ticket that may use the slot next
+    uint64_t in_len;      // caller: encode: field bytes after EncIn; decode: record bytes
+    uint64_t pad[4];
+};
+
+struct EncIn {            // encode in area: the record's scalars, then its var fields' bytes back to back
+    int32_t fixed[kMaxFixed];
+    uint32_t service_id, method_id;
+    uint64_t len[kMaxVar];
+};
+static_assert(sizeof(EncIn) == 32, "EncIn layout");
+
+struct DecOut {           // decode out area: the parse, then field 0's bytes at kDecData, field 1's at
+    uint32_t status;      // kDecData + at1
+    int32_t fixed[kMaxFixed];
+    uint32_t pad;
+    uint64_t len[kMaxVar];
+    uint64_t at1;
+};
+constexpr size_t kDecData = 64;
+static_assert(sizeof(DecOut) <= kDecData, "DecOut layout");
+// decode out area bound: header + two fields of up to a record's bytes each (a malformed record may
+// point both at the same bytes), 16-byte rounded
+static_assert(kDecData + 2 * (kRingRecordMax + 16) <= kSlotOut, "decode out area");
+static_assert(sizeof(EncIn) + kRingRecordMax <= kSlotIn, "encode in area");
+
+hipError_t launch_record_worker(RingCtl* ctl, uint8_t* slots, Layout lay, int dir, uint64_t gen, hipStream_t stream);
+
+}  // namespace symhip

@@ -194,21 +194,29 @@ def cpu_baseline(kw: dict, seconds: float) -> dict:
                       "by oracle/symphony_oracle.c (-O2): C restatement of the Go codec, not Go (no Go toolchain)"}
 
 
-def decode_kernel_name(s) -> str:
-    """rocprof's name of the default decode's main launch for schema s: kv layouts (no int32 fields)
-    run the speculative parsers (decode_pipe.hip), followed by the small gate launch."""
+def decode_kernel_name(s, mixed: bool = False) -> str:
+    """rocprof's name of the default decode's main launch for schema s (mixed: the Get/Set batch):
+    kv layouts (no int32 fields) run the speculative parsers (decode_pipe.hip), followed by the
+    small gate launch."""
     spec, sk = ("true", 1) if s.nfixed == 0 else ("false", 2)  # scanner tiles per thread (decode_pipe.hip)
-    return f"decode_pipe_kernel<{s.nfixed}, {s.nvar}, false, 0, 0, {sk}, 2, 22528, false, 0, false, 0, 0, {spec}, 0>"
+    return (f"decode_pipe_kernel<{s.nfixed}, {s.nvar}, {'true' if mixed else 'false'}, 0, 0, {sk}, 2, 22528, false, 0, "
+            f"false, 0, 0, {spec}, 0, 6, 2>")
 
 
-def load_traffic(kernel: str):
-    """Per-launch HBM bytes of `kernel` from the committed PMC summary (profiles/), else None."""
+ENCODE_KERNEL = "encode_kernel<0, 2, 1, false, 4, false, 64>"
+ENCODE_MIXED_KERNEL = "encode_pipe_kernel<false, 1>"
+
+
+def load_traffic(kernel: str, workload: str):
+    """Per-launch HBM bytes (FETCH_SIZE x 2 + WRITE_SIZE) of `kernel` when it ran `workload`
+    ("config2", "config3", "config4", "mixed"), from the committed PMC summary profiles/traffic.json
+    (tools/make_traffic.py), else None: a kernel's bytes on one workload never stand in for another's."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     if not os.path.exists(path):
         return None
     try:
         d = json.load(open(path))
-        return d.get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")
+        return d.get("workloads", {}).get(workload, {}).get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")
     except (ValueError, OSError):
         return None
 
@@ -494,6 +502,53 @@ def boutique_leg(codec: Codec, dev, reps: int, n: int = 1 << 18) -> dict:
                     "reads of item totals); synthetic payloads, not the reference's trace"}
 
 
+def boutique_payloads_leg(codec: Codec, dev, reps: int) -> dict:
+    """SURVEY.md 8f N5 on the reference's own workload: the 93,275 online-boutique payloads of 30
+    message types (benchmark/serialization/online-boutique/payloads/*.jsonl, kept as data in
+    tests/golden/boutique_payloads.json.xz), each type one batch through arpc_amd.flat with
+    arpc_amd.boutique's schemas (onlineboutique.proto), device-resident columns.  Host clock around
+    all 30 encodes (then all 30 decodes), synchronised at the end.  The reference benchmark
+    (bench_test.go:282-351) runs the same payloads one message per call on one CPU core:
+    README.md:74-75 quotes Symphony Write 481,109 msg/s and Read 340,225 msg/s (Xeon Gold 6142,
+    99,848 payloads of an earlier payload set) -- context, not a like-for-like target."""
+    import lzma
+
+    from arpc_amd import boutique, flat
+    with lzma.open(os.path.join(ROOT, "tests", "golden", "boutique_payloads.json.xz"), "rt", encoding="utf-8") as fh:
+        types = json.load(fh)["types"]
+    batches = []
+    for name, objs in sorted(types.items()):
+        s = boutique.SCHEMAS[name]
+        batches.append((s, len(objs), boutique.columns_from_json(s, objs, dev)))
+    nmsg = sum(n for _, n, _ in batches)
+    enc = [flat.encode(codec, s, cols, n=n) for s, n, cols in batches]
+    dec = [flat.decode(codec, s, d, o, span=d.numel()) for (s, n, _), (d, o) in zip(batches, enc)]
+    torch.cuda.synchronize()
+    codec.check()
+    ok = all(bool((st == 0).all().item()) for _, st in dec)
+    stream_b = sum(int(d.numel()) for d, _ in enc)
+
+    def timed(fn) -> float:
+        ts = []
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        codec.check()
+        return float(np.median(ts))
+
+    te = timed(lambda: [flat.encode(codec, s, cols, n=n) for s, n, cols in batches])
+    td = timed(lambda: [flat.decode(codec, s, d, o, span=d.numel()) for (s, n, _), (d, o) in zip(batches, enc)])
+    return {"types": len(batches), "messages": nmsg, "stream_bytes": stream_b, "all_ok": ok,
+            "encode_ms": round(te * 1e3, 3), "decode_ms": round(td * 1e3, 3),
+            "encode_msg_per_s": round(nmsg / te), "decode_msg_per_s": round(nmsg / td),
+            "reference_readme_msg_per_s": {"write": 481109, "read": 340225},
+            "note": "all 30 payload files, one batch per type (30 encode and 30 decode tree walks), host clock; "
+                    "the reference README's numbers are Go, one message per call, one core"}
+
+
 def host_inclusive(codec: Codec, kw: dict, dev, steps: int) -> dict:
     """Host memory in, host memory out, through the C ABI's host entry points (what a cgo Serializer
     adapter calls): sym_encode_host then sym_decode_host on the same workload, each call chunked over
@@ -670,7 +725,17 @@ def mixed_leg(codec: Codec, dev, reps: int, cfg=None) -> dict:
     enc_alg = n + kb + 8 * (n + 1) + vb + 8 * (n + 1) + total + 8 * (n + 1)
     dec_alg = total + 8 * (n + 1) + n + kb + vb + 16 * (n + 1) + n
     nset = int(b.type.sum())
+    # the leg's own roofline: its dominant kernel by time, traffic from the mixed workload's profile
+    if enc_ms >= dec_ms:
+        kname, dom_ms, dom_b = ENCODE_MIXED_KERNEL, enc_ms, enc_alg
+    else:
+        kname, dom_ms, dom_b = decode_kernel_name(schemas.BY_NAME["kv_set_request"], mixed=True), dec_ms, dec_alg
+    ach = dom_b / (dom_ms * 1e-3) / 1e9
+    roof = {"bound": "hbm", "kernel": kname, "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBPS, 4),
+            "traffic": load_traffic(kname, "mixed") if cfg is None else None}
     return {"records": n, "set_records": nset, "set_fraction": round(nset / n, 4), "stream_bytes": total,
+            "roofline": roof,
             "round_trip_ok": ok, "encode_ms": round(enc_ms, 4), "encode_gbps": round(enc_alg / enc_ms / 1e6, 1),
             "decode_ms": round(dec_ms, 4), "decode_gbps": round(dec_alg / dec_ms / 1e6, 1),
             "gbps_algorithmic": round((enc_alg + dec_alg) / (enc_ms + dec_ms) / 1e6, 1),
@@ -725,8 +790,7 @@ def config3_leg(codec: Codec, dev, reps: int, cfg=None) -> dict:
             "encode_ms": round(enc_ms, 4), "encode_gbps": round(enc_b / enc_ms / 1e6, 1),
             "decode_ms": round(dec_ms, 4), "decode_gbps": round(dec_b / dec_ms / 1e6, 1),
             "gbps_algorithmic": round((enc_b + dec_b) / (enc_ms + dec_ms) / 1e6, 1),
-            "kernels": {"encode": "encode_kernel<0, 2, 1, false, 4, false, 64>",
-                        "decode": decode_kernel_name(schemas.BY_NAME["kv_set_request"])},
+            "kernels": {"encode": ENCODE_KERNEL, "decode": decode_kernel_name(schemas.BY_NAME["kv_set_request"])},
             "note": "config 3 (seed 0x5EED0002), the headline's algorithmic byte definition"}
 
 
@@ -751,6 +815,8 @@ def main():
     ap.add_argument("--crypto-reps", type=int, default=3, help="segment cipher leg repetitions (0 = skip)")
     ap.add_argument("--flat-reps", type=int, default=5, help="flat-schema codec leg repetitions (0 = skip)")
     ap.add_argument("--boutique-reps", type=int, default=3, help="online-boutique nested leg repetitions (0 = skip)")
+    ap.add_argument("--payload-reps", type=int, default=3,
+                    help="online-boutique reference payloads leg (all 30 types) repetitions (0 = skip)")
     ap.add_argument("--mixed-reps", type=int, default=10, help="mixed Get/Set leg repetitions (0 = skip)")
     ap.add_argument("--config3-reps", type=int, default=6, help="config 3 leg repetitions (0 = skip)")
     ap.add_argument("--trace-reps", type=int, default=3,
@@ -922,7 +988,7 @@ def main():
         kname, dom_ms, dom_bytes = (decode_kernel_name(s),
                                      dec_ms, dec_b)
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
-    traffic = load_traffic(kname)
+    traffic = load_traffic(kname, f"config{args.config}")
 
     if rank != 0:
         return
@@ -999,6 +1065,8 @@ def main():
         line["flat"] = flat_leg(codec, dev, args.flat_reps)
     if world == 1 and args.boutique_reps > 0:
         line["boutique"] = boutique_leg(codec, dev, args.boutique_reps)
+    if world == 1 and args.payload_reps > 0:
+        line["boutique_payloads"] = boutique_payloads_leg(codec, dev, args.payload_reps)
     if world == 1 and args.per_record > 0:
         line["per_record"] = per_record_leg(args.per_record, 64)
     if world == 1 and args.cpu_seconds > 0:

@@ -199,3 +199,40 @@ def test_batching_serializer_records_over_the_slot_size(gpu):
         ser.unmarshal(data, out)
         assert out == m, vlen
     ser.close()
+
+
+@pytest.mark.gpu
+def test_ring_path_limits_and_worker_relaunch(gpu):
+    """Records up to kRingRecordMax (4000) field / record bytes go through the persistent worker's ring
+    (record_worker.hip), larger ones through batches: both bit-exact with the oracle, at the edge too.
+    The worker leaves after 20 ms without records and the next call starts another (a sleep between
+    calls), and a batcher destroyed while idle or busy leaves nothing running."""
+    import time
+    from arpc_amd.serializer import BatchingSerializer, EchoRequest, SetRequest
+    ser = BatchingSerializer(gpu, service_id=3, method_id=4, max_bytes=1 << 16)
+    for total in (0, 1, 3999, 4000, 4001, 9000):
+        k = min(total, 64)
+        m = SetRequest(bytes(range(k)), bytes((7 * j) & 255 for j in range(total - k)))
+        data = ser.marshal(m)
+        want = bytearray(oracle.marshal([], [m.Key, m.Value]))
+        want[5:13] = struct.pack("<II", 3, 4)
+        assert data == bytes(want), total
+        out = SetRequest()
+        ser.unmarshal(data, out)
+        assert out == m, total
+        # decode of records around the limit, ring or batch by the record's own length
+        rec = bytes(oracle.marshal([], [b"", bytes(max(0, total - 30))]))
+        out = SetRequest()
+        ser.unmarshal(rec, out)
+        assert out.Value == bytes(max(0, total - 30)), total
+    e = EchoRequest(-5, 2**31 - 1, b"alice", b"x" * 3000)
+    data = ser.marshal(e)
+    assert data[:5] == b"\x01\x0d\x00\x00\x00"
+    for pause in (0.0, 0.05, 0.2):  # the worker exits when idle; the next call relaunches it
+        time.sleep(pause)
+        out = EchoRequest()
+        ser.unmarshal(data, out)
+        assert out == e, pause
+    st = ser.stats()
+    assert sum(v["decode_records"] for v in st.values()) >= 9
+    ser.close()

@@ -110,6 +110,47 @@ def test_mixed_full_size_stream_matches_pin(codec, dev, pins):
     assert sha(enc.offsets.cpu().numpy().view(np.uint64)) == pins["config2_mixed"]["sha256_offsets"]
 
 
+def test_mixed_ab_sequence_every_decode_impl(codec, dev):
+    """The input and call sequence of the one unexplained divergence (round 3, gpurun_out/kb_spec.txt:
+    tools/mixed_ab.py on CONFIG2_MIXED): two 2^20 Get/Set sets (set k's bytes XOR 0x3B*k), both
+    encoded, then decoded set by set with each decode implementation in turn on ONE ctx and into
+    output buffers that are not cleared between calls (speculative pipeline, three-kernel, forced
+    look-back, the pipeline again).  Every decode must return the encoded columns exactly
+    ("The round-3 mixed divergence")."""
+    from arpc_amd import _native
+    from arpc_amd.codec import DecodedBatch
+    b = datagen.make_mixed_batch(**datagen.CONFIG2_MIXED)
+    n, total = b.n, b.encoded_size()
+    kb, vb = int(b.key[1][-1]), int(b.val[1][-1])
+    t = torch.from_numpy(b.type).to(dev)
+    sets = []
+    for k in range(2):
+        key = (torch.from_numpy(b.key[0]).to(dev) ^ (0x3B * k), torch.from_numpy(b.key[1].view(np.int64)).to(dev))
+        val = (torch.from_numpy(b.val[0]).to(dev) ^ (0x3B * k), torch.from_numpy(b.val[1].view(np.int64)).to(dev))
+        out = (torch.empty(total + 16, dtype=torch.uint8, device=dev), torch.empty(n + 1, dtype=torch.int64, device=dev))
+        codec.encode_kv_mixed(t, key, val, 1, 1, 2, out=out[0], out_off=out[1])
+        dec = DecodedBatch(fixed=[], var=[(torch.empty(kb + 16, dtype=torch.uint8, device=dev),
+                                           torch.empty(n + 1, dtype=torch.int64, device=dev)),
+                                          (torch.empty(vb + 16, dtype=torch.uint8, device=dev),
+                                           torch.empty(n + 1, dtype=torch.int64, device=dev))],
+                           status=torch.empty(n, dtype=torch.uint8, device=dev))
+        sets.append((key, val, out, dec))
+    codec.check()
+    try:
+        for impl in (_native.SYM_DECODE_PIPELINE, _native.SYM_DECODE_THREE_KERNEL, _native.SYM_DECODE_LOOKBACK,
+                     _native.SYM_DECODE_PIPELINE):
+            codec.set_decode_impl(impl)
+            for k, (key, val, out, dec) in enumerate(sets):
+                codec.decode_kv_mixed(out[0], out[1], t, outputs=dec)
+                codec.check()
+                assert int(dec.status.sum().item()) == 0, (impl, k)
+                assert torch.equal(dec.var[0][0][:kb], key[0]), (impl, k, "keys")
+                assert torch.equal(dec.var[1][0][:vb], val[0]), (impl, k, "values")
+                assert torch.equal(dec.var[0][1], key[1]) and torch.equal(dec.var[1][1], val[1]), (impl, k, "offsets")
+    finally:
+        codec.set_decode_impl(_native.SYM_DECODE_PIPELINE)
+
+
 def _free_port() -> int:
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
