@@ -99,13 +99,9 @@ __device__ __forceinline__ int rec_nvar(const DecodeParams& p, u64 r) {
     else return NV;
 }
 
-// PACE > 0: a parser wave starts a step only once tile t0 - PACE has its prefix (bounded wait), so
-// the header lines it reads are still cached when that tile's copier stages them.  XCDP: a parser
-// takes only tiles whose copier shares its blockIdx % 8 group (one XCD under round-robin placement),
-// so those lines are in that XCD's L2 (speed only; any placement gives the same results).
 // R tiles th[] by one wave (lane = record): the records' field lengths with Go's checks, then each
 // tile's aggregate word per column.  Every load of the R records is issued before any is used.
-template <int NF, int NV, bool MIX, int R, int WB, bool LIGHT = false>
+template <int NF, int NV, bool MIX, int R, int WB>
 __device__ __forceinline__ void parse_tiles(const DecodeParams& p, u64* aw, u64 ntiles, u32 epoch, const u64 (&th)[R]) {
     constexpr int NW = WB / 4;  // window dwords
     const int lane = threadIdx.x & 63;
@@ -127,7 +123,6 @@ __device__ __forceinline__ void parse_tiles(const DecodeParams& p, u64* aw, u64 
 #pragma unroll
     for (int h = 0; h < R; ++h) {
         win[h] = live[h] && L[h] >= (u64)WB;
-        if constexpr (LIGHT) live[h] = win[h] = false;  // timing: offsets only, no header reads
         const uintptr_t wa = win[h] ? in + start[h] : (uintptr_t)aw;  // readable filler (>= 256 B)
 #pragma unroll
         for (int k = 0; k < WB / 16; ++k) {
@@ -258,48 +253,22 @@ __device__ __forceinline__ void parse_tiles_spec(const DecodeParams& p, u64* aw,
     }
 }
 
-// PACE > 0: a parser wave starts a step only once tile t0 - PACE has its prefix (bounded wait), so
-// the header lines it reads are still cached when that tile's copier stages them.  XCDP: a parser
-// takes only tiles whose copier shares its blockIdx % 8 group (one XCD under round-robin placement),
-// so those lines are in that XCD's L2 (speed only; any placement gives the same results).  tmax:
-// only tiles below it (the copiers parse the others ahead, AHEAD in decode_pipe_kernel).
-template <int NF, int NV, bool MIX, int R = 2, int WB = 32, bool LIGHT = false, int PACE = 0, bool XCDP = false,
-          bool SPEC = false>
-__device__ void parser(const DecodeParams& p, u64* aw, u64* pw, u64 ntiles, u32 epoch, u32 P, u64 tmax = ~0ull) {
+// Parser workgroup blockIdx.x of P: each wave takes R consecutive tiles per step, steps P * 4 * R
+// tiles apart.  SPEC: speculative lengths unless the ctx holds exact parsing (spec_held).
+template <int NF, int NV, bool MIX, int R = 2, int WB = 32, bool SPEC = false>
+__device__ void parser(const DecodeParams& p, u64* aw, u64 ntiles, u32 epoch, u32 P) {
     const int wave = threadIdx.x >> 6;
-    const u64 tlim = min(ntiles, tmax);
     const bool held = SPEC && NF == 0 && spec_held(p);  // exact parsing this call (wave-uniform)
-    // tile of (sequence index j, slot h) = tb + ts * (j + h)
-    u64 tb = 0, ts = 1, j0 = ((u64)blockIdx.x * 4 + wave) * R, jstep = (u64)P * 4 * R;
-    if (XCDP && P % 8 == 0) {
-        const u64 g = blockIdx.x & 7, i = blockIdx.x >> 3;
-        tb = (g + 8 - ((P + 1) & 7)) & 7;  // copier of tile t is block P + 1 + t
-        ts = 8;
-        j0 = (i * 4 + wave) * R;
-        jstep = (u64)(P / 8) * 4 * R;
-    }
-    for (u64 j = j0; tb + ts * j < tlim; j += jstep) {
+    for (u64 j = ((u64)blockIdx.x * 4 + wave) * R; j < ntiles; j += (u64)P * 4 * R) {
         u64 th[R];
 #pragma unroll
-        for (int h = 0; h < R; ++h) {
-            th[h] = tb + ts * (j + h);
-            if (th[h] >= tlim) th[h] = ntiles;  // past the parsers' range: skipped
-        }
-        const u64 t0 = th[0];
-        if constexpr (PACE > 0) {
-            if (t0 >= (u64)PACE) {
-                u64* w = &pw[t0 - PACE];
-                for (const u64 ts0 = now_ticks(); !tagged(load_word(w), epoch) && now_ticks() - ts0 <= kFallbackTicks;)
-                    __builtin_amdgcn_s_sleep(8);
-            }
-        }
+        for (int h = 0; h < R; ++h) th[h] = j + h < ntiles ? j + h : ntiles;  // past the end: skipped
         if (SPEC && NF == 0 && !held) parse_tiles_spec<NV, MIX, R>(p, aw, ntiles, epoch, th);
-        else parse_tiles<NF, NV, MIX, R, WB, LIGHT>(p, aw, ntiles, epoch, th);
+        else parse_tiles<NF, NV, MIX, R, WB>(p, aw, ntiles, epoch, th);
     }
 }
 
 // ---------------------------------------------------------------- scanner role: pipe_words.hpp scanner()
-constexpr int kScanPerG = 2;  // the gather copier's scanner: tiles per thread per step
 constexpr int kScanPer = 2;   // the pipeline's scanner: tiles per thread per step (512-tile steps)
 
 // ---------------------------------------------------------------- look-back (the fallback)
@@ -354,6 +323,54 @@ __device__ void lookback(const DecodeParams& p, u64* aw, u64* pw, u64 ntiles, u6
     lookback_with<NV>(aw, pw, ntiles, tile, epoch, pre, [&](u64 t, u64 (&a)[NV]) { tile_agg_global<NF, NV, MIX>(p, t, a); });
 }
 
+// ---------------------------------------------------------------- Go's parse of one record
+// kv.syn.go:681-745 (echo.syn.go:186-263 for int32 fields) on a record of L bytes read through
+// rd8 / rd32 (lane = record): status, int32 fields, each string field's length and position.
+template <int NF, int NV, typename Rd8, typename Rd32>
+__device__ __forceinline__ void exact_parse(bool live, u64 L, int nvr, Rd8&& rd8, Rd32&& rd32, u32& st,
+                                            int32_t (&fx)[NF > 0 ? NF : 1], u64 (&flen)[NV], u64 (&fpos)[NV]) {
+    st = 0;
+#pragma unroll
+    for (int f = 0; f < NV; ++f) flen[f] = fpos[f] = 0;
+    if (!live) return;
+    if (L < 13) {
+        st = SYM_STATUS_TOO_SHORT;  // "invalid data: too short" (kv.syn.go:681-683)
+    } else if (rd8(0) != 0x01) {
+        st = SYM_STATUS_BAD_VERSION;  // "invalid data: wrong public version" (:686-688)
+    } else {
+        const u64 off2p = rd32(1);
+        if (off2p >= L || rd8(off2p) != 0x01) {
+            st = SYM_STATUS_NO_PRIVATE;  // "missing private segment" (:696-698)
+        } else {
+            const u64 pts = off2p + 1;
+            u64 toff = 0;
+#pragma unroll
+            for (int f = 0; f < NF; ++f, toff += 4) {  // echo.syn.go:223-231
+                if (st == 0) {
+                    if (L < pts + toff + 4) st = SYM_STATUS_FIELD_TOO_SHORT;
+                    else fx[f] = (int32_t)rd32(pts + toff);
+                }
+            }
+            if (st == 0) {
+#pragma unroll
+                for (int f = 0; f < NV; ++f, toff += 4) {  // kv.syn.go:717-742
+                    if (f < nvr && L >= pts + toff + 4) {
+                        u64 q = rd32(pts + toff);
+                        if (q > 0) q += off2p;
+                        if (q > 0 && L >= q + 4) {
+                            const u64 nb = rd32(q);
+                            if (L >= q + 4 + nb) {
+                                flen[f] = nb;
+                                fpos[f] = q + 4;
+                            }
+                        }
+                    }
+                }
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------- the copier
 // Tile `tile`: stage, parse (wave 0), prefix, copy.  forced: no parsers / scanner in this launch, so
 // the prefix comes from look-back at once.  SPEC: the parsers published speculative aggregates
@@ -361,7 +378,7 @@ __device__ void lookback(const DecodeParams& p, u64* aw, u64* pw, u64 ntiles, u6
 // bytes and tags ctrl[kCtrlMismatch] on any difference (the gate then decodes the batch again), and
 // a capacity error is tagged in ctrl[kCtrlSpecErr] (it may come from a speculative prefix), merged
 // into p.err by the gate when the speculation held.
-template <int NF, int NV, bool MIX, int MODE, int DIAG, int STG, bool EARLY, int AHEAD, int NOP, bool SPEC, int UK = kU>
+template <int NF, int NV, bool MIX, int MODE, int DIAG, int STG, bool SPEC, int UK = kU, bool FAST = false>
 __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 epoch, u64 tile, bool forced, Lds<NV, STG>& S) {
     constexpr int kLoads = (STG / 16 + kThreads - 1) / kThreads;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -385,13 +402,15 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
     const uintptr_t stop = min((in + s1 + 15) & ~(uintptr_t)15, in_end16);
     const int nst = (int)min((u64)STG, (u64)(stop > base ? stop - base : 0));  // multiple of 16
 
-    // ---- 1. stage (and wave 0's record offsets, and with EARLY its prefix words) ----
-    u64 start = 0, endv = 0, wv_early = 0;
+    // ---- 1. stage (and wave 0's record offsets) ----
+    u64 start = 0, endv = 0;
     const bool held = SPEC && spec_held(p);  // loaded beside the stage, used after the parse
+    // FAST: the copy takes the speculative field positions (the generator's layout, spec_flen) right
+    // after the stage, and wave 0 runs Go's exact parse as the check WHILE waves 1-3 copy
+    const bool fast = FAST && SPEC && NF == 0 && !held;
     if (wave == 0) {
         start = p.rec_off[r0 + min(lane, cnt)];
         endv = p.rec_off[r0 + min(lane + 1, cnt)];
-        if (EARLY && MODE == 0 && lane < NV) wv_early = load_word(&pw[(size_t)lane * ntiles + tile]);
     }
     {
         u32x4 sv[kLoads];
@@ -409,82 +428,40 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
     lds_barrier();
     stamp(1);
 
-    // ---- 2. parse + 3. prefix (wave 0); with AHEAD, wave 1 parses tile + AHEAD meanwhile ----
-    if constexpr (AHEAD > 0) {
-        if (wave == 1 && !forced && tile + AHEAD < ntiles) {
-            const u64 ta[1] = {tile + AHEAD};
-            parse_tiles<NF, NV, MIX, 1, 32>(p, aw, ntiles, epoch, ta);
-        }
-    }
+    // ---- 2. parse + 3. prefix (wave 0) ----
+    // wave 0, lane = record: its bytes from the stage (past the stage, from HBM)
+    const bool live = lane < cnt;
+    const u64 L = endv - start;
+    const uintptr_t A = in + start;
+    auto rd8 = [&](u64 q) -> u32 {
+        const u64 a = (u64)(A - base) + q;
+        return a < (u64)nst ? (u32)S.stage[a] : ld_u8(A + q);
+    };
+    auto rd32 = [&](u64 q) -> u32 {
+        const u64 a = (u64)(A - base) + q;
+        return a + 4 <= (u64)nst ? *(const u32*)&S.stage[a] : *(gc_u32*)(A + q);  // unaligned OK
+    };
+    const int nvr = rec_nvar<NV, MIX>(p, live ? r0 + lane : 0);
+    u64 flen[NV], fpos[NV];  // (wave 0; fast: the speculative ones, kept for the check)
     if (wave == 0) {
-        const bool live = lane < cnt;
-        const u64 L = endv - start;
-        const uintptr_t A = in + start;
-        auto rd8 = [&](u64 q) -> u32 {
-            const u64 a = (u64)(A - base) + q;
-            return a < (u64)nst ? (u32)S.stage[a] : ld_u8(A + q);
-        };
-        auto rd32 = [&](u64 q) -> u32 {
-            const u64 a = (u64)(A - base) + q;
-            return a + 4 <= (u64)nst ? *(const u32*)&S.stage[a] : *(gc_u32*)(A + q);  // unaligned OK
-        };
         u32 st = 0;
         int32_t fx[NF > 0 ? NF : 1] = {};
-        u64 flen[NV], fpos[NV];
+        if (fast) {  // the generator's layout: fields back to back after the table (spec_flen)
+            const u32 k0 = live && nvr == 2 && L >= 30 ? rd32(22) : 0u;
+            spec_flen<NV>(live ? L : 0, nvr, k0, flen);
+            fpos[0] = nvr == 2 ? 26 : 22;
+            if constexpr (NV == 2) fpos[1] = 30 + (u64)k0;
+            if (live) p.status[r0 + lane] = 0;  // (no int32 columns: NF == 0)
+        } else {
+            exact_parse<NF, NV>(live, L, nvr, rd8, rd32, st, fx, flen, fpos);
+            if (live) {
+                p.status[r0 + lane] = (uint8_t)st;
 #pragma unroll
-        for (int f = 0; f < NV; ++f) flen[f] = fpos[f] = 0;
-        const int nvr = rec_nvar<NV, MIX>(p, live ? r0 + lane : 0);
-        if (NOP && live) {  // timing only: the config-2 SetRequest layout assumed, no LDS reads
-            flen[0] = 64;
-            fpos[0] = 26;
-            if constexpr (NV == 2) {
-                flen[1] = L - 94;
-                fpos[1] = 94;
+                for (int f = 0; f < NF; ++f) p.fixed[f][r0 + lane] = fx[f];
             }
-            p.status[r0 + lane] = 0;
-        } else if (live) {
-            if (L < 13) {
-                st = SYM_STATUS_TOO_SHORT;  // "invalid data: too short" (kv.syn.go:681-683)
-            } else if (rd8(0) != 0x01) {
-                st = SYM_STATUS_BAD_VERSION;  // "invalid data: wrong public version" (:686-688)
-            } else {
-                const u64 off2p = rd32(1);
-                if (off2p >= L || rd8(off2p) != 0x01) {
-                    st = SYM_STATUS_NO_PRIVATE;  // "missing private segment" (:696-698)
-                } else {
-                    const u64 pts = off2p + 1;
-                    u64 toff = 0;
-#pragma unroll
-                    for (int f = 0; f < NF; ++f, toff += 4) {  // echo.syn.go:223-231
-                        if (st == 0) {
-                            if (L < pts + toff + 4) st = SYM_STATUS_FIELD_TOO_SHORT;
-                            else fx[f] = (int32_t)rd32(pts + toff);
-                        }
-                    }
-                    if (st == 0) {
-#pragma unroll
-                        for (int f = 0; f < NV; ++f, toff += 4) {  // kv.syn.go:717-742
-                            if (f < nvr && L >= pts + toff + 4) {
-                                u64 q = rd32(pts + toff);
-                                if (q > 0) q += off2p;
-                                if (q > 0 && L >= q + 4) {
-                                    const u64 nb = rd32(q);
-                                    if (L >= q + 4 + nb) {
-                                        flen[f] = nb;
-                                        fpos[f] = q + 4;
-                                    }
-                                }
-                            }
-                        }
-                    }
-                }
-            }
-            p.status[r0 + lane] = (uint8_t)st;
-#pragma unroll
-            for (int f = 0; f < NF; ++f) p.fixed[f][r0 + lane] = fx[f];
         }
         u64* const ctrl = ctrl_words(flags, NV, ntiles);
-        if (SPEC && !held) {  // the parsers' speculative lengths of these records, from the same bytes
+        if (SPEC && !held && !fast) {  // the parsers' speculative lengths of these records, from the same bytes
             const u32 k0 = live && nvr == 2 && L >= 30 ? rd32(22) : 0u;
             u64 sf[NV];
             spec_flen<NV>(live ? L : 0, nvr, k0, sf);
@@ -519,7 +496,7 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
                 // this tile's aggregate (a parser may have published the same value), then its prefix
                 store_word(&aw[(size_t)lane * ntiles + tile], make_word(epoch, kStAgg, lane == 0 ? agg[0] : agg[NV - 1]));
                 u64* a = &pw[(size_t)lane * ntiles + tile];
-                wv = EARLY && tagged(wv_early, epoch) ? wv_early : load_word(a);
+                wv = load_word(a);
                 if (!forced) {
                     for (const u64 t0 = now_ticks(); !tagged(wv, epoch) && now_ticks() - t0 <= kFallbackTicks;) {
                         __builtin_amdgcn_s_sleep(2);
@@ -538,8 +515,6 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
                 if constexpr (NV == 2) pre[1] = (i64)((u64)__shfl((long long)wv, 1, 64) & kValMask);
             }
         } else {  // timing only: spread the tiles over the columns in proportion to their stream offset
-            if ((MODE == 2 || MODE == 3) && lane < NV)
-                store_word(&aw[(size_t)lane * ntiles + tile], make_word(epoch, kStAgg, lane == 0 ? agg[0] : agg[NV - 1]));
             const double frac = (double)(s0 - p.rec_off[0]) / (double)(p.rec_off[n] - p.rec_off[0] + 1);
 #pragma unroll
             for (int f = 0; f < NV; ++f) pre[f] = (i64)(frac * (double)p.cap[f]);
@@ -574,13 +549,29 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
     }
     lds_barrier();
 
-    // ---- 4. copy (all lanes) ----
+    if (fast && wave == 0) {  // the check: Go's exact parse of the staged records, while waves 1-3 copy
+        u32 st;
+        int32_t fx[NF > 0 ? NF : 1] = {};
+        u64 elen[NV], epos[NV];
+        exact_parse<NF, NV>(live, L, nvr, rd8, rd32, st, fx, elen, epos);
+        bool mm = live && st != 0;  // (the copy wrote status 0)
+#pragma unroll
+        for (int f = 0; f < NV; ++f) mm |= elen[f] != flen[f] || (flen[f] > 0 && epos[f] != fpos[f]);
+        u64* const ctrl = ctrl_words(flags, NV, ntiles);
+        if (__ballot(mm) && lane == 0 && !tagged(load_word(&ctrl[kCtrlMismatch]), epoch))
+            store_word(&ctrl[kCtrlMismatch], make_word(epoch, kStAgg, 1));
+        return;
+    }
+
+    // ---- 4. copy (all lanes; fast: waves 1-3) ----
+    const int nct = fast ? kThreads - 64 : kThreads;  // copy threads
+    const int ctid = fast ? tid - 64 : tid;
     const int T = __builtin_amdgcn_readfirstlane(S.total);
     // per-column values as named scalars: a two-element array indexed by a lane value goes to scratch
     const i64 pre0 = uniform_i64(S.pre[0]), pre1 = uniform_i64(S.pre[NV - 1]);
     const i64 lim0 = uniform_i64(S.lim[0]), lim1 = uniform_i64(S.lim[NV - 1]);
     const uintptr_t stage_end = base + (uintptr_t)nst;
-    for (int c0 = 0; c0 < T; c0 += kThreads * UK) {  // uniform loop
+    for (int c0 = 0; c0 < T; c0 += nct * UK) {  // uniform loop
         u32x4 v[UK];
         int P_[UK], code[UK];
         uintptr_t X[UK];
@@ -588,7 +579,7 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
         bool anyg = false;
 #pragma unroll
         for (int u = 0; u < UK; ++u) {
-            const int c = c0 + kThreads * u + tid;
+            const int c = c0 + nct * u + ctid;
             const bool has = c < T;
             const int k = has ? lds_search_64(S.cs, cnt, c) : 0;
             int q = c - S.cs[k];
@@ -645,43 +636,48 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
 }
 
 // ---------------------------------------------------------------- the kernel
-// MODE 0: the pipeline.  MODE 1: copiers only, every prefix taken as 0 (timing of the data movement
-// alone; wrong output -- tools/kbench.py variant 402).  DIAG: per-tile phase timestamps into p.dbg
-// (8 u64 per tile, s_memrealtime at 100 MHz; tools/fused_timeline.py).
-// STG: staged bytes per tile (LDS: 24.7 KB at kStage -> 6 copiers per CU; below ~21 KB -> 7).
-// EARLY: the prefix word is loaded when the tile starts, so its cross-XCD round trip overlaps the
-// stage instead of following the parse.  PACE, XCDP: see parser().
-// AHEAD > 0: the parsers take only tiles [0, AHEAD); the copier of tile t parses tile t + AHEAD
-// (wave 1, while wave 0 parses its own tile from LDS) -- the same XCD under round-robin placement
-// when AHEAD % 8 == 0, so the header lines it reads are still in that XCD's L2 when tile t + AHEAD
-// is staged, and the stream is fetched from HBM about once.
-template <int NF, int NV, bool MIX, int MODE = 0, int DIAG = 0, int SK = 4, int PR = 2, int STG = kStage,
-          bool EARLY = false, int PACE = 0, bool XCDP = false, int AHEAD = 0, int NOP = 0, bool SPEC = false, int SPECX = 0,
-          int WPE = 6, int UK = kU>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void decode_pipe_kernel(
+// The launch geometry and the measurement modes, one value per decode_pipe_kernel instantiation.
+struct PipeCfg {
+    int mode = 0;       // 0 the pipeline; 1 copiers only, every prefix taken as 0 (the data movement
+                        // alone: a timing bound with WRONG output, tools/kbench.py variant 402)
+    int diag = 0;       // 1: per-tile phase timestamps into p.dbg (8 u64 per tile, s_memrealtime at
+                        // 100 MHz; tools/fused_timeline.py)
+    int sk = kScanPer;  // scanner tiles per thread per step
+    int pr = 2;         // parser tiles per wave step
+    int stg = kStage;   // staged bytes per tile (LDS: 24.7 KB at kStage -> 6 copiers per CU)
+    bool spec = false;  // speculative parsers for kv layouts, the copiers' check and the gate
+    int specx = 0;      // timing only: 1 speculation without check or gate, 2 without gate (both
+                        // WRONG on misfit records), 3 the gate on one workgroup per CU
+    int wpe = 6;        // waves per SIMD the kernel is built for (8 needs <= 64 VGPRs and ~20 KB LDS)
+    int uk = kU;        // copy chunks per lane per step
+    bool fast = false;  // the copy takes the speculative positions; wave 0 checks them meanwhile
+};
+
+template <int NF, int NV, bool MIX, PipeCfg C>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(C.wpe, 8))) void decode_pipe_kernel(
     DecodeParams p, u64* flags, u32 epoch) {
     static_assert(NV == 1 || NV == 2, "decode handles one or two string columns");
-    __shared__ Lds<NV, STG> S;
+    static_assert(C.mode == 0 || C.mode == 1, "pipeline or copiers only");
+    __shared__ Lds<NV, C.stg> S;
     const u64 ntiles = num_tiles(p.n);
     u64* aw = flags;                        // aggregate words [NV][ntiles]
     u64* pw = flags + (size_t)NV * ntiles;  // prefix words [NV][ntiles]
 
     const u32 P = p.pipe_parsers;
     const bool forced = p.impl == kImplLookback;  // parsers and scanner idle: look-back only
-    // MODE 2 / 3 (timing): roles run, copiers never wait; 3: parsers read only the offsets
-    constexpr bool kRoles = MODE == 0 || MODE == 2 || MODE == 3;
+    constexpr bool kRoles = C.mode == 0;
     if (kRoles && blockIdx.x < P) {
-        if (!forced)
-            parser<NF, NV, MIX, PR, 32, MODE == 3, PACE, XCDP, SPEC>(p, aw, pw, ntiles, epoch, P, AHEAD > 0 ? (u64)AHEAD : ~0ull);
+        if (!forced) parser<NF, NV, MIX, C.pr, 32, C.spec>(p, aw, ntiles, epoch, P);
         return;
     }
     if (kRoles && blockIdx.x == P) {
-        if (!forced) scanner<NV, SK>(aw, pw, ntiles, epoch, S);
+        if (!forced) scanner<NV, C.sk>(aw, pw, ntiles, epoch, S);
         return;
     }
     const u64 tile = kRoles ? blockIdx.x - P - 1 : blockIdx.x;
     if (tile >= ntiles) return;
-    copier<NF, NV, MIX, MODE, DIAG, STG, EARLY, AHEAD, NOP, SPEC && MODE == 0 && SPECX != 1, UK>(p, flags, epoch, tile, forced, S);
+    copier<NF, NV, MIX, C.mode, C.diag, C.stg, C.spec && C.mode == 0 && C.specx != 1, C.uk, C.fast>(p, flags, epoch, tile,
+                                                                                                    forced, S);
 }
 
 // ---------------------------------------------------------------- the gate
@@ -711,7 +707,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
     u64* pw = flags + (size_t)NV * ntiles;
     const u32 G = gridDim.x, P = G >= 8 ? G / 4 : 0;
     if (blockIdx.x < P) {
-        parser<NF, NV, MIX, 2, 32>(p, aw, pw, ntiles, epoch + 1, P);
+        parser<NF, NV, MIX, 2, 32>(p, aw, ntiles, epoch + 1, P);
         return;
     }
     if (P && blockIdx.x == P) {
@@ -720,307 +716,14 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
     }
     const u32 c0 = P ? P + 1 : 0;
     for (u64 tile = blockIdx.x - c0; tile < ntiles; tile += G - c0) {
-        copier<NF, NV, MIX, 0, 0, kStage, false, 0, 0, false>(p, flags, epoch + 1, tile, P == 0, S);
+        copier<NF, NV, MIX, 0, 0, kStage, false>(p, flags, epoch + 1, tile, P == 0, S);
         lds_barrier();  // the next tile restages S
     }
 }
 
-// ---------------------------------------------------------------- the gather copier
-// A copier without the LDS stage.  Wave 0 parses its 64 records straight from HBM through a 96-byte
-// register window per record -- the lines the copy reads next, so they are fetched once -- runs Go's
-// checks, publishes the tile's aggregate and takes its prefix as the staged copier does.  Then all
-// four waves write the tile's column ranges output-stationary, as encode_kernel writes records: lane
-// = aligned 16-byte output chunk, assembled from byte-unaligned 16-byte loads of the one or two
-// fields it covers (more only under fields shorter than 16 bytes) under byte masks, one
-// global_store_dwordx4 per chunk (byte stores only at a range's two edges).  kGU chunks per lane per
-// step, every load of the step issued before its stores.  LDS holds only the field tables (~2 KB),
-// so a CU keeps up to 8 copiers resident instead of 6.
-constexpr int kGWin = 96;  // parse window bytes per record
-constexpr int kGU = 4;     // output chunks per lane per step
-
-
-template <int NV>
-struct GatherLds {
-    u64 addr[NV][kRecs];   // the tile's non-empty fields, compacted: source address
-    int o[NV][kRecs + 1];  // output start inside the tile's column range; [nl] = the range length
-    i64 pre[NV];           // the range's start in the column
-    int hi[NV];            // bytes of the range to write (the capacity may cut it)
-    int nl[NV];
-    int nch[NV];           // output chunks of the range
-    int first[NV];         // the first chunk's start relative to the range, in (-16, 0]
-    int safe;              // every 16-byte window of the tile lies inside the stream's readable extent
-    int skip;              // a range of 2 GiB or more (reported): nothing is written
-};
-
-template <int NF, int NV, bool MIX, int MODE = 0>
-__global__ __launch_bounds__(kThreads) void decode_gather_kernel(DecodeParams p, u64* flags, u32 epoch) {
-    static_assert(NV == 1 || NV == 2, "decode handles one or two string columns");
-    constexpr int NW = kGWin / 4;
-    __shared__ GatherLds<NV> S;
-    __shared__ ScanLds SL;
-    __shared__ MaskTable masks;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const u64 n = p.n, ntiles = num_tiles(n);
-    const uintptr_t in = (uintptr_t)p.in;
-    const uintptr_t in_lo = in + p.rec_off[0];
-    const uintptr_t in_end16 = (in + p.rec_off[n] + 15) & ~(uintptr_t)15;  // readable limit (ABI rule)
-    u64* aw = flags;
-    u64* pw = flags + (size_t)NV * ntiles;
-    const u32 P = p.pipe_parsers;
-    const bool forced = p.impl == kImplLookback;
-    if (blockIdx.x < P) {
-        if (!forced) parser<NF, NV, MIX, 2, 32>(p, aw, pw, ntiles, epoch, P);
-        return;
-    }
-    if (blockIdx.x == P) {
-        if (!forced) scanner<NV, kScanPerG>(aw, pw, ntiles, epoch, SL);
-        return;
-    }
-    const u64 tile = blockIdx.x - P - 1;
-    if (tile >= ntiles) return;
-    mask_table_init(masks, tid);
-    const u64 r0 = tile * kRecs;
-    const int cnt = (int)min((u64)kRecs, n - r0);
-
-    // ---- 1. parse from HBM (wave 0, lane = record), prefix, tables ----
-    if (wave == 0) {
-        const bool live = lane < cnt;
-        const u64 start = p.rec_off[r0 + min(lane, cnt)];
-        const u64 L = p.rec_off[r0 + min(lane + 1, cnt)] - start;
-        const uintptr_t A = in + start;
-        // the window: every 16-byte block that lies inside the readable extent (zero past it)
-        u32 w[NW];
-        const u64 room = in_end16 > A ? (u64)(in_end16 - A) : 0;
-        const int wv = live ? (int)min((u64)kGWin, room) & ~15 : 0;  // window bytes loaded
-#pragma unroll
-        for (int k = 0; k < kGWin / 16; ++k) {
-            const u32x4 a = ld16u(16 * k < wv ? A + 16 * k : (uintptr_t)flags);
-            w[4 * k] = a.x;
-            w[4 * k + 1] = a.y;
-            w[4 * k + 2] = a.z;
-            w[4 * k + 3] = a.w;
-        }
-        auto rd8 = [&](u64 q) -> u32 {
-            constexpr u64 M = kGWin - 4;
-            return q < (u64)wv ? (win_u32<NW>(w, (u32)min(q, M)) >> (8 * (q > M ? q - M : 0))) & 0xffu : ld_u8(A + q);
-        };
-        auto rd32 = [&](u64 q) -> u32 {
-            return q + 4 <= (u64)wv ? win_u32<NW>(w, (u32)q) : *(gc_u32*)(A + q);  // unaligned OK
-        };
-        u32 st = 0;
-        int32_t fx[NF > 0 ? NF : 1] = {};
-        u64 flen[NV], fpos[NV];
-#pragma unroll
-        for (int f = 0; f < NV; ++f) flen[f] = fpos[f] = 0;
-        const int nvr = rec_nvar<NV, MIX>(p, live ? r0 + lane : 0);
-        if (live) {  // kv.syn.go:681-745, echo.syn.go:186-263
-            if (L < 13) {
-                st = SYM_STATUS_TOO_SHORT;
-            } else if (rd8(0) != 0x01) {
-                st = SYM_STATUS_BAD_VERSION;
-            } else {
-                const u64 off2p = rd32(1);
-                if (off2p >= L || rd8(off2p) != 0x01) {
-                    st = SYM_STATUS_NO_PRIVATE;
-                } else {
-                    const u64 pts = off2p + 1;
-                    u64 toff = 0;
-#pragma unroll
-                    for (int f = 0; f < NF; ++f, toff += 4) {
-                        if (st == 0) {
-                            if (L < pts + toff + 4) st = SYM_STATUS_FIELD_TOO_SHORT;
-                            else fx[f] = (int32_t)rd32(pts + toff);
-                        }
-                    }
-                    if (st == 0) {
-#pragma unroll
-                        for (int f = 0; f < NV; ++f, toff += 4) {
-                            if (f < nvr && L >= pts + toff + 4) {
-                                u64 q = rd32(pts + toff);
-                                if (q > 0) q += off2p;
-                                if (q > 0 && L >= q + 4) {
-                                    const u64 nb = rd32(q);
-                                    if (L >= q + 4 + nb) {
-                                        flen[f] = nb;
-                                        fpos[f] = q + 4;
-                                    }
-                                }
-                            }
-                        }
-                    }
-                }
-            }
-            p.status[r0 + lane] = (uint8_t)st;
-#pragma unroll
-            for (int f = 0; f < NF; ++f) p.fixed[f][r0 + lane] = fx[f];
-        }
-        u64 agg[NV], excl[NV];
-        bool too_large = false;
-#pragma unroll
-        for (int f = 0; f < NV; ++f) {
-            const u64 inc = wave_incl_scan_u32w_dpp((u32)flen[f]);
-            agg[f] = (u64)__builtin_amdgcn_readlane((u32)inc, 63) |
-                     ((u64)__builtin_amdgcn_readlane((u32)(inc >> 32), 63) << 32);
-            excl[f] = inc - flen[f];
-            too_large |= agg[f] >= ((u64)1 << 31);  // positions inside a tile's range are 32-bit
-        }
-        // the prefix: from the scanner, else (after kFallbackTicks, or forced) by look-back
-        i64 pre[NV];
-        if constexpr (MODE == 0) {
-            u64 wvv = 0;
-            bool got = true;
-            if (lane < NV) {
-                store_word(&aw[(size_t)lane * ntiles + tile], make_word(epoch, kStAgg, lane == 0 ? agg[0] : agg[NV - 1]));
-                u64* a = &pw[(size_t)lane * ntiles + tile];
-                wvv = load_word(a);
-                if (!forced) {
-                    for (const u64 t0 = now_ticks(); !tagged(wvv, epoch) && now_ticks() - t0 <= kFallbackTicks;) {
-                        __builtin_amdgcn_s_sleep(2);
-                        wvv = load_word(a);
-                    }
-                }
-                got = tagged(wvv, epoch);
-            }
-            if (__ballot(!got)) {
-                lookback<NF, NV, MIX>(p, aw, pw, ntiles, tile, epoch, pre);
-#pragma unroll
-                for (int f = 0; f < NV; ++f)
-                    if (lane == 0) store_word(&pw[(size_t)f * ntiles + tile], make_word(epoch, kStPre, (u64)pre[f]));
-            } else {
-                pre[0] = (i64)((u64)__shfl((long long)wvv, 0, 64) & kValMask);
-                if constexpr (NV == 2) pre[1] = (i64)((u64)__shfl((long long)wvv, 1, 64) & kValMask);
-            }
-        } else {  // timing only (wrong output): every prefix in proportion to the stream offset
-            const double frac = (double)(start - p.rec_off[0]) / (double)(p.rec_off[n] - p.rec_off[0] + 1);
-#pragma unroll
-            for (int f = 0; f < NV; ++f) pre[f] = uniform_i64((i64)(__shfl(frac, 0, 64) * (double)p.cap[f]));
-        }
-#pragma unroll
-        for (int f = 0; f < NV; ++f) {
-            if (live) p.offs[f][r0 + lane] = (u64)pre[f] + excl[f];
-            if (lane == 0 && r0 + cnt == n) p.offs[f][n] = (u64)pre[f] + agg[f];
-        }
-        // the tables: non-empty fields compacted, each with its source and its output start
-        bool safe = true;
-#pragma unroll
-        for (int f = 0; f < NV; ++f) {
-            const bool ne = live && flen[f] > 0;
-            const u64 m = __ballot(ne);
-            const int slot = (int)__builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u));
-            const uintptr_t src = A + fpos[f];
-            if (ne) {
-                S.addr[f][slot] = (u64)src;
-                S.o[f][slot] = (int)excl[f];
-                safe = safe && src >= in_lo + 16 && src + flen[f] + 16 <= in_end16 - 16;
-            }
-            if (lane == 0) {
-                const int nl = (int)__popcll(m);
-                S.o[f][nl] = (int)agg[f];
-                S.nl[f] = nl;
-                S.pre[f] = pre[f];
-                const i64 cap = (i64)p.cap[f];
-                if (MODE == 0 && agg[f] > 0 && pre[f] + (i64)agg[f] > cap) atomicOr(p.err, kErrCapacity);
-                S.hi[f] = (int)max((i64)0, min((i64)agg[f], cap - pre[f]));
-                const int first = -(int)(((uintptr_t)p.bytes[f] + (uintptr_t)pre[f]) & 15);
-                S.first[f] = first;
-                S.nch[f] = agg[f] > 0 ? (int)(((i64)agg[f] - first + 15) >> 4) : 0;
-            }
-        }
-        const bool all_safe = __all(safe);
-        if (lane == 0) {
-            S.safe = all_safe;
-            S.skip = __ballot(too_large) != 0;
-            if (too_large) atomicOr(p.err, kErrTooLarge);
-        }
-    }
-    __syncthreads();
-    if (S.skip) return;
-
-    // ---- 2. the column ranges, output-stationary (all lanes) ----
-    const int n0 = S.nch[0];
-    const int ntot = n0 + (NV == 2 ? S.nch[NV - 1] : 0);
-    const bool safe = S.safe != 0;
-    const uintptr_t dummy = (uintptr_t)flags;  // readable; its bytes are masked off
-    for (int c0 = 0; c0 < ntot; c0 += kThreads * kGU) {  // uniform loop
-        u32x4 r[kGU];
-        int Pq[kGU], fq[kGU];
-#pragma unroll
-        for (int u = 0; u < kGU; ++u) {
-            const int c = c0 + kThreads * u + tid;
-            const int f = NV == 2 && c >= n0 ? 1 : 0;
-            fq[u] = c < ntot ? f : -1;
-            const int Pc = S.first[f] + 16 * (c - (f ? n0 : 0));
-            Pq[u] = Pc;
-            r[u] = u32x4{0, 0, 0, 0};
-            if (c >= ntot) continue;
-            const int nl = S.nl[f];
-            const int k0 = lds_search_64(S.o[f], nl, max(Pc, 0));
-            const int o0 = S.o[f][k0], o1 = S.o[f][k0 + 1];
-            const bool two = k0 + 1 < nl && o1 < Pc + 16;  // the next field starts inside this chunk
-            if (safe) {
-                const int o2 = two ? S.o[f][k0 + 2] : o1;
-                const uintptr_t X0 = (uintptr_t)(S.addr[f][k0] + (u64)(i64)(Pc - o0));
-                const uintptr_t X1 = two ? (uintptr_t)(S.addr[f][k0 + 1] + (u64)(i64)(Pc - o1)) : dummy;
-                r[u] = (ld16u(X0) & range_mask(masks, o0 - Pc, o1 - Pc)) |
-                       (ld16u(X1) & range_mask(masks, two ? o1 - Pc : 16, o2 - Pc));
-                for (int k = k0 + 2; two && k < nl && S.o[f][k] < Pc + 16; ++k)  // fields under 16 bytes
-                    r[u] |= ld16u((uintptr_t)(S.addr[f][k] + (u64)(i64)(Pc - S.o[f][k]))) &
-                            range_mask(masks, S.o[f][k] - Pc, S.o[f][k + 1] - Pc);
-            } else {  // batch edges: aligned blocks holding valid bytes only
-                u32 t[4] = {0, 0, 0, 0};
-                for (int k = k0; k < nl && S.o[f][k] < Pc + 16; ++k) {
-                    const int lo = S.o[f][k] - Pc, hi = S.o[f][k + 1] - Pc;
-                    if (hi <= 0) continue;
-                    or_window_global((uintptr_t)(S.addr[f][k] + (u64)(i64)(Pc - S.o[f][k])), max(lo, 0), min(hi, 16), t);
-                }
-                r[u] = u32x4{t[0], t[1], t[2], t[3]};
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < kGU; ++u) {
-            if (fq[u] < 0) continue;
-            const int f = fq[u];
-            const u32 rr[4] = {r[u].x, r[u].y, r[u].z, r[u].w};
-            store_chunk(p.bytes[f] + S.pre[f], Pq[u], 0, S.hi[f], rr);
-        }
-    }
-}
-
-template <int NF, int NV, bool MIX, int MODE>
-hipError_t launch_gather(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stream, int pnum, int pden) {
-    static int cus[16] = {0};
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return e;
-    int& ncu = cus[dev & 15];
-    if (ncu == 0 && (e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
-    const u64 nt = num_tiles(p.n);
-    u64 P = (u64)ncu * pnum / pden;
-    if (P > (nt + 3) / 4) P = (nt + 3) / 4;
-    DecodeParams q = p;
-    q.pipe_parsers = (unsigned)P;
-    hipLaunchKernelGGL((decode_gather_kernel<NF, NV, MIX, MODE>), dim3((unsigned)(P + 1 + nt)), dim3(kThreads), 0,
-                       stream, q, flags, epoch);
-    return hipGetLastError();
-}
-
-template <int MODE>
-hipError_t launch_gather_layout(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stream, int pnum = 3,
-                                int pden = 4) {
-    if (p.type)
-        return p.lay.nfixed == 0 && p.lay.nvar == 2 ? launch_gather<0, 2, true, MODE>(p, flags, epoch, stream, pnum, pden)
-                                                     : hipErrorInvalidValue;
-    if (p.lay.nfixed == 0 && p.lay.nvar == 1) return launch_gather<0, 1, false, MODE>(p, flags, epoch, stream, pnum, pden);
-    if (p.lay.nfixed == 0 && p.lay.nvar == 2) return launch_gather<0, 2, false, MODE>(p, flags, epoch, stream, pnum, pden);
-    if (p.lay.nfixed == 2 && p.lay.nvar == 2) return launch_gather<2, 2, false, MODE>(p, flags, epoch, stream, pnum, pden);
-    return hipErrorInvalidValue;
-}
-
-template <int NF, int NV, bool MIX, int MODE, int DIAG, int SK = 4, int PR = 2, int STG = kStage, bool EARLY = false,
-          int PACE = 0, bool XCDP = false, int AHEAD = 0, int NOP = 0, bool SPEC = false, int SPECX = 0, int WPE = 6,
-          int UK = kU>
+template <int NF, int NV, bool MIX, PipeCfg C>
 hipError_t launch(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stream, int pnum = 1, int pden = 1) {
-    if (DIAG && !p.dbg) return hipErrorInvalidValue;  // timestamps need SYMHIP_DEBUG_PTR (tuning builds)
+    if (C.diag && !p.dbg) return hipErrorInvalidValue;  // timestamps need SYMHIP_DEBUG_PTR (tuning builds)
     static int cus[16] = {0};
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
@@ -1028,56 +731,46 @@ hipError_t launch(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stre
     int& ncu = cus[dev & 15];
     if (ncu == 0 && (e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
     const u64 nt = num_tiles(p.n);
-    constexpr bool kRoles = MODE == 0 || MODE == 2 || MODE == 3;
+    constexpr bool kRoles = C.mode == 0;
     u64 P = kRoles ? (u64)ncu * pnum / pden : 0;  // parser workgroups: pnum / pden per CU
     if (P > (nt + 3) / 4) P = (nt + 3) / 4;
-    if (AHEAD > 0 && P > (u64)(AHEAD + 4 * PR - 1) / (4 * PR)) P = (AHEAD + 4 * PR - 1) / (4 * PR);  // tiles [0, AHEAD)
     DecodeParams q = p;
     q.pipe_parsers = (unsigned)P;
     const u64 grid = kRoles ? P + 1 + nt : nt;
     // speculative parsers: only kv layouts (no int32 fields) under the pipeline with its parsers
-    constexpr bool kSpec = SPEC && NF == 0 && MODE == 0;
+    constexpr bool kSpec = C.spec && NF == 0 && C.mode == 0;
     if constexpr (kSpec) {
         if (p.impl != kImplLookback && P > 0) {
-            hipLaunchKernelGGL((decode_pipe_kernel<NF, NV, MIX, MODE, DIAG, SK, PR, STG, EARLY, PACE, XCDP, AHEAD, NOP, true, SPECX, WPE, UK>),
-                               dim3((unsigned)grid), dim3(kThreads), 0, stream, q, flags, epoch);
+            hipLaunchKernelGGL((decode_pipe_kernel<NF, NV, MIX, C>), dim3((unsigned)grid), dim3(kThreads), 0, stream, q, flags,
+                               epoch);
             if ((e = hipGetLastError()) != hipSuccess) return e;
-            if (SPECX == 1 || SPECX == 2) return hipSuccess;  // timing variants: no gate (WRONG on misfits)
-            // four workgroups per CU (the gate's cost is the launch behind the first kernel, the same
-            // for 1 or 4 per CU); a re-decode is the exact pipeline on them
-            const u64 g = min(nt + 1 + ncu, (u64)ncu * (SPECX == 3 ? 1 : 4));
+            if (C.specx == 1 || C.specx == 2) return hipSuccess;  // timing variants: no gate (WRONG on misfits)
+            // one workgroup per CU (the gate's cost is the launch behind the first kernel); a
+            // re-decode is the exact pipeline on them
+            const u64 g = min(nt + 1 + ncu, (u64)ncu * (C.specx == 3 ? 1 : 4));
             hipLaunchKernelGGL((decode_gate_kernel<NF, NV, MIX>), dim3((unsigned)g), dim3(kThreads), 0, stream, q, flags, epoch);
             return hipGetLastError();
         }
     }
-    hipLaunchKernelGGL((decode_pipe_kernel<NF, NV, MIX, MODE, DIAG, SK, PR, STG, EARLY, PACE, XCDP, AHEAD, NOP, false, 0, WPE, UK>), dim3((unsigned)grid),
-                       dim3(kThreads), 0, stream, q, flags, epoch);
+    constexpr PipeCfg X = [] { PipeCfg c = C; c.spec = false; c.specx = 0; return c; }();
+    hipLaunchKernelGGL((decode_pipe_kernel<NF, NV, MIX, X>), dim3((unsigned)grid), dim3(kThreads), 0, stream, q, flags, epoch);
     return hipGetLastError();
 }
 
 constexpr int kParsersNum = 3;   // parser workgroups = #CUs * 3/4
 constexpr int kParsersDen = 4;
 
-template <int MODE, int DIAG, int SK = kScanPer, int PR = 2, int STG = kStage, bool EARLY = false, int PACE = 0,
-          bool XCDP = false, int AHEAD = 0, int NOP = 0, bool SPEC = false, int SPECX = 0, int WPE = 6, int UK = kU>
+template <PipeCfg C>
 hipError_t launch_layout(const DecodeParams& p, u64* flags, u32 epoch, hipStream_t stream, int pnum = kParsersNum,
                          int pden = kParsersDen) {
-#define SYMHIP_PIPE_LAUNCH(NF, NV, MIX) \
-    launch<NF, NV, MIX, MODE, DIAG, SK, PR, STG, EARLY, PACE, XCDP, AHEAD, NOP, SPEC, SPECX, WPE, UK>(p, flags, epoch, stream, pnum, pden)
     if (p.type)  // mixed kv batch: GetRequest / SetRequest per record
-        return p.lay.nfixed == 0 && p.lay.nvar == 2 ? SYMHIP_PIPE_LAUNCH(0, 2, true) : hipErrorInvalidValue;
-    if (p.lay.nfixed == 0 && p.lay.nvar == 1) return SYMHIP_PIPE_LAUNCH(0, 1, false);
-    if (p.lay.nfixed == 0 && p.lay.nvar == 2) return SYMHIP_PIPE_LAUNCH(0, 2, false);
-    if (p.lay.nfixed == 2 && p.lay.nvar == 2) return SYMHIP_PIPE_LAUNCH(2, 2, false);
-#undef SYMHIP_PIPE_LAUNCH
+        return p.lay.nfixed == 0 && p.lay.nvar == 2 ? launch<0, 2, true, C>(p, flags, epoch, stream, pnum, pden)
+                                                     : hipErrorInvalidValue;
+    if (p.lay.nfixed == 0 && p.lay.nvar == 1) return launch<0, 1, false, C>(p, flags, epoch, stream, pnum, pden);
+    if (p.lay.nfixed == 0 && p.lay.nvar == 2) return launch<0, 2, false, C>(p, flags, epoch, stream, pnum, pden);
+    if (p.lay.nfixed == 2 && p.lay.nvar == 2) return launch<2, 2, false, C>(p, flags, epoch, stream, pnum, pden);
     return hipErrorInvalidValue;
 }
-
-#ifdef SYMHIP_TUNING
-// The persistent "ring" decode (tuning variants 500-512): an experiment measured against the pipeline
-// above (decode section).
-#include "decode_ring.inc"
-#endif
 
 }  // namespace pipe
 
@@ -1088,115 +781,66 @@ size_t decode_pipe_flag_bytes(int nvar, uint64_t n) {
     return ((size_t)nvar * 2 * pipe::num_tiles(n) * sizeof(u64) + 512 + 255) & ~(size_t)255;
 }
 
-// The pipeline: 512-tile scanner steps, parsers on 3/4 of the CUs (tools/kbench.py sweep).
-// Tuning builds (make tuning) add the measurement variants: 402 data movement only (copiers without
-// the scan: WRONG output, a timing bound), 410 / 412 per-tile timestamps, 43x-46x geometry sweeps.
+// The default: speculative kv decodes with parsers on half the CUs and 256-tile scanner steps;
+// exact parsers (int32 fields) on 3/4 of the CUs with 512-tile steps (tools/kbench.py sweeps,
+// DESIGN.md section 4).  Tuning builds (make tuning) add the measurement variants below; the decode
+// experiments of rounds 1-3 that were not adopted (parse geometry sweeps 431-492, the gather copier
+// 600-603, copier parse-ahead 620-624, parse-free copiers 700-702, early prefix loads and 20992-byte
+// stages 720-728, the persistent ring 500-512) were retired in round 4 with their numbers recorded
+// in DESIGN.md; their code is in the history before that commit.
+namespace pipe {
+constexpr PipeCfg kSpecCfg{.sk = 1, .spec = true};   // kv layouts
+constexpr PipeCfg kExactCfg{.spec = true};          // int32 layouts (exact parsers: spec needs NF == 0)
+}  // namespace pipe
+
 hipError_t launch_decode_pipe(const DecodeParams& p, void* flags, unsigned epoch, hipStream_t stream) {
+    using pipe::launch_layout;
+    using pipe::PipeCfg;
     u64* fl = (u64*)flags;
 #ifdef SYMHIP_TUNING
     switch (p.variant) {
-        case 402: return pipe::launch_layout<1, 0>(p, fl, epoch, stream);
-        case 410: return pipe::launch_layout<0, 1>(p, fl, epoch, stream);
-        case 412: return pipe::launch_layout<1, 1>(p, fl, epoch, stream);
-        case 431: return pipe::launch_layout<0, 0>(p, fl, epoch, stream, 1, 2);
-        case 432: return pipe::launch_layout<0, 0>(p, fl, epoch, stream, 2, 1);
-        case 433: return pipe::launch_layout<0, 0>(p, fl, epoch, stream, 1, 4);
-        case 434: return pipe::launch_layout<0, 0>(p, fl, epoch, stream, 3, 2);
-        case 440: return pipe::launch_layout<0, 0, 8>(p, fl, epoch, stream);
-        case 443: return pipe::launch_layout<0, 0, 1>(p, fl, epoch, stream);
-        case 446: return pipe::launch_layout<0, 0, 3>(p, fl, epoch, stream);
-        case 447: return pipe::launch_layout<0, 0, 2>(p, fl, epoch, stream, 5, 8);
-        case 449: return pipe::launch_layout<0, 0, 2>(p, fl, epoch, stream, 11, 16);
-        case 460: return pipe::launch_layout<0, 0, 2, 1>(p, fl, epoch, stream);
-        case 461: return pipe::launch_layout<0, 0, 2, 4>(p, fl, epoch, stream);
-        // round 2: early prefix load, 7 copiers per CU (20992-byte stage), both
-        case 470: return pipe::launch_layout<0, 0, 2, 2, pipe::kStage, true>(p, fl, epoch, stream);
-        case 471: return pipe::launch_layout<0, 0, 2, 2, 20992, false>(p, fl, epoch, stream);
-        case 472: return pipe::launch_layout<0, 0, 2, 2, 20992, true>(p, fl, epoch, stream);
-        case 473: return pipe::launch_layout<0, 0, 2, 2, 20992, true>(p, fl, epoch, stream, 1, 2);
-        case 474: return pipe::launch_layout<0, 0, 2, 2, 20992, true>(p, fl, epoch, stream, 1, 1);
-        case 475: return pipe::launch_layout<1, 0, 2, 2, 20992, false>(p, fl, epoch, stream);
-        case 476: return pipe::launch_layout<2, 0>(p, fl, epoch, stream);  // roles run, no waits (WRONG output)
-        case 477: return pipe::launch_layout<0, 0>(p, fl, epoch, stream, 0, 1);  // no parsers
-        case 478: return pipe::launch_layout<0, 0>(p, fl, epoch, stream, 1, 8);
-        case 479: return pipe::launch_layout<0, 0>(p, fl, epoch, stream, 1, 4);
-        case 480: return pipe::launch_layout<0, 0>(p, fl, epoch, stream, 1, 2);
-        case 481: return pipe::launch_layout<0, 0, 2, 1>(p, fl, epoch, stream);
-        case 482: return pipe::launch_layout<2, 0>(p, fl, epoch, stream, 0, 1);  // scanner only, no waits
-        case 483: return pipe::launch_layout<3, 0>(p, fl, epoch, stream);  // parsers read offsets only, no waits
-        case 484: return pipe::launch_layout<0, 0, 2, 2, pipe::kStage, false, 2048>(p, fl, epoch, stream);
-        case 485: return pipe::launch_layout<0, 0, 2, 2, pipe::kStage, false, 4096>(p, fl, epoch, stream);
-        case 486: return pipe::launch_layout<0, 0, 2, 2, pipe::kStage, false, 8192>(p, fl, epoch, stream);
-        case 487: return pipe::launch_layout<0, 0, 2, 2, pipe::kStage, false, 4096>(p, fl, epoch, stream, 1, 2);
-        case 488: return pipe::launch_layout<0, 0, 2, 2, pipe::kStage, false, 0, true>(p, fl, epoch, stream);
-        case 489: return pipe::launch_layout<0, 0, 2, 2, pipe::kStage, false, 512, true>(p, fl, epoch, stream);
-        case 490: return pipe::launch_layout<0, 0, 2, 2, pipe::kStage, false, 1024, true>(p, fl, epoch, stream);
-        case 491: return pipe::launch_layout<0, 0, 2, 2, pipe::kStage, false, 2048, true>(p, fl, epoch, stream);
-        case 492: return pipe::launch_layout<2, 0, 2, 2, pipe::kStage, false, 0, true>(p, fl, epoch, stream);
-        // copiers parse ahead (AHEAD tiles; the parsers take only the first AHEAD tiles)
-        case 620: return pipe::launch_layout<0, 0, 2, 2, pipe::kStage, false, 0, false, 256>(p, fl, epoch, stream);
-        case 621: return pipe::launch_layout<0, 0, 2, 2, pipe::kStage, false, 0, false, 512>(p, fl, epoch, stream);
-        case 622: return pipe::launch_layout<0, 0, 2, 2, pipe::kStage, false, 0, false, 1024>(p, fl, epoch, stream);
-        case 623: return pipe::launch_layout<0, 0, 2, 2, pipe::kStage, false, 0, false, 2048>(p, fl, epoch, stream);
-        case 624: return pipe::launch_layout<0, 0, 2, 2, pipe::kStage, false, 0, false, 4096>(p, fl, epoch, stream);
-        // round 3: the copier's parse replaced by the config-2 layout (timing bound of a parse-free copier)
-        case 700: return pipe::launch_layout<0, 0, 2, 2, pipe::kStage, false, 0, false, 0, 1>(p, fl, epoch, stream);
-        case 701: return pipe::launch_layout<1, 0, 2, 2, pipe::kStage, false, 0, false, 0, 1>(p, fl, epoch, stream);
-        case 702: return pipe::launch_layout<2, 0, 2, 2, pipe::kStage, false, 0, false, 0, 1>(p, fl, epoch, stream);
-        // round 3: exact parsers (no speculation, no gate): the round-2 default
-        case 710: return pipe::launch_layout<0, 0>(p, fl, epoch, stream);
+        // timing bounds and timelines: copiers only (WRONG output), per-tile timestamps
+        case 402: return launch_layout<PipeCfg{.mode = 1}>(p, fl, epoch, stream);
+        case 410: return launch_layout<PipeCfg{.diag = 1}>(p, fl, epoch, stream);
+        case 412: return launch_layout<PipeCfg{.mode = 1, .diag = 1}>(p, fl, epoch, stream);
+        // exact parsers (no speculation, no gate): the round-2 default
+        case 710: return launch_layout<PipeCfg{}>(p, fl, epoch, stream);
         // speculation without the copiers' check and the gate / with the check, no gate / gate on one
         // workgroup per CU (711 and 712 are WRONG on batches the speculation misses)
-        case 711: return pipe::launch_layout<0, 0, pipe::kScanPer, 2, pipe::kStage, false, 0, false, 0, 0, true, 1>(p, fl, epoch, stream);
-        case 712: return pipe::launch_layout<0, 0, pipe::kScanPer, 2, pipe::kStage, false, 0, false, 0, 0, true, 2>(p, fl, epoch, stream);
-        case 713: return pipe::launch_layout<0, 0, pipe::kScanPer, 2, pipe::kStage, false, 0, false, 0, 0, true, 3>(p, fl, epoch, stream);
-        // round 3: the speculative default with an early prefix load and / or a 20992-byte stage
-        case 720: return pipe::launch_layout<0, 0, pipe::kScanPer, 2, pipe::kStage, true, 0, false, 0, 0, true>(p, fl, epoch, stream);
-        case 721: return pipe::launch_layout<0, 0, pipe::kScanPer, 2, 20992, true, 0, false, 0, 0, true>(p, fl, epoch, stream);
-        case 722: return pipe::launch_layout<0, 0, pipe::kScanPer, 2, 20992, false, 0, false, 0, 0, true>(p, fl, epoch, stream);
-        case 723: return pipe::launch_layout<0, 0, pipe::kScanPer, 2, pipe::kStage, false, 0, false, 0, 0, true>(p, fl, epoch, stream, 1, 2);
-        case 724: return pipe::launch_layout<0, 0, pipe::kScanPer, 2, pipe::kStage, false, 0, false, 0, 0, true>(p, fl, epoch, stream, 1, 1);
-        case 725: return pipe::launch_layout<0, 0, pipe::kScanPer, 2, pipe::kStage, false, 0, false, 0, 0, true>(p, fl, epoch, stream, 1, 4);
-        case 726: return pipe::launch_layout<0, 0, pipe::kScanPer, 2, pipe::kStage, false, 0, false, 0, 0, true>(p, fl, epoch, stream, 3, 8);
-        case 727: return pipe::launch_layout<0, 0, pipe::kScanPer, 2, pipe::kStage, false, 0, false, 0, 0, true>(p, fl, epoch, stream, 5, 8);
-        case 728: return pipe::launch_layout<0, 0, pipe::kScanPer, 2, pipe::kStage, false, 0, false, 0, 0, true>(p, fl, epoch, stream, 1, 8);
+        case 711: return launch_layout<PipeCfg{.spec = true, .specx = 1}>(p, fl, epoch, stream);
+        case 712: return launch_layout<PipeCfg{.spec = true, .specx = 2}>(p, fl, epoch, stream);
+        case 713: return launch_layout<PipeCfg{.spec = true, .specx = 3}>(p, fl, epoch, stream);
         // speculative parsers on half the CUs: scanner tiles per thread 1 / 4, parser tiles per wave step 4 / 1
-        case 730: return pipe::launch_layout<0, 0, 1, 2, pipe::kStage, false, 0, false, 0, 0, true>(p, fl, epoch, stream, 1, 2);
-        case 731: return pipe::launch_layout<0, 0, 4, 2, pipe::kStage, false, 0, false, 0, 0, true>(p, fl, epoch, stream, 1, 2);
-        case 732: return pipe::launch_layout<0, 0, pipe::kScanPer, 4, pipe::kStage, false, 0, false, 0, 0, true>(p, fl, epoch, stream, 1, 2);
-        case 733: return pipe::launch_layout<0, 0, pipe::kScanPer, 1, pipe::kStage, false, 0, false, 0, 0, true>(p, fl, epoch, stream, 1, 2);
-        // round 4: 8 waves per SIMD (<= 64 VGPRs) with a 16 KiB stage (8 copiers per CU by LDS), with the
-        // speculative default's geometry; 742: copiers only at 8 per CU (WRONG output); 743: the 16 KiB
-        // stage at 6 waves per SIMD
-        case 740: return pipe::launch_layout<0, 0, 1, 2, 16384, false, 0, false, 0, 0, true, 0, 8>(p, fl, epoch, stream, 1, 2);
-        case 742: return pipe::launch_layout<1, 0, 1, 2, 16384, false, 0, false, 0, 0, true, 0, 8>(p, fl, epoch, stream, 1, 2);
-        case 743: return pipe::launch_layout<0, 0, 1, 2, 16384, false, 0, false, 0, 0, true, 0, 6>(p, fl, epoch, stream, 1, 2);
-        // round 4: copy chunks per lane per step 3 / 4 (default stage), and with the 8-wave 16 KiB stage
-        case 744: return pipe::launch_layout<0, 0, 1, 2, pipe::kStage, false, 0, false, 0, 0, true, 0, 6, 3>(p, fl, epoch, stream, 1, 2);
-        case 745: return pipe::launch_layout<0, 0, 1, 2, pipe::kStage, false, 0, false, 0, 0, true, 0, 6, 4>(p, fl, epoch, stream, 1, 2);
-        case 746: return pipe::launch_layout<0, 0, 1, 2, 16384, false, 0, false, 0, 0, true, 0, 8, 3>(p, fl, epoch, stream, 1, 2);
-        // the gather copier (no LDS stage, output-stationary copy); 601: its timing mode (WRONG output)
-        case 600: return pipe::launch_gather_layout<0>(p, fl, epoch, stream);
-        case 601: return pipe::launch_gather_layout<1>(p, fl, epoch, stream);
-        case 602: return pipe::launch_gather_layout<0>(p, fl, epoch, stream, 1, 2);
-        case 603: return pipe::launch_gather_layout<0>(p, fl, epoch, stream, 1, 1);
-        // the ring decode: lead 3 / 4, barrier / one-wave scanner; 51x: with timestamps
-        case 500: return pipe::launch_ring_layout<0, 3, 0>(p, fl, epoch, stream);
-        case 501: return pipe::launch_ring_layout<0, 3, 1>(p, fl, epoch, stream);
-        case 502: return pipe::launch_ring_layout<0, 4, 0>(p, fl, epoch, stream);
-        case 503: return pipe::launch_ring_layout<0, 4, 1>(p, fl, epoch, stream);
-        case 504: return pipe::launch_ring_layout<0, 3, 2>(p, fl, epoch, stream);  // no scan (WRONG output)
-        case 510: return pipe::launch_ring_layout<1, 3, 0>(p, fl, epoch, stream);
-        case 512: return pipe::launch_ring_layout<1, 4, 0>(p, fl, epoch, stream);
+        case 730: return launch_layout<pipe::kSpecCfg>(p, fl, epoch, stream, 1, 2);
+        case 731: return launch_layout<PipeCfg{.sk = 4, .spec = true}>(p, fl, epoch, stream, 1, 2);
+        case 732: return launch_layout<PipeCfg{.sk = 2, .pr = 4, .spec = true}>(p, fl, epoch, stream, 1, 2);
+        case 733: return launch_layout<PipeCfg{.sk = 2, .pr = 1, .spec = true}>(p, fl, epoch, stream, 1, 2);
+        // round 4: 8 waves per SIMD (<= 64 VGPRs) with a 16 KiB stage (8 copiers per CU by LDS); 742:
+        // copiers only at 8 per CU (WRONG output); 743: the 16 KiB stage at 6 waves per SIMD; 747: a
+        // 17 KiB stage; 748 / 749: parsers on 3/8, 3/4 of the CUs
+        case 740: return launch_layout<PipeCfg{.sk = 1, .stg = 16384, .spec = true, .wpe = 8}>(p, fl, epoch, stream, 1, 2);
+        case 742: return launch_layout<PipeCfg{.mode = 1, .sk = 1, .stg = 16384, .spec = true, .wpe = 8}>(p, fl, epoch, stream, 1, 2);
+        case 743: return launch_layout<PipeCfg{.sk = 1, .stg = 16384, .spec = true}>(p, fl, epoch, stream, 1, 2);
+        case 747: return launch_layout<PipeCfg{.sk = 1, .stg = 17408, .spec = true, .wpe = 8}>(p, fl, epoch, stream, 1, 2);
+        case 748: return launch_layout<PipeCfg{.sk = 1, .stg = 16384, .spec = true, .wpe = 8}>(p, fl, epoch, stream, 3, 8);
+        case 749: return launch_layout<PipeCfg{.sk = 1, .stg = 16384, .spec = true, .wpe = 8}>(p, fl, epoch, stream, 3, 4);
+        // round 4: copy chunks per lane per step 3 / 4 (default stage), and 3 with the 8-wave 16 KiB stage
+        case 744: return launch_layout<PipeCfg{.sk = 1, .spec = true, .uk = 3}>(p, fl, epoch, stream, 1, 2);
+        case 745: return launch_layout<PipeCfg{.sk = 1, .spec = true, .uk = 4}>(p, fl, epoch, stream, 1, 2);
+        case 746: return launch_layout<PipeCfg{.sk = 1, .stg = 16384, .spec = true, .wpe = 8, .uk = 3}>(p, fl, epoch, stream, 1, 2);
+        // round 4: the fast copier (speculative positions, the exact parse as a check beside the copy)
+        case 750: return launch_layout<PipeCfg{.sk = 1, .spec = true, .fast = true}>(p, fl, epoch, stream, 1, 2);
+        case 751: return launch_layout<PipeCfg{.sk = 1, .spec = true, .uk = 3, .fast = true}>(p, fl, epoch, stream, 1, 2);
+        case 752: return launch_layout<PipeCfg{.sk = 1, .stg = 16384, .spec = true, .wpe = 8, .fast = true}>(p, fl, epoch, stream, 1, 2);
+        case 753: return launch_layout<PipeCfg{.sk = 1, .stg = 16384, .spec = true, .wpe = 8, .uk = 3, .fast = true}>(p, fl, epoch, stream, 1, 2);
         default: break;
     }
 #endif
     // speculative parsers are lighter: half the CUs' worth of them keeps ahead of the copiers, and the
     // scanner's 256-tile steps publish sooner (sweeps with configs 2, 3 and the mixed batch,
     // DESIGN.md); exact parsers (int32 fields) keep 3/4 of the CUs and 512-tile steps
-    if (p.lay.nfixed == 0)
-        return pipe::launch_layout<0, 0, 1, 2, pipe::kStage, false, 0, false, 0, 0, true>(p, fl, epoch, stream, 1, 2);
-    return pipe::launch_layout<0, 0, pipe::kScanPer, 2, pipe::kStage, false, 0, false, 0, 0, true>(p, fl, epoch, stream);
+    if (p.lay.nfixed == 0) return launch_layout<pipe::kSpecCfg>(p, fl, epoch, stream, 1, 2);
+    return launch_layout<pipe::kExactCfg>(p, fl, epoch, stream);
 }
 
 }  // namespace symhip

@@ -256,6 +256,15 @@ __device__ __forceinline__ u64 wave_incl_scan_u32w_dpp(u32 v) {
     return ((u64)hi << 25) + lo;
 }
 
+// 64-lane inclusive scan of values < 2^43 with a 64-bit result: two 32-bit DPP scans over a
+// 22/21-bit split (64 * 2^22 fits in 32 bits).  No shuffles: no permute-address registers held
+// across a loop (the streaming scanner's, pipe_words.hpp).
+__device__ __forceinline__ u64 wave_incl_scan_u43_dpp(u64 v) {
+    const u32 lo = wave_incl_scan_u32_dpp((u32)v & 0x3FFFFFu);
+    const u32 hi = wave_incl_scan_u32_dpp((u32)(v >> 22));
+    return ((u64)hi << 22) + lo;
+}
+
 // 64-lane inclusive scan of a u32.
 __device__ __forceinline__ u32 wave_incl_scan_u32(u32 v, int lane) {
 #pragma unroll

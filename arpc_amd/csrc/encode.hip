@@ -658,7 +658,8 @@ template <int NF, int NV, int kVariant, bool MIXED = false, int WPT = 1, bool DI
           bool PIPE = false, int SSK = 8, bool PF = false>
 __device__ __forceinline__ void encode_body(const EncodeParams& p) {
     static_assert(!PF || (WPT == kWaves && TR == kWaveRecs && kVariant == 1), "the prefetching encode takes 64-record workgroup tiles");
-    static_assert(!PIPE || (MIXED && WPT == kWaves && TR == kWaveRecs), "the pipelined size scan is for mixed 64-record workgroup tiles");
+    static_assert(!PIPE || (MIXED && WPT == kWaves && (TR == kWaveRecs || TR == 2 * kWaveRecs)),
+                  "the pipelined size scan is for mixed 64- or 128-record workgroup tiles");
     static_assert(!MIXED || (NF == 0 && NV == 2 && kVariant <= 1), "mixed batches are kv Get/Set");
     static_assert(WPT == 1 || (WPT == kWaves && kVariant <= 1), "whole-workgroup tiles take one step per wave");
     static_assert(TR == kWaveRecs || (TR == 2 * kWaveRecs && WPT == kWaves), "128-record tiles are workgroup tiles");
@@ -775,9 +776,9 @@ __global__ __launch_bounds__(256) void encode_kernel(EncodeParams p) {
 // The one-launch mixed encode: its role code (sizer, scanner, look-back) would otherwise lift the
 // kernel past 64 VGPRs, i.e. from 8 to 6 waves per SIMD, and the encode tiles are latency-bound
 // (tools/mixed_timeline.py: resident tiles x lifetime sets the rate).
-template <bool DIAG = false, int SSK = 1>
+template <bool DIAG = false, int SSK = 1, int TR = kWaveRecs>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void encode_pipe_kernel(EncodeParams p) {
-    encode_body<0, 2, 1, true, kWaves, DIAG, kWaveRecs, true, SSK>(p);
+    encode_body<0, 2, 1, true, kWaves, DIAG, TR, true, SSK>(p);
 }
 
 // The prefetching encode (tuning variants 50-53): persistent wave-specialised workgroups, see
@@ -1019,6 +1020,12 @@ hipError_t launch_encode_mixed(EncodeParams p, void* ws, hipStream_t stream) {
     const u64 grid = p.pipe_lookback ? nt : P + 1 + nt;
     if (grid > 0xFFFFFFFFull) return hipErrorInvalidValue;
 #ifdef SYMHIP_TUNING
+    if (p.variant == 25) {  // 128-record tiles (two header waves, each its 64-record part's prefix)
+        const u64 nt2 = (p.n + 2 * kWaveRecs - 1) / (2 * kWaveRecs);
+        hipLaunchKernelGGL((encode_pipe_kernel<false, 1, 2 * kWaveRecs>), dim3((unsigned)(p.pipe_lookback ? nt2 : P + 1 + nt2)),
+                           dim3(64 * kWaves), 0, stream, p);
+        return hipGetLastError();
+    }
     if (p.variant == 51) {  // the prefetching persistent encode tiles
         launch_pf<0, 2, true, true>(p, stream);
         return hipGetLastError();

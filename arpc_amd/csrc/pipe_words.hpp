@@ -117,7 +117,10 @@ __device__ void scanner(u64* aw, u64* pw, u64 ntiles, u32 epoch, LdsT& S, u64* d
                 x[k] = (u32)(tid * kPer + k) < m ? v[f][k] & kValMask : 0;
                 sum += x[k];
             }
-            const u64 inc = wave_incl_scan_u64(sum, lane);
+            // word values are 42-bit, so up to two of them sum below 2^43: DPP scan (no shuffles)
+            u64 inc;
+            if constexpr (kPer <= 2) inc = wave_incl_scan_u43_dpp(sum);
+            else inc = wave_incl_scan_u64(sum, lane);
             if (lane == 63) S.red[wave] = inc;
             lds_barrier();
             u64 wpre = 0, tot = 0;

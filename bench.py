@@ -180,7 +180,10 @@ def cpu_baseline(kw: dict, seconds: float) -> dict:
                           "share_from": "cgroup cpu quota" if info["cgroup_cpu_quota"] else
                                         ("OMP_NUM_THREADS" if omp else "affinity")},
             "nproc_threads": {"value": gb(repsP, elP), "threads": nproc,
-                              "mrecords_per_s": round(2 * b.n * repsP / elP / 1e6, 4)},
+                              "mrecords_per_s": round(2 * b.n * repsP / elP / 1e6, 4),
+                              "oversubscribed": bool(info["cgroup_cpu_quota"] and nproc > info["cgroup_cpu_quota"]),
+                              "note": "nproc threads on the CPUs this process may use: above its cgroup quota they "
+                                      "time-slice, so this row shows the quota's cap, not a baseline"},
             "host": info,
             "config1_echo": {"marshal_ns": round(m_ns, 2), "unmarshal_ns": round(u_ns, 2),
                              "records_per_s": round(1e9 / (m_ns + u_ns), 1),
@@ -196,11 +199,11 @@ def cpu_baseline(kw: dict, seconds: float) -> dict:
 
 def decode_kernel_name(s, mixed: bool = False) -> str:
     """rocprof's name of the default decode's main launch for schema s (mixed: the Get/Set batch):
-    kv layouts (no int32 fields) run the speculative parsers (decode_pipe.hip), followed by the
-    small gate launch."""
-    spec, sk = ("true", 1) if s.nfixed == 0 else ("false", 2)  # scanner tiles per thread (decode_pipe.hip)
-    return (f"decode_pipe_kernel<{s.nfixed}, {s.nvar}, {'true' if mixed else 'false'}, 0, 0, {sk}, 2, 22528, false, 0, "
-            f"false, 0, 0, {spec}, 0, 6, 2>")
+    kv layouts (no int32 fields) run the speculative parsers with 256-tile scanner steps
+    (decode_pipe.hip kSpecCfg), followed by the small gate launch; int32 layouts the exact parsers
+    (kExactCfg).  PipeCfg{mode, diag, sk, pr, stg, spec, specx, wpe, uk}."""
+    cfg = "0, 0, 1, 2, 22528, true, 0, 6, 2" if s.nfixed == 0 else "0, 0, 2, 2, 22528, false, 0, 6, 2"
+    return f"decode_pipe_kernel<{s.nfixed}, {s.nvar}, {'true' if mixed else 'false'}, symhip::pipe::PipeCfg{{{cfg}}}>"
 
 
 ENCODE_KERNEL = "encode_kernel<0, 2, 1, false, 4, false, 64>"
