@@ -9,11 +9,10 @@
 namespace symhip {
 namespace host {
 constexpr int kSlots = 3;  // chunks in flight in the host-memory entry points
-// One in-flight chunk of a *_host call: its stream, device buffers and pinned staging.
+// One in-flight chunk of a *_host call: its events, device buffers and pinned staging.
 struct Slot {
-    hipStream_t stream = nullptr;
-    hipEvent_t done = nullptr;    // the chunk's last copy
-    hipEvent_t kernel = nullptr;  // the chunk's kernel (kernels of consecutive chunks are ordered)
+    hipEvent_t done = nullptr;    // the chunk's last D2H
+    hipEvent_t kernel = nullptr;  // the chunk's kernels (on the H2D stream, in chunk order)
     void* dev = nullptr;
     size_t dev_bytes = 0;
     void* pin = nullptr;  // pinned staging for pageable caller memory (inputs, then outputs)
@@ -46,8 +45,14 @@ struct sym_ctx {
     // join events (created on first use)
     hipStream_t rx_aux = nullptr;
     hipEvent_t rx_ev[2] = {nullptr, nullptr};
-    // host-memory entry points: chunk slots (created on first use)
+    // host-memory entry points (created on first use): chunk slots; one stream per direction
+    // ([0]: H2D and the kernels, [1]: D2H); the decode's per-slot column (base, total) pairs, written
+    // by the device into coherent pinned memory; the device's running column bases (two sets,
+    // alternating by chunk)
     symhip::host::Slot slots[symhip::host::kSlots];
+    hipStream_t host_stream[2] = {nullptr, nullptr};
+    uint64_t* host_meta = nullptr;
+    uint64_t* host_base = nullptr;
     bool slots_ready = false;
 };
 

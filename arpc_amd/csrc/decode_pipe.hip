@@ -791,6 +791,10 @@ size_t decode_pipe_flag_bytes(int nvar, uint64_t n) {
 namespace pipe {
 constexpr PipeCfg kSpecCfg{.sk = 1, .spec = true};   // kv layouts
 constexpr PipeCfg kExactCfg{.spec = true};          // int32 layouts (exact parsers: spec needs NF == 0)
+// mixed Get/Set batches: 8 waves per SIMD (<= 64 VGPRs) with a 16 KiB stage, 8 copiers per CU
+// (tuning variant 740; r04b: 117.7 -> 102.4 us for the 2^20-record mix, trace mix 551 -> 554 us;
+// config 2's 350-byte records run slower so, 159 -> 188 us, and keep kSpecCfg)
+constexpr PipeCfg kMixCfg{.sk = 1, .stg = 16384, .spec = true, .wpe = 8};
 }  // namespace pipe
 
 hipError_t launch_decode_pipe(const DecodeParams& p, void* flags, unsigned epoch, hipStream_t stream) {
@@ -839,6 +843,9 @@ hipError_t launch_decode_pipe(const DecodeParams& p, void* flags, unsigned epoch
     // speculative parsers are lighter: half the CUs' worth of them keeps ahead of the copiers, and the
     // scanner's 256-tile steps publish sooner (sweeps with configs 2, 3 and the mixed batch,
     // DESIGN.md); exact parsers (int32 fields) keep 3/4 of the CUs and 512-tile steps
+    if (p.type)
+        return p.lay.nfixed == 0 && p.lay.nvar == 2 ? pipe::launch<0, 2, true, pipe::kMixCfg>(p, fl, epoch, stream, 1, 2)
+                                                     : hipErrorInvalidValue;
     if (p.lay.nfixed == 0) return launch_layout<pipe::kSpecCfg>(p, fl, epoch, stream, 1, 2);
     return launch_layout<pipe::kExactCfg>(p, fl, epoch, stream);
 }

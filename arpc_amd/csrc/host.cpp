@@ -2,22 +2,33 @@
 //
 // aRPC hands the codec host buffers: Marshal's output goes to fragmentation and the socket, and
 // Unmarshal reads pooled receive buffers (pkg/transport/transport.go:87, pkg/common/bufferpool.go).
-// These entry points move a host batch through the GPU in record chunks of about kChunkBytes:
-//   chunk c on slot c % kSlots (its own stream, device buffers and pinned staging):
-//     H2D inputs -> kernel -> D2H outputs
-// so one chunk's H2D, another's kernel and a third's D2H run at once (PCIe is full duplex; the
-// kernels of consecutive chunks are ordered by events because they share the ctx's workspaces).
+// These entry points move a host batch through the GPU in record chunks of about kChunkBytes, chunk c
+// in slot c % kSlots (device buffers and pinned staging), over ONE stream per direction:
+//   stream A: [wait: the slot's last D2H] H2D inputs -> kernel -> event K(c)
+//   stream B: [wait: K(c)] D2H outputs -> event D(c)
+// so the next chunks' H2D run on A while earlier chunks' D2H run on B.  PCIe is full duplex, but
+// only with one stream per direction: tools/pcie_bw.py measured 97 GB/s both ways that way and
+// 48-80 GB/s with two to four streams per direction (profiles/r03_pcie_bw.txt), which is what the
+// round-3 form (every slot its own stream doing H2D, kernel and D2H) ran into.  Kernels stay on A,
+// in chunk order (they share the ctx's workspaces).  A slot is reused after a HOST wait for its
+// last D2H (tools/pcie_pattern.hip, profiles/r04_pcie_pattern.txt: the same dependency as a
+// device-side wait of A on B's event ran at half the rate).
 // Caller memory that is pinned (hipHostMalloc, sym_host_alloc, a registered range) is read and
 // written by DMA in place; pageable memory is staged through the slot's pinned buffer with a host
 // memcpy, which overlaps the other slots' transfers.
 //
-// Decode output sizes are only known after the kernel, so a decode chunk has two phases: the
-// fixed-size outputs (status, int32 fields, column offsets) come back first; once they have
-// landed the host places the chunk's column bytes after the previous chunks' and issues their
-// D2H, while later chunks are already on the GPU.
+// Decode output sizes are only known after the kernel, and a chunk's column bytes go right after
+// the previous chunks' in the caller's columns: after each chunk's decode a small kernel on stream
+// A rebases its column offsets by the device's running column totals and writes the chunk's
+// (base, total) per column into coherent pinned memory.  The host waits for that (an event on A,
+// two chunks behind) and issues all of the chunk's D2H at once on B, so B never waits for A on the
+// device and never idles behind a chunk whose kernel has not run.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstdint>
 #include <cstring>
 #include <vector>
@@ -33,16 +44,69 @@ using symhip::host::Slot;
 
 namespace {
 
-constexpr size_t kChunkBytes = 8u << 20;  // target stream bytes per chunk
+constexpr size_t kChunkBytes = 32u << 20;  // target stream bytes per chunk (fewer, larger copies: each op on a
+                                            // stream costs ~10 us of dependency latency, r04e trace)
 constexpr uint64_t kMinChunkRecords = 1024;
+constexpr uint64_t kLag = 1;  // decode: chunk c's D2H are issued after chunk c + kLag's kernels are queued
+static_assert(kLag + 2 <= (uint64_t)kSlots, "a slot is reused only after its D2H were issued");
+
+// Tuning builds: SYMHIP_HOST_TRACE=1 prints, per call, the host time spent inside the copy
+// enqueues, the waits and the kernel launches (tools/host_timeline.py).
+#ifdef SYMHIP_TUNING
+struct HostProbe {
+    double t[4] = {};
+    long n[4] = {};
+    std::chrono::steady_clock::time_point t0;
+};
+HostProbe g_probe;
+bool probe_on() {
+    static const bool v = getenv("SYMHIP_HOST_TRACE") != nullptr;
+    return v;
+}
+template <class F>
+auto timed(int cat, F&& f) {  // 0 H2D enqueue, 1 D2H enqueue, 2 waits, 3 kernel launches
+    if (!probe_on()) return f();
+    const auto a = std::chrono::steady_clock::now();
+    auto r = f();
+    g_probe.t[cat] += std::chrono::duration<double>(std::chrono::steady_clock::now() - a).count();
+    ++g_probe.n[cat];
+    return r;
+}
+void probe_begin() {
+    if (probe_on()) g_probe = HostProbe{{}, {}, std::chrono::steady_clock::now()};
+}
+void probe_end(const char* what) {
+    if (!probe_on()) return;
+    const double tot = std::chrono::duration<double>(std::chrono::steady_clock::now() - g_probe.t0).count();
+    fprintf(stderr, "%s: %.3f ms; h2d enqueue %.3f ms (%ld), d2h enqueue %.3f ms (%ld), waits %.3f ms (%ld), kernels %.3f ms (%ld)\n",
+            what, 1e3 * tot, 1e3 * g_probe.t[0], g_probe.n[0], 1e3 * g_probe.t[1], g_probe.n[1], 1e3 * g_probe.t[2],
+            g_probe.n[2], 1e3 * g_probe.t[3], g_probe.n[3]);
+}
+#else
+template <class F>
+auto timed(int, F&& f) {
+    return f();
+}
+inline void probe_begin() {}
+inline void probe_end(const char*) {}
+#endif
 
 int slots_init(sym_ctx* ctx) {
     if (ctx->slots_ready) return SYM_OK;
+    hipError_t e = hipSuccess;
+    for (hipStream_t& st : ctx->host_stream)
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
     for (Slot& s : ctx->slots) {
-        hipError_t e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&s.kernel, hipEventDisableTiming);
-        if (e != hipSuccess) return hip_fail(e, "host slot streams / events");
+    }
+    if (e == hipSuccess)
+        e = hipHostMalloc((void**)&ctx->host_meta, sizeof(uint64_t) * 2 * symhip::kMaxVar * kSlots,
+                          hipHostMallocCoherent | hipHostMallocMapped);
+    if (e == hipSuccess) e = hipMalloc((void**)&ctx->host_base, sizeof(uint64_t) * 2 * symhip::kMaxVar);
+    if (e != hipSuccess) {
+        symhip::capi::host_slots_destroy(ctx);
+        return hip_fail(e, "host slot streams / events");
     }
     ctx->slots_ready = true;
     return SYM_OK;
@@ -110,26 +174,62 @@ uint64_t records_per_chunk(uint64_t n, uint64_t bytes) {
 }
 
 int sync_all(sym_ctx* ctx) {
-    for (Slot& s : ctx->slots) {
-        hipError_t e = hipStreamSynchronize(s.stream);
+    for (hipStream_t st : ctx->host_stream) {
+        hipError_t e = hipStreamSynchronize(st);
         if (e != hipSuccess) return hip_fail(e, "host staging: hipStreamSynchronize");
     }
     return SYM_OK;
 }
 
+// After chunk c's decode (stream A): its column offsets 1..m rebased by the running totals of the
+// chunks before it, base[c & 1] (base[(c + 1) & 1] = base[c & 1] + the chunk's totals for the next
+// chunk), and (base, total) per column into meta, coherent pinned memory the host reads once the
+// kernel's event has completed.
+struct RebaseArgs {
+    uint64_t* offs[symhip::kMaxVar];  // chunk-local offsets, entries 0..m, [0] = 0
+    uint64_t m;
+    int nvar;
+    uint64_t* base_in;
+    uint64_t* base_out;
+    uint64_t* meta;  // [2 * kMaxVar]: base, total per column
+};
+
+__global__ __launch_bounds__(256) void rebase_kernel(RebaseArgs a) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x + 1;
+    if (i > a.m) return;
+    for (int f = 0; f < a.nvar; ++f) {
+        const uint64_t b = a.base_in[f], v = a.offs[f][i];
+        a.offs[f][i] = v + b;
+        if (i == a.m) {  // the entry's owner: v is the chunk's total
+            a.base_out[f] = b + v;
+            a.meta[2 * f] = b;
+            a.meta[2 * f + 1] = v;
+            __threadfence_system();
+        }
+    }
+}
+
 }  // namespace
 
 void symhip::capi::host_slots_destroy(sym_ctx* ctx) {
-    if (!ctx->slots_ready) return;
+    for (hipStream_t& st : ctx->host_stream) {
+        if (st) {
+            (void)hipStreamSynchronize(st);
+            (void)hipStreamDestroy(st);
+        }
+        st = nullptr;
+    }
     for (Slot& s : ctx->slots) {
-        if (s.stream) (void)hipStreamSynchronize(s.stream);
         if (s.dev) (void)hipFree(s.dev);
         if (s.pin) (void)hipHostFree(s.pin);
         if (s.done) (void)hipEventDestroy(s.done);
         if (s.kernel) (void)hipEventDestroy(s.kernel);
-        if (s.stream) (void)hipStreamDestroy(s.stream);
         s = Slot{};
     }
+    if (ctx->host_meta) (void)hipHostFree(ctx->host_meta);
+    if (ctx->host_base) (void)hipFree(ctx->host_base);
+    ctx->host_meta = nullptr;
+    ctx->host_base = nullptr;
     ctx->slots_ready = false;
 }
 
@@ -217,7 +317,7 @@ int sym_encode_host(sym_ctx* ctx, int schema, uint64_t n, const int32_t* const* 
     auto finish = [&](int k) -> int {
         Pending& P = pend[k];
         if (!P.live) return SYM_OK;
-        hipError_t e = hipEventSynchronize(ctx->slots[k].done);
+        hipError_t e = timed(2, [&] { return hipEventSynchronize(ctx->slots[k].done); });
         if (e != hipSuccess) return hip_fail(e, "sym_encode_host: chunk");
         char* pin = (char*)ctx->slots[k].pin;
         memcpy(h_out + P.out_at, pin + P.pin_out, P.out_bytes);
@@ -227,11 +327,15 @@ int sym_encode_host(sym_ctx* ctx, int schema, uint64_t n, const int32_t* const* 
     };
 
     hipError_t e = hipSuccess;
+    hipStream_t sa = ctx->host_stream[0], sb = ctx->host_stream[1];  // H2D + kernels, D2H
+    probe_begin();
     for (uint64_t c = 0; c < C && rc == SYM_OK; ++c) {
         const int k = (int)(c % kSlots);
         Slot& S = ctx->slots[k];
         if ((rc = finish(k)) != SYM_OK) break;
-        if ((e = hipEventSynchronize(S.done)) != hipSuccess) break;  // the slot's previous chunk is done
+        // the slot's buffers are free once its last D2H is done: a host wait (tools/pcie_pattern: a
+        // device-side wait of the H2D stream on the D2H stream's event halved the duplex rate, 80 -> 40 GB/s)
+        if ((e = timed(2, [&] { return hipEventSynchronize(S.done); })) != hipSuccess) break;
         const uint64_t a = c * R, b = std::min(n, a + R), m = b - a;
         char* dev = (char*)S.dev;
         char* pin = (char*)S.pin;
@@ -245,7 +349,7 @@ int sym_encode_host(sym_ctx* ctx, int schema, uint64_t n, const int32_t* const* 
                 memcpy(pin + o, src, bytes);
                 from = pin + o;
             }
-            if (e == hipSuccess) e = hipMemcpyAsync(dev + o, from, bytes, hipMemcpyHostToDevice, S.stream);
+            if (e == hipSuccess) e = timed(0, [&] { return hipMemcpyAsync(dev + o, from, bytes, hipMemcpyHostToDevice, sa); });
             return o;
         };
         const int32_t* d_fixed[symhip::kMaxFixed] = {};
@@ -265,16 +369,20 @@ int sym_encode_host(sym_ctx* ctx, int schema, uint64_t n, const int32_t* const* 
         const uint64_t out_bytes = m * ovh + vb;
         const size_t o_out = d.take(out_bytes), o_off = d.take(8 * (m + 1));
         if (e != hipSuccess) break;
-        if (c > 0 && (e = hipStreamWaitEvent(S.stream, ctx->slots[(c - 1) % kSlots].kernel, 0)) != hipSuccess) break;
-        rc = encode_call(ctx, schema, m, d_fixed, d_bytes, d_offs, service_id, method_id, (uint8_t*)(dev + o_out),
-                         (uint64_t*)(dev + o_off), base, S.stream);
+        rc = timed(3, [&] {
+            return encode_call(ctx, schema, m, d_fixed, d_bytes, d_offs, service_id, method_id, (uint8_t*)(dev + o_out),
+                               (uint64_t*)(dev + o_off), base, sa);
+        });
         if (rc != SYM_OK) break;
-        if ((e = hipEventRecord(S.kernel, S.stream)) != hipSuccess) break;
+        // output sizes are known on the host: B waits for the kernel on the device (tools/pcie_pattern
+        // "kernel": 90 GB/s both ways)
+        if ((e = hipEventRecord(S.kernel, sa)) != hipSuccess) break;
+        if ((e = hipStreamWaitEvent(sb, S.kernel, 0)) != hipSuccess) break;
         uint8_t* to_out = direct ? h_out + base : (uint8_t*)(pin + o_out);
         uint64_t* to_off = direct ? h_out_off + a : (uint64_t*)(pin + o_off);
-        if ((e = hipMemcpyAsync(to_out, dev + o_out, out_bytes, hipMemcpyDeviceToHost, S.stream)) != hipSuccess) break;
-        if ((e = hipMemcpyAsync(to_off, dev + o_off, 8 * (m + 1), hipMemcpyDeviceToHost, S.stream)) != hipSuccess) break;
-        if ((e = hipEventRecord(S.done, S.stream)) != hipSuccess) break;
+        if ((e = timed(1, [&] { return hipMemcpyAsync(to_out, dev + o_out, out_bytes, hipMemcpyDeviceToHost, sb); })) != hipSuccess) break;
+        if ((e = timed(1, [&] { return hipMemcpyAsync(to_off, dev + o_off, 8 * (m + 1), hipMemcpyDeviceToHost, sb); })) != hipSuccess) break;
+        if ((e = hipEventRecord(S.done, sb)) != hipSuccess) break;
         if (!direct) pend[k] = Pending{true, o_out, o_off, base, out_bytes, a, m};
     }
     if (rc == SYM_OK && e != hipSuccess) rc = hip_fail(e, "sym_encode_host");
@@ -284,7 +392,8 @@ int sym_encode_host(sym_ctx* ctx, int schema, uint64_t n, const int32_t* const* 
     }
     const int r3 = sync_all(ctx);
     if (rc == SYM_OK) rc = r3;
-    const int r4 = sym_ctx_check(ctx, ctx->slots[0].stream);  // the kernels' device error word
+    const int r4 = sym_ctx_check(ctx, sa);  // the kernels' device error word
+    probe_end("sym_encode_host");
     return rc == SYM_OK ? r4 : rc;
 }
 
@@ -339,44 +448,45 @@ int sym_decode_host(sym_ctx* ctx, int schema, uint64_t n, const uint8_t* h_in, c
     for (int k = 0; k < kSlots && rc == SYM_OK; ++k) rc = ensure_slot(ctx->slots[k], dev_need, direct ? 0 : dev_need);
     if (rc != SYM_OK) return rc;
 
-    struct Chunk {  // a chunk between its two phases
-        int phase = 0;  // 0 idle, 1 fixed-size outputs in flight, 2 column bytes in flight
-        uint64_t a = 0, m = 0, span = 0;
+    struct Chunk {  // a chunk between its kernels and its D2H
+        int phase = 0;  // 0 idle, 1 kernels queued (no D2H yet), 2 D2H in flight
+        uint64_t a = 0, m = 0;
         size_t o_status = 0, o_fixed[symhip::kMaxFixed] = {}, o_col[symhip::kMaxVar] = {}, o_offs[symhip::kMaxVar] = {};
         uint64_t col_at[symhip::kMaxVar] = {}, col_len[symhip::kMaxVar] = {};
     } ch[kSlots];
-    uint64_t base[symhip::kMaxVar] = {0, 0};  // column bytes placed so far
     bool overflow = false;
     hipError_t e = hipSuccess;
+    hipStream_t sa = ctx->host_stream[0], sb = ctx->host_stream[1];  // H2D + kernels, D2H
 
-    // phase 1 -> 2: the chunk's offsets have landed; place its column bytes, rebase its offsets
-    auto place = [&](int k) -> int {
+    // phase 1 -> 2: the chunk's kernels are done; its column (base, total) pairs are in host_meta:
+    // every D2H of the chunk at once (fixed-size outputs, rebased offsets, column bytes)
+    auto issue = [&](int k) -> int {
         Chunk& Q = ch[k];
         Slot& S = ctx->slots[k];
         if (Q.phase != 1) return SYM_OK;
-        if ((e = hipEventSynchronize(S.done)) != hipSuccess) return hip_fail(e, "sym_decode_host: chunk");
+        if ((e = timed(2, [&] { return hipEventSynchronize(S.kernel); })) != hipSuccess) return hip_fail(e, "sym_decode_host: chunk");
+        const volatile uint64_t* meta = ctx->host_meta + 2 * symhip::kMaxVar * k;
         char* pin = (char*)S.pin;
         const char* dev = (const char*)S.dev;
+        auto d2h = [&](void* final_dst, size_t o, size_t bytes) {
+            if (e == hipSuccess && bytes)
+                e = timed(1, [&] { return hipMemcpyAsync(direct ? final_dst : (void*)(pin + o), dev + o, bytes, hipMemcpyDeviceToHost, sb); });
+        };
+        d2h(h_status + Q.a, Q.o_status, Q.m);
+        for (int f = 0; f < lay.nfixed; ++f) d2h(h_fixed[f] + Q.a, Q.o_fixed[f], 4 * Q.m);
         for (int f = 0; f < lay.nvar; ++f) {
-            // entries 1..m of the chunk-local offsets (entry 0 is the previous chunk's last)
-            const uint64_t* loc = direct ? h_offs[f] + Q.a + 1 : (const uint64_t*)(pin + Q.o_offs[f]) + 1;
-            const uint64_t total = loc[Q.m - 1];
-            uint64_t* dst = h_offs[f] + Q.a + 1;
-            for (uint64_t i = 0; i < Q.m; ++i) dst[i] = loc[i] + base[f];
-            Q.col_at[f] = base[f];
+            d2h(h_offs[f] + Q.a + 1, Q.o_offs[f] + 8, 8 * Q.m);  // entries 1..m, rebased on the device
+            const uint64_t base = meta[2 * f], total = meta[2 * f + 1];
+            Q.col_at[f] = base;
             Q.col_len[f] = total;
-            if (base[f] + total > caps[f]) {  // SYM_ERR_CAPACITY; the bytes that fit are kept
+            if (base + total > caps[f]) {  // SYM_ERR_CAPACITY; the bytes that fit are kept
                 overflow = true;
-                Q.col_len[f] = caps[f] > base[f] ? caps[f] - base[f] : 0;
+                Q.col_len[f] = caps[f] > base ? caps[f] - base : 0;
             }
-            base[f] += total;
-            if (Q.col_len[f]) {
-                void* to = direct ? (void*)(h_bytes[f] + Q.col_at[f]) : (void*)(pin + Q.o_col[f]);
-                if ((e = hipMemcpyAsync(to, dev + Q.o_col[f], Q.col_len[f], hipMemcpyDeviceToHost, S.stream)) != hipSuccess)
-                    return hip_fail(e, "sym_decode_host: column D2H");
-            }
+            if (Q.col_len[f]) d2h(h_bytes[f] + Q.col_at[f], Q.o_col[f], Q.col_len[f]);
         }
-        if ((e = hipEventRecord(S.done, S.stream)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+        if (e == hipSuccess) e = hipEventRecord(S.done, sb);
+        if (e != hipSuccess) return hip_fail(e, "sym_decode_host: D2H");
         Q.phase = 2;
         return SYM_OK;
     };
@@ -384,28 +494,33 @@ int sym_decode_host(sym_ctx* ctx, int schema, uint64_t n, const uint8_t* h_in, c
     auto complete = [&](int k) -> int {
         Chunk& Q = ch[k];
         if (Q.phase == 1) {
-            const int r = place(k);
+            const int r = issue(k);
             if (r != SYM_OK) return r;
         }
         if (Q.phase != 2) return SYM_OK;
         Slot& S = ctx->slots[k];
-        if ((e = hipEventSynchronize(S.done)) != hipSuccess) return hip_fail(e, "sym_decode_host: chunk");
+        if ((e = timed(2, [&] { return hipEventSynchronize(S.done); })) != hipSuccess) return hip_fail(e, "sym_decode_host: chunk");
         if (!direct) {
             const char* pin = (const char*)S.pin;
             memcpy(h_status + Q.a, pin + Q.o_status, Q.m);
             for (int f = 0; f < lay.nfixed; ++f) memcpy(h_fixed[f] + Q.a, pin + Q.o_fixed[f], 4 * Q.m);
-            for (int f = 0; f < lay.nvar; ++f)
+            for (int f = 0; f < lay.nvar; ++f) {
+                memcpy(h_offs[f] + Q.a + 1, pin + Q.o_offs[f] + 8, 8 * Q.m);
                 if (Q.col_len[f]) memcpy(h_bytes[f] + Q.col_at[f], pin + Q.o_col[f], Q.col_len[f]);
+            }
         }
         Q.phase = 0;
         return SYM_OK;
     };
 
     for (int f = 0; f < lay.nvar; ++f) h_offs[f][0] = 0;
+    probe_begin();
+    if ((e = hipMemsetAsync(ctx->host_base, 0, sizeof(uint64_t) * 2 * symhip::kMaxVar, sa)) != hipSuccess)
+        rc = hip_fail(e, "sym_decode_host");
     for (uint64_t c = 0; c < C && rc == SYM_OK; ++c) {
         const int k = (int)(c % kSlots);
         Slot& S = ctx->slots[k];
-        if ((rc = complete(k)) != SYM_OK) break;
+        if ((rc = complete(k)) != SYM_OK) break;  // the slot's previous chunk has landed
         const uint64_t a = c * R, b = std::min(n, a + R), m = b - a;
         const uint64_t lo = h_rec_off[a], span = h_rec_off[b] - lo;
         char* dev = (char*)S.dev;
@@ -419,14 +534,13 @@ int sym_decode_host(sym_ctx* ctx, int schema, uint64_t n, const uint8_t* h_in, c
                 memcpy(pin + o, src, bytes);
                 from = pin + o;
             }
-            if (e == hipSuccess) e = hipMemcpyAsync(dev + o, from, bytes, hipMemcpyHostToDevice, S.stream);
+            if (e == hipSuccess) e = timed(0, [&] { return hipMemcpyAsync(dev + o, from, bytes, hipMemcpyHostToDevice, sa); });
             return o;
         };
         Chunk& Q = ch[k];
         Q = Chunk{};
         Q.a = a;
         Q.m = m;
-        Q.span = span;
         const uint8_t* d_in = (const uint8_t*)(dev + h2d(h_in + lo, span)) - lo;  // absolute offsets stay valid
         const uint64_t* d_rec = (const uint64_t*)(dev + h2d(h_rec_off + a, 8 * (m + 1)));
         Q.o_status = d.take(m);
@@ -441,23 +555,27 @@ int sym_decode_host(sym_ctx* ctx, int schema, uint64_t n, const uint8_t* h_in, c
             d_offs[f] = (uint64_t*)(dev + (Q.o_offs[f] = d.take(8 * (m + 1))));
         }
         if (e != hipSuccess) break;
-        if (c > 0 && (e = hipStreamWaitEvent(S.stream, ctx->slots[(c - 1) % kSlots].kernel, 0)) != hipSuccess) break;
-        rc = decode_call("sym_decode_host", ctx, lay, nullptr, m, d_in, d_rec, d_fixed, d_bytes, dcaps, d_offs,
-                         (uint8_t*)(dev + Q.o_status), S.stream);
+        rc = timed(3, [&] {
+            return decode_call("sym_decode_host", ctx, lay, nullptr, m, d_in, d_rec, d_fixed, d_bytes, dcaps, d_offs,
+                               (uint8_t*)(dev + Q.o_status), sa);
+        });
         if (rc != SYM_OK) break;
-        if ((e = hipEventRecord(S.kernel, S.stream)) != hipSuccess) break;
-        // fixed-size outputs: status, int32 fields, offsets entries 1..m
-        auto d2h = [&](void* final_dst, size_t o, size_t bytes) {
-            if (e == hipSuccess && bytes)
-                e = hipMemcpyAsync(direct ? final_dst : (void*)(pin + o), dev + o, bytes, hipMemcpyDeviceToHost, S.stream);
-        };
-        d2h(h_status + a, Q.o_status, m);
-        for (int f = 0; f < lay.nfixed; ++f) d2h(h_fixed[f] + a, Q.o_fixed[f], 4 * m);
-        for (int f = 0; f < lay.nvar; ++f) d2h(h_offs[f] + a + 1, Q.o_offs[f] + 8, 8 * m);
-        if (e == hipSuccess) e = hipEventRecord(S.done, S.stream);
-        if (e != hipSuccess) break;
+        if (lay.nvar) {
+            RebaseArgs ra{};
+            for (int f = 0; f < lay.nvar; ++f) ra.offs[f] = d_offs[f];
+            ra.m = m;
+            ra.nvar = lay.nvar;
+            ra.base_in = ctx->host_base + (c & 1) * symhip::kMaxVar;
+            ra.base_out = ctx->host_base + ((c + 1) & 1) * symhip::kMaxVar;
+            ra.meta = ctx->host_meta + 2 * symhip::kMaxVar * k;
+            hipLaunchKernelGGL(rebase_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, sa, ra);
+            if ((e = hipGetLastError()) != hipSuccess) break;
+        }
+        if ((e = hipEventRecord(S.kernel, sa)) != hipSuccess) break;
         Q.phase = 1;
-        if (c > 0 && (rc = place((int)((c - 1) % kSlots))) != SYM_OK) break;  // overlaps chunk c on the GPU
+        // chunk c - kLag's D2H: its kernels finished long ago (the H2D of the chunks after it are queued
+        // on A), and B still has the chunks before it to copy meanwhile
+        if (c >= kLag && (rc = issue((int)((c - kLag) % kSlots))) != SYM_OK) break;
     }
     if (rc == SYM_OK && e != hipSuccess) rc = hip_fail(e, "sym_decode_host");
     for (uint64_t i = 0; i < (uint64_t)kSlots; ++i) {  // drain in chunk order
@@ -466,7 +584,8 @@ int sym_decode_host(sym_ctx* ctx, int schema, uint64_t n, const uint8_t* h_in, c
     }
     const int r3 = sync_all(ctx);
     if (rc == SYM_OK) rc = r3;
-    const int r4 = sym_ctx_check(ctx, ctx->slots[0].stream);
+    const int r4 = sym_ctx_check(ctx, sa);
+    probe_end("sym_decode_host");
     if (rc != SYM_OK) return rc;
     if (r4 != SYM_OK) return r4;
     if (overflow) return fail(SYM_ERR_CAPACITY, "sym_decode_host: a decoded column exceeds its capacity");

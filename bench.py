@@ -201,8 +201,12 @@ def decode_kernel_name(s, mixed: bool = False) -> str:
     """rocprof's name of the default decode's main launch for schema s (mixed: the Get/Set batch):
     kv layouts (no int32 fields) run the speculative parsers with 256-tile scanner steps
     (decode_pipe.hip kSpecCfg), followed by the small gate launch; int32 layouts the exact parsers
-    (kExactCfg).  PipeCfg{mode, diag, sk, pr, stg, spec, specx, wpe, uk}."""
-    cfg = "0, 0, 1, 2, 22528, true, 0, 6, 2" if s.nfixed == 0 else "0, 0, 2, 2, 22528, false, 0, 6, 2"
+    (kExactCfg); the mixed batch 8 waves per SIMD with a 16 KiB stage (kMixCfg).
+    PipeCfg{mode, diag, sk, pr, stg, spec, specx, wpe, uk}."""
+    if mixed:
+        cfg = "0, 0, 1, 2, 16384, true, 0, 8, 2"
+    else:
+        cfg = "0, 0, 1, 2, 22528, true, 0, 6, 2" if s.nfixed == 0 else "0, 0, 2, 2, 22528, false, 0, 6, 2"
     return f"decode_pipe_kernel<{s.nfixed}, {s.nvar}, {'true' if mixed else 'false'}, symhip::pipe::PipeCfg{{{cfg}}}>"
 
 
@@ -552,13 +556,13 @@ def boutique_payloads_leg(codec: Codec, dev, reps: int) -> dict:
                     "the reference README's numbers are Go, one message per call, one core"}
 
 
-def host_inclusive(codec: Codec, kw: dict, dev, steps: int) -> dict:
+def host_inclusive(codec: Codec, kw: dict, dev, steps: int, warm_s: float = 2.0) -> dict:
     """Host memory in, host memory out, through the C ABI's host entry points (what a cgo Serializer
     adapter calls): sym_encode_host then sym_decode_host on the same workload, each call chunked over
-    three streams with H2D / kernel / D2H overlapped (arpc_amd/csrc/host.cpp).  Timed with the host
-    clock around the synchronous calls.  Two caller-memory kinds: pinned (DMA in place) and pageable
-    (staged through the ctx's pinned buffers).  For comparison, the same work serially on one stream
-    (pinned H2D, kernel, D2H, no chunking)."""
+    one stream per direction with H2D / kernel / D2H overlapped (arpc_amd/csrc/host.cpp).  Timed with the host
+    clock around the synchronous calls, after `warm_s` seconds of the same calls.  Two caller-memory
+    kinds: pinned (DMA in place) and pageable (staged through the ctx's pinned buffers).  For
+    comparison, the same work serially on one stream (pinned H2D, kernel, D2H, no chunking)."""
     import ctypes
 
     from arpc_amd import _native
@@ -597,6 +601,12 @@ def host_inclusive(codec: Codec, kw: dict, dev, steps: int) -> dict:
                                             st.data_ptr()), "sym_decode_host")
         enc()
         dcd()  # warm (allocates the slots)
+        # PCIe warm-up: a process's first ~1.5 s of copies run at 55 GB/s both ways, 90 after
+        # (tools/pcie_pattern.hip, profiles/r04_pcie_pattern.txt: two identical sweeps)
+        t_w = time.perf_counter()
+        while time.perf_counter() - t_w < warm_s:
+            enc()
+            dcd()
         ok = bool((st == 0).all()) and all(torch.equal(d[0][:x.numel()], x) for d, (x, _) in zip(dec, var))
         te = td = 0.0
         for _ in range(steps):
@@ -641,8 +651,25 @@ def host_inclusive(codec: Codec, kw: dict, dev, steps: int) -> dict:
         el = time.perf_counter() - t0
         return {"gbps_algorithmic": round((enc_b + dec_b) * steps / el / 1e9, 2), "ms_per_step": round(el / steps * 1e3, 3)}
 
-    return {"pinned": run(True), "pageable": run(False), "serial_one_stream": serial(),
-            "note": "sym_encode_host + sym_decode_host (chunked, 3 streams, H2D/kernel/D2H overlapped), host clock; "
+    def c_caller() -> dict:
+        """tests/bin/host_bench: the same entry points from a plain-C process (no torch: /opt/rocm's HIP
+        runtime, as a cgo adapter links it) on a config-2-shaped batch (64-byte keys, 256-byte values)."""
+        import subprocess
+        drv = os.path.join(ROOT, "tests", "bin", "host_bench")
+        if not os.path.exists(drv):
+            subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests")], check=True, capture_output=True)
+        r = subprocess.run([drv, str(max(steps, 4)), str(warm_s)], capture_output=True, text=True, timeout=300)
+        if r.returncode != 0:
+            raise RuntimeError(r.stdout + r.stderr)
+        return json.loads(r.stdout.strip().splitlines()[-1])
+
+    return {"pinned": c_caller(), "pinned_in_torch_process": run(True), "pageable": run(False),
+            "serial_one_stream": serial(),
+            "note": "sym_encode_host + sym_decode_host (chunked, one stream per direction, H2D/kernel/D2H "
+                    "overlapped), host clock after a 2 s warm-up of the same calls; pinned: from a plain-C "
+                    "process (tests/host_bench.c), the caller a cgo adapter is; pinned_in_torch_process: the same "
+                    "calls on torch's bundled HIP runtime, which runs D2H copies as blit kernels "
+                    "(profiles/r04_host_timeline.txt); "
                     "algorithmic bytes as the headline; serial_one_stream: the same work unchunked on one stream"}
 
 

@@ -166,15 +166,15 @@ def _pinned(L, ctx, nbytes, dtype, keep):
 @pytest.mark.parametrize("schema,lens", [("kv_set_request", (64, ("loguniform", 1, 4096))),
                                          ("echo_request", (("uniform", 0, 300), ("uniform", 0, 600)))])
 def test_host_entry_points_many_chunks(codec, memory, schema, lens):
-    """sym_encode_host / sym_decode_host over a batch of ~5 chunks (kChunkBytes = 8 MiB): outputs of
-    every chunk land in place, bit-exact against the oracle; a corrupted record's status and the
-    record after it come back exactly as the oracle decodes them."""
+    """sym_encode_host / sym_decode_host over a batch of ~5 chunks (kChunkBytes = 32 MiB, 3 slots:
+    every slot reused): outputs of every chunk land in place, bit-exact against the oracle; a
+    corrupted record's status and the record after it come back exactly as the oracle decodes them."""
     L, ctx = codec._lib, codec._ctx
     sid = datagen.schemas.BY_NAME[schema].schema_id
-    n = 64000 if schema == "kv_set_request" else 110000
+    n = 260000 if schema == "kv_set_request" else 420000
     b = datagen.make_batch(schema, n, lens, seed=0x5EEDC0DE)
     want, want_off = oracle.encode_batch(b.fixed, b.var, 3, 4)
-    assert int(want_off[-1]) > 4 * (8 << 20)
+    assert int(want_off[-1]) > 4 * (32 << 20)
     keep = []
     try:
         if memory == "pinned":
