@@ -9,11 +9,13 @@
 //   caller   t = ticket++; wait until slot[t % kRingSlots].turn == t; write the record into the slot;
 //            store req = t + 1; posted += 1; if the worker announced that it is quitting, see that
 //            one runs (batcher.cpp); spin until done == t + 1; copy the result out; turn = t + kRingSlots
-//   worker   poll `posted` (one 8-byte PCIe read); when it passed the records served, every lane looks
-//            at one slot of the window [e, e + kRingSlots) and the ready ones are served, one wave per
-//            record: the record is read into LDS with system-scope 8-byte loads, encoded or parsed there
-//            exactly as MarshalSymphony / UnmarshalSymphony (kv.syn.go:611-745, echo.syn.go:111-263),
-//            the result written back with system-scope 8-byte stores, waited for, then done = t + 1
+//   worker   poll `posted` (one 8-byte PCIe read) while cold; when it passed the records served -- or
+//            at once while hot (a record within the last 50 us) -- every lane of the first 256 looks at
+//            one slot of the window [e, e + kRingSlots) (req and in_len in one round trip) and the ready
+//            ones are served, one wave per record, 16 at once: the record is read into LDS with
+//            system-scope 8-byte loads and encoded or parsed there exactly as MarshalSymphony /
+//            UnmarshalSymphony (kv.syn.go:611-745, echo.syn.go:111-263), each 8-byte word of the result
+//            built from LDS and written with a system-scope store, waited for, then done = t + 1
 //
 // The worker exits when told to (sym_batcher_destroy) or after kIdleTicks without a record; before it
 // exits it announces `quit` and looks at `posted` once more (a Dekker hand-shake with the callers,
@@ -34,25 +36,28 @@ __device__ __forceinline__ u64 ld_sys(const u64* p) { return __hip_atomic_load(p
 __device__ __forceinline__ void st_sys(u64* p, u64 v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); }
 __device__ __forceinline__ void fence_sys() { __atomic_thread_fence(__ATOMIC_SEQ_CST); }
 
-constexpr int kThreads = 256;
+constexpr int kThreads = 1024;  // 16 waves: up to 16 records served at once (each latency-bound)
 constexpr int kWaves = kThreads / 64;
-
-constexpr size_t kOutStage = (kDecData + 2 * (kRingRecordMax + 16) + 15) & ~(size_t)15;  // >= any result
-struct alignas(16) WaveBuf {
-    uint8_t in[kSlotIn + 16];
-    uint8_t out[kOutStage + 16];
-};
+constexpr u64 kHotTicks = 5000;  // 50 us after the last record the worker polls the slots directly
 
 struct alignas(16) Lds {
-    WaveBuf w[kWaves];
+    uint8_t in[kWaves][kSlotIn + 16];  // a wave's record (results are built from it word by word)
     u64 served[kRingSlots];  // served[t % kRingSlots] == t + 1: ticket t was served by a worker
     int list[kRingSlots];    // ready tickets of this pass (offsets from e)
+    u32 len[kRingSlots];     // and their in_len
     int nlist;
     int quit;                // 1: leave the loop
+    int hot;                 // 1: records came lately: look at the slots without waiting for `posted`
 };
 
 __device__ __forceinline__ u32 rd32(const uint8_t* b, u64 q) {
     return (u32)b[q] | ((u32)b[q + 1] << 8) | ((u32)b[q + 2] << 16) | ((u32)b[q + 3] << 24);
+}
+__device__ __forceinline__ u64 rd64(const uint8_t* b) {  // 8 bytes from any LDS byte address
+    u64 v = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v |= (u64)b[i] << (8 * i);
+    return v;
 }
 
 // One wave copies `bytes` (rounded up to 8) from host memory at src (8-byte aligned) into LDS with
@@ -60,16 +65,18 @@ __device__ __forceinline__ u32 rd32(const uint8_t* b, u64 q) {
 __device__ __forceinline__ void load_in(uint8_t* dst, const uint8_t* src, u64 bytes, int lane) {
     for (u64 c = 8 * (u64)lane; c < bytes; c += 8 * 64) *(u64*)(dst + c) = ld_sys((const u64*)(src + c));
 }
-// One wave copies `bytes` (rounded up to 8) from LDS to host memory at dst with system-scope 8-byte
-// stores, then waits until they are performed: the done flag that follows cannot overtake them.
-__device__ __forceinline__ void store_out(uint8_t* dst, const uint8_t* src, u64 bytes, int lane) {
-    for (u64 c = 8 * (u64)lane; c < bytes; c += 8 * 64) st_sys((u64*)(dst + c), *(const u64*)(src + c));
+// One wave writes words [0, words) of a result, word(w) computed from LDS, to host memory at dst
+// with system-scope 8-byte stores, then waits until they are performed: the done flag that follows
+// cannot overtake them.
+template <class W>
+__device__ __forceinline__ void store_words(uint8_t* dst, u64 words, int lane, W&& word) {
+    for (u64 w = (u64)lane; w < words; w += 64) st_sys((u64*)dst + w, word(w));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// MarshalSymphony of one record (+ the client's ID patch, pkg/rpc/client.go:267-271) into LDS.
-// In area: EncIn header, then the var fields' bytes back to back.  Returns the record size.
-__device__ u64 encode_one(const Layout lay, const uint8_t* in, uint8_t* out, int lane) {
+// MarshalSymphony of one record (+ the client's ID patch, pkg/rpc/client.go:267-271) from its in
+// area (EncIn header, then the var fields' bytes back to back) straight to the slot's out area.
+__device__ void encode_one(const Layout lay, const uint8_t* in, uint8_t* dst, int lane) {
     const EncIn* h = (const EncIn*)in;
     const int F = lay.nfixed, V = lay.nvar;
     const u64 tab = 14 + 4 * (u64)(F + V);  // header + private table
@@ -86,36 +93,35 @@ __device__ u64 encode_one(const Layout lay, const uint8_t* in, uint8_t* out, int
         }
     }
     const u64 size = p;
-    for (u64 q = (u64)lane; q < size; q += 64) {
-        u32 b;
+    // scalars for the lambdas (a captured array would live in scratch)
+    const u64 len0 = len[0], len1 = len[1], pay0 = pay[0], pay1 = pay[1], src0 = src[0], src1 = src[1];
+    auto byte_at = [&](u64 q) -> u32 {
+        if (q >= size) return 0;
         if (q < tab) {
-            u32 word = 0;  // the 4-byte word holding byte q (the two version bytes aside)
+            if (q == 0 || q == 13) return 1;  // public / private version
             const u64 w = q < 13 ? (q - 1) / 4 : (q - 14) / 4;
-            if (q == 0 || q == 13) {
-                b = 1;  // public / private version
-                out[q] = (uint8_t)b;
-                continue;
-            }
+            u32 word;  // the 4-byte word holding byte q
             if (q < 13) word = w == 0 ? 13u : (w == 1 ? h->service_id : h->method_id);
             else if ((int)w < F) word = (u32)h->fixed[w];
-            else word = (u32)((w == (u64)F ? pay[0] : pay[1]) - 13);  // offset relative to the private segment
+            else word = (u32)((w == (u64)F ? pay0 : pay1) - 13);  // offset relative to the private segment
             const u64 k = q < 13 ? (q - 1) % 4 : (q - 14) % 4;
-            b = (word >> (8 * k)) & 0xffu;
-        } else {
-            const bool second = V == 2 && q >= pay[1];
-            const u64 r = q - (second ? pay[1] : pay[0]);
-            const u64 ln = second ? len[1] : len[0];
-            b = r < 4 ? (u32)((ln >> (8 * r)) & 0xffu) : in[(second ? src[1] : src[0]) + (r - 4)];
+            return (word >> (8 * k)) & 0xffu;
         }
-        out[q] = (uint8_t)b;
-    }
-    return size;
+        const bool second = V == 2 && q >= pay1;
+        const u64 r = q - (second ? pay1 : pay0);
+        const u64 ln = second ? len1 : len0;
+        return r < 4 ? (u32)((ln >> (8 * r)) & 0xffu) : in[(second ? src1 : src0) + (r - 4)];
+    };
+    store_words(dst, (size + 7) / 8, lane, [&](u64 w) {
+        u64 v = 0;
+        for (int i = 0; i < 8; ++i) v |= (u64)byte_at(8 * w + i) << (8 * i);
+        return v;
+    });
 }
 
-// UnmarshalSymphony of one record (kv.syn.go:680-745, echo.syn.go:186-263) from LDS: the DecOut header
-// and the fields' bytes (field f at kDecData + its offset) into LDS.  Returns the out bytes used.
-__device__ u64 decode_one(const Layout lay, const uint8_t* in, u64 L, uint8_t* out, int lane) {
-    DecOut* o = (DecOut*)out;
+// UnmarshalSymphony of one record (kv.syn.go:680-745, echo.syn.go:186-263) from its in area straight
+// to the slot's out area: the DecOut header, field 0's bytes at kDecData, field 1's at kDecData + at1.
+__device__ void decode_one(const Layout lay, const uint8_t* in, u64 L, uint8_t* dst, int lane) {
     u64 flen[kMaxVar] = {0, 0}, fpos[kMaxVar] = {0, 0};
     u32 st = SYM_STATUS_OK;
     int32_t fx[kMaxFixed] = {0, 0};
@@ -159,16 +165,23 @@ __device__ u64 decode_one(const Layout lay, const uint8_t* in, u64 L, uint8_t* o
         }
     }
     const u64 at1 = (flen[0] + 15) & ~(u64)15;  // field 1's bytes start 16-byte aligned after field 0's
-    if (lane == 0) {
-        o->status = st;
-        for (int f = 0; f < kMaxFixed; ++f) o->fixed[f] = fx[f];
-        for (int f = 0; f < kMaxVar; ++f) o->len[f] = flen[f];
-        o->at1 = at1;
-    }
-    uint8_t* d = out + kDecData;
-    for (u64 q = (u64)lane; q < flen[0]; q += 64) d[q] = in[fpos[0] + q];
-    for (u64 q = (u64)lane; q < flen[1]; q += 64) d[at1 + q] = in[fpos[1] + q];
-    return kDecData + at1 + flen[1];
+    static_assert(sizeof(DecOut) == 40 && kDecData == 64, "DecOut words: status | fixed[0], fixed[1], len[0], len[1], at1");
+    // (a field's last word may read up to 7 bytes past it: inside the in area, never used)
+    const u64 flen0 = flen[0], flen1 = flen[1], fpos0 = fpos[0], fpos1 = fpos[1];  // (no captured arrays)
+    const u64 w0 = (u64)st | ((u64)(u32)fx[0] << 32), w1 = (u64)(u32)fx[1];
+    store_words(dst, (kDecData + at1 + flen1 + 7) / 8, lane, [&](u64 w) -> u64 {
+        switch (w) {
+            case 0: return w0;
+            case 1: return w1;
+            case 2: return flen0;
+            case 3: return flen1;
+            case 4: return at1;
+            case 5: case 6: case 7: return 0;
+            default: break;
+        }
+        const u64 p = 8 * w - kDecData;
+        return p < at1 ? rd64(in + fpos0 + p) : rd64(in + fpos1 + (p - at1));
+    });
 }
 
 __global__ __launch_bounds__(kThreads) void worker_kernel(RingCtl* ctl, uint8_t* slots, Layout lay, int dir, u64 gen) {
@@ -182,15 +195,18 @@ __global__ __launch_bounds__(kThreads) void worker_kernel(RingCtl* ctl, uint8_t*
         const u64 d = ld_sys(&sc->done);
         S.served[t % kRingSlots] = d == t + 1 ? t + 1 : 0;
     }
-    if (tid == 0) S.quit = 0;
+    if (tid == 0) {
+        S.quit = 0;
+        S.hot = 0;
+    }
     __syncthreads();
-    u64 progress = __builtin_amdgcn_s_memrealtime();  // lane 0 of wave 0: when a record was last served
+    u64 progress = __builtin_amdgcn_s_memrealtime();  // when a record was last served (every thread)
     u64 served = tid == 0 ? ld_sys(&ctl->served) : 0, passes = tid == 0 ? ld_sys(&ctl->passes) : 0;
     for (;;) {
-        // ---- wave 0, lane 0: is there work, should we stop? ----
+        // ---- cold: wave 0, lane 0 waits for work on `posted` (one 8-byte PCIe read per look) ----
         if (tid == 0) {
             S.nlist = 0;
-            for (;;) {
+            while (!S.hot) {
                 if (ld_sys(&ctl->stop)) {
                     S.quit = 1;
                     break;
@@ -216,35 +232,40 @@ __global__ __launch_bounds__(kThreads) void worker_kernel(RingCtl* ctl, uint8_t*
         }
         __syncthreads();
         if (S.quit) break;
-        // ---- the window: which tickets are ready and not served yet ----
-        {
+        // ---- the window: which tickets are ready and not served yet (req and in_len in one round
+        // trip; hot, the stop flag with them) ----
+        if (tid < kRingSlots) {
             const u64 t = e + (u64)tid;
             const SlotCtl* sc = (const SlotCtl*)(slots + (size_t)(t % kRingSlots) * kSlotBytes);
-            const bool ready = S.served[t % kRingSlots] != t + 1 && ld_sys(&sc->req) == t + 1;
-            if (ready) S.list[atomicAdd(&S.nlist, 1)] = tid;
+            const u64 rq = ld_sys(&sc->req), il = ld_sys(&sc->in_len);
+            const u64 stop = tid == 0 && S.hot ? ld_sys(&ctl->stop) : 0;
+            if (S.served[t % kRingSlots] != t + 1 && rq == t + 1) {
+                const int k = atomicAdd(&S.nlist, 1);
+                S.list[k] = tid;
+                S.len[k] = (u32)min(il, (u64)kRingRecordMax);  // (the caller checked it)
+            }
+            if (stop) S.quit = 1;
         }
         __syncthreads();
+        if (S.quit) break;
         const int nl = S.nlist;
         for (int i = wave; i < nl; i += kWaves) {  // one wave per record
             const u64 t = e + (u64)S.list[i];
             uint8_t* slot = slots + (size_t)(t % kRingSlots) * kSlotBytes;
             SlotCtl* sc = (SlotCtl*)slot;
-            WaveBuf& B = S.w[wave];
-            const u64 in_len = min(ld_sys(&sc->in_len), (u64)kRingRecordMax);  // (the caller checked it)
+            uint8_t* in = S.in[wave];
+            const u64 in_len = S.len[i];
             if (dir == 0) {
-                load_in(B.in, slot + kSlotInAt, sizeof(EncIn) + in_len, lane);
+                load_in(in, slot + kSlotInAt, sizeof(EncIn) + in_len, lane);
                 wave_sync();
-                const u64 size = encode_one(lay, B.in, B.out, lane);
-                wave_sync();
-                store_out(slot + kSlotOutAt, B.out, size, lane);
+                encode_one(lay, in, slot + kSlotOutAt, lane);
             } else {
-                load_in(B.in, slot + kSlotInAt, in_len, lane);
+                load_in(in, slot + kSlotInAt, in_len, lane);
                 wave_sync();
-                const u64 used = decode_one(lay, B.in, in_len, B.out, lane);
-                wave_sync();
-                store_out(slot + kSlotOutAt, B.out, used, lane);
+                decode_one(lay, in, in_len, slot + kSlotOutAt, lane);
             }
             if (lane == 0) st_sys(&sc->done, t + 1);  // after the wave's stores were performed
+            wave_sync();  // the wave's in buffer is read before its next record overwrites it
         }
         __syncthreads();
         // ---- served: advance the window over its served prefix ----
@@ -255,15 +276,18 @@ __global__ __launch_bounds__(kThreads) void worker_kernel(RingCtl* ctl, uint8_t*
         __syncthreads();
         nproc += (u64)nl;
         while (S.served[e % kRingSlots] == e + 1) ++e;  // (every thread, the same walk)
+        const u64 now = __builtin_amdgcn_s_memrealtime();
         if (nl) {
-            progress = __builtin_amdgcn_s_memrealtime();
+            progress = now;
             if (tid == 0) {  // (stores only: the counters of earlier workers were read at the start)
                 served += (u64)nl;
                 st_sys(&ctl->served, served);
                 st_sys(&ctl->passes, ++passes);
+                S.hot = 1;
             }
         } else {
-            __builtin_amdgcn_s_sleep(20);  // published records outside the window: look again shortly
+            if (tid == 0 && now - progress > kHotTicks) S.hot = 0;  // cold again: wait on `posted`
+            __builtin_amdgcn_s_sleep(2);
         }
         __syncthreads();
     }
