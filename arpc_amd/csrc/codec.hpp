@@ -171,6 +171,7 @@ struct GatherArgs {
     uint64_t* kept_index;  // FW: input position of each kept record (nullable)
     uint64_t* nkept;       // FW
     unsigned* err;
+    uint64_t seg_bytes_hint;  // VAR: the caller's estimate of the mean segment length (0: none)
 };
 }  // namespace raw
 hipError_t launch_tile_scan(const raw::Pair* agg, raw::Pair* pre, uint64_t ntiles, hipStream_t stream);

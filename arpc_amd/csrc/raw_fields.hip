@@ -200,7 +200,7 @@ __device__ __forceinline__ u64 readlane_u64(u64 v, int l) {
 
 // One 256-segment tile (the workgroup's loop body below).  pre[ntiles] is the total: a scan over
 // the capacity's tiles has it there too, at the exclusive prefix of the first empty tile.
-template <bool FW>
+template <bool FW, int KU = 4>
 __device__ __forceinline__ void gather_tile(const GatherArgs& a, u64 tile, u64 n, u64 ntiles, WaveLds* lds_all,
                                             const MaskTable& masks, u64* wsum_b, u64* wsum_c) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -284,7 +284,7 @@ __device__ __forceinline__ void gather_tile(const GatherArgs& a, u64 tile, u64 n
     uint8_t* const out_t = a.out + D0;
     if (safe) {
         // kU chunks per lane per step: every load of the step is issued before its stores
-        constexpr int kU = 4;
+        constexpr int kU = KU;
         for (int B = firstc; B < span; B += 16 * 64 * kU) {  // wave-uniform loop
             u32x4 r[kU];
 #pragma unroll
@@ -297,9 +297,9 @@ __device__ __forceinline__ void gather_tile(const GatherArgs& a, u64 tile, u64 n
                 const bool two = k0 + 1 < nl && o1 < P + 16;  // the next segment starts in this chunk
                 const int o2 = two ? S.o[k0 + 2] : o1;
                 const uintptr_t X0 = (uintptr_t)(S.addr[k0] + (u64)(i64)(P - o0));
-                const uintptr_t X1 = two ? (uintptr_t)(S.addr[k0 + 1] + (u64)(i64)(P - o1)) : X0;
-                r[u] = (ld16u(X0) & range_mask(masks, o0 - P, o1 - P)) |
-                       (ld16u(X1) & range_mask(masks, two ? o1 - P : 16, o2 - P));
+                r[u] = ld16u(X0) & range_mask(masks, o0 - P, o1 - P);
+                if (two)  // (a chunk inside one segment, the usual case, issues one load)
+                    r[u] |= ld16u((uintptr_t)(S.addr[k0 + 1] + (u64)(i64)(P - o1))) & range_mask(masks, o1 - P, o2 - P);
                 for (int k = k0 + 2; two && k < nl && S.o[k] < P + 16; ++k)  // segments < 16 bytes
                     r[u] |= ld16u((uintptr_t)(S.addr[k] + (u64)(i64)(P - S.o[k]))) &
                             range_mask(masks, S.o[k] - P, S.o[k + 1] - P);
@@ -330,7 +330,7 @@ __device__ __forceinline__ void gather_tile(const GatherArgs& a, u64 tile, u64 n
 
 // Grid-stride over the tiles of the segment count (*n_ptr when given, else n): a launch sized for a
 // capacity far above the real count (nested item lists) does not dispatch a workgroup per empty tile.
-template <bool FW>
+template <bool FW, int KU = 4>
 __global__ __launch_bounds__(kWaves * 64) void gather_kernel(GatherArgs a) {
     __shared__ WaveLds lds_all[kWaves];
     __shared__ MaskTable masks;
@@ -340,7 +340,7 @@ __global__ __launch_bounds__(kWaves * 64) void gather_kernel(GatherArgs a) {
     if (n == 0) return;  // nothing to place (and the scan of an empty count may not have run)
     mask_table_init(masks, threadIdx.x);
     for (u64 t = blockIdx.x; t < ntiles; t += gridDim.x) {  // workgroup-uniform loop
-        gather_tile<FW>(a, t, n, ntiles, lds_all, masks, wsum_b, wsum_c);
+        gather_tile<FW, KU>(a, t, n, ntiles, lds_all, masks, wsum_b, wsum_c);
         __syncthreads();  // wsum_* and the wave slots are rewritten by the next tile
     }
 }
@@ -384,8 +384,19 @@ hipError_t launch_tile_scan_gated(const raw::Pair* agg, raw::Pair* pre, u64 ntil
 hipError_t launch_segment_gather(const raw::GatherArgs& a, hipStream_t stream) {
     // a workgroup per tile of the capacity, up to 16384 (a 2^22-segment batch); past that (item
     // capacities of nested lists, far above their real counts) the workgroups stride over the tiles
-    hipLaunchKernelGGL(raw::gather_kernel<false>, dim3((unsigned)std::min<u64>(raw::tiles_of(a.n), 16384)), dim3(256), 0,
-                       stream, a);
+    const dim3 grid((unsigned)std::min<u64>(raw::tiles_of(a.n), 16384));
+    // segments of ~640 bytes (config-3 datagram payloads) ran faster with 2 chunks per lane per step
+    // (more waves per SIMD: reassembly config 3 0.718 -> 0.689 ms); ~350-byte ones with 4 (config 2
+    // 0.302 vs 0.313 ms, flat decode 0.339 vs 0.349 ms; r04h, SYMHIP_GATHER_VARIANT 1 / 2 below)
+    int ku = a.seg_bytes_hint >= 512 ? 2 : 4;
+#ifdef SYMHIP_TUNING
+    if (const int v = tuning_variant("SYMHIP_GATHER_VARIANT")) ku = v == 1 ? 2 : v == 2 ? 8 : 4;
+#endif
+    if (ku == 2) hipLaunchKernelGGL((raw::gather_kernel<false, 2>), grid, dim3(256), 0, stream, a);
+#ifdef SYMHIP_TUNING
+    else if (ku == 8) hipLaunchKernelGGL((raw::gather_kernel<false, 8>), grid, dim3(256), 0, stream, a);
+#endif
+    else hipLaunchKernelGGL(raw::gather_kernel<false>, grid, dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 

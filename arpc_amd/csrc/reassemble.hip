@@ -747,6 +747,7 @@ hipError_t launch_reassemble(const uint8_t* wire, const u64* dg_off, u64 n, uint
         ga.out = msg;
         ga.cap = msg_cap;
         ga.err = err;
+        ga.seg_bytes_hint = msg_cap / n;  // (the capacity is usually the wire size)
         return launch_segment_gather(ga, st);
     };
     // Simple batches (every DataPacket one whole message) complete here: parse (with the tile
