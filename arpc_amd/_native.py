@@ -73,11 +73,16 @@ SIGNATURES = {
     "sym_flat_decode": (_int, [_ctx, _vp, _int, _u64, _u8p, _u64p, _vp, _vp, _vp, _u8p, _vp]),
     "sym_flat_encoded_size_ex": (_u64, [_vp, _int, _u64, _vp, _vp]),
     "sym_flat_encode_ex": (_int, [_ctx, _vp, _int, _u64, _vp, _vp, _vp, _u32, _u32, _u8p, _u64p, _vp]),
+    "sym_flat_encode_ex2": (_int, [_ctx, _vp, _int, _u64, _vp, _vp, _vp, _u32, _u32, _int, _u8p, _u64p, _vp]),
     "sym_flat_decode_ex": (_int, [_ctx, _vp, _int, _u64, _u8p, _u64p, _vp, _vp, _vp, _vp, _vp, _u8p, _u8p, _vp]),
     "sym_flat_decode_ex2": (_int, [_ctx, _vp, _int, _u64, _u8p, _u64p, _u64p, _u64p, _u64p, _vp, _vp, _vp, _vp, _vp,
                                    _vp, _u8p, _u8p, _vp]),
     "sym_flat_nested_status": (_int, [_ctx, _vp, _int, _int, _u64, _u64p, _u8p, _u8p, _u8p, _vp]),
     "sym_flat_list_sizes": (_int, [_ctx, _int, _u64, _vp, _vp, _vp, _u64p, _vp]),
+    "sym_flat_decode_ex3": (_int, [_ctx, _vp, _int, _u64, _u64p, _u8p, _u64p, _u64p, _u64p, _u64p, _vp, _vp, _vp, _vp,
+                                   _vp, _vp, _u8p, _u8p, _vp]),
+    "sym_flat_nested_status2": (_int, [_ctx, _vp, _int, _int, _vp, _u64, _u64p, _vp, _vp, _u8p, _u8p, _vp]),
+    "sym_flat_list_sizes2": (_int, [_ctx, _int, _u64, _u64p, _vp, _vp, _vp, _u64p, _vp]),
     "sym_raw_set": (_int, [_ctx, _vp, _int, _int, _u8p, _u64p, _u64, _vp, _u64p, _u8p, _u64, _u64p, _u8p, _vp]),
     "sym_batcher_create": (_int, [_int, _int, _u32, _u64, _u32, ctypes.POINTER(ctypes.c_void_p)]),
     "sym_batcher_destroy": (_int, [_vp]),
@@ -137,6 +142,7 @@ SYM_SET_BAD_LENGTH = 7
 SYM_MAX_FLAT_FIELDS = 16
 SYM_FIELD_REPEATED = 0x80
 SYM_FIELD_MESSAGE = 0x40
+SYM_FIELD_FRAMED = 0x20
 SYM_STATUS_NESTED = 5
 
 

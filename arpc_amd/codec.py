@@ -63,7 +63,21 @@ class Codec:
         _native.check(self._lib.sym_ctx_create(self.device.index or 0, ctypes.byref(h)), "sym_ctx_create")
         self._ctx = h
 
+    def branch(self, i: int):
+        """(ctx, stream) of concurrent branch i (created on first use): a context of its own (decode
+        workspace, error word) and a stream, for a tree walk's independent subtrees (arpc_amd/flat.py).
+        check() covers the branches' error words too."""
+        br = self.__dict__.setdefault("_branches", [])
+        while len(br) <= i:
+            h = ctypes.c_void_p()
+            _native.check(self._lib.sym_ctx_create(self.device.index or 0, ctypes.byref(h)), "sym_ctx_create")
+            br.append((h, torch.cuda.Stream(self.device)))
+        return br[i]
+
     def close(self):
+        for h, _ in self.__dict__.get("_branches", []):
+            self._lib.sym_ctx_destroy(h)
+        self.__dict__["_branches"] = []
         if getattr(self, "_ctx", None):
             self._lib.sym_ctx_destroy(self._ctx)
             self._ctx = None
@@ -80,6 +94,8 @@ class Codec:
     def check(self, stream=None):
         """Synchronize and raise if a call reported a device-side error (capacity, unplaceable batch)."""
         _native.check(self._lib.sym_ctx_check(self._ctx, _stream_handle(self.device, stream)), "sym_ctx_check")
+        for h, st in self.__dict__.get("_branches", []):
+            _native.check(self._lib.sym_ctx_check(h, st.cuda_stream), "sym_ctx_check")
 
     def set_decode_impl(self, impl: int):
         """SYM_DECODE_PIPELINE (default), SYM_DECODE_THREE_KERNEL or SYM_DECODE_LOOKBACK (same results)."""

@@ -632,10 +632,10 @@ static int flat_check(const char* what, const sym_field* fields, int nf, bool li
     for (int k = 0; k < nf; ++k) {
         if (fields[k].segment > 1) return fail(SYM_ERR_INVALID, "%s: field %d segment %u", what, k, fields[k].segment);
         const unsigned wd = fields[k].width;
-        const unsigned w = wd & ~(SYM_FIELD_REPEATED | SYM_FIELD_MESSAGE), rep = wd & SYM_FIELD_REPEATED;
+        const unsigned w = wd & ~(SYM_FIELD_REPEATED | SYM_FIELD_MESSAGE | SYM_FIELD_FRAMED), rep = wd & SYM_FIELD_REPEATED;
         const bool list = symhip::flat::list_kind(fields[k]) != symhip::flat::kListNone;
         if ((w != 0 && w != 1 && w != 4 && w != 8) || ((wd & SYM_FIELD_MESSAGE) && w != 0) || (list && !lists) ||
-            (rep && w == 0 && !lists))
+            (rep && w == 0 && !lists) || ((wd & SYM_FIELD_FRAMED) && !(wd & SYM_FIELD_MESSAGE)))
             return fail(SYM_ERR_INVALID, "%s: field %d width 0x%x%s", what, k, wd,
                         list && !lists ? " (list-like fields need the _ex entry points)" : "");
     }
@@ -663,8 +663,9 @@ uint64_t sym_flat_encoded_size_ex(const sym_field* fields, int nfields, uint64_t
         const uint64_t b = bytes ? bytes[k] : 0, m = items ? items[k] : 0;
         if (flat_scalar(f)) t += (uint64_t)f.width * n;
         else if (!flat_list(f)) t += 8 * n + b;  // entry + prefix + payload
-        else if (f.width & SYM_FIELD_REPEATED) t += 8 * n + 4 * m + b;  // entry + count + items
-        else t += 4 * n + 4 * m + b;  // nested: entry, and [len] + message when present
+        else if (f.width & SYM_FIELD_REPEATED) t += 8 * n + ((f.width & SYM_FIELD_FRAMED) ? 0 : 4 * m) + b;  // entry + count + items
+        else t += 4 * n + ((f.width & SYM_FIELD_FRAMED) ? 0 : 4 * m) + b;  // nested: entry, and [len] + message when present
+        // (framed items: b holds their [len] prefixes already)
     }
     return t;
 }
@@ -672,6 +673,13 @@ uint64_t sym_flat_encoded_size_ex(const sym_field* fields, int nfields, uint64_t
 int sym_flat_encode_ex(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const void* const* d_cols,
                        const uint64_t* const* d_offs, const uint64_t* const* d_items, uint32_t service_id,
                        uint32_t method_id, uint8_t* d_out, uint64_t* d_out_off, void* stream) {
+    return sym_flat_encode_ex2(ctx, fields, nfields, n, d_cols, d_offs, d_items, service_id, method_id, 0, d_out,
+                               d_out_off, stream);
+}
+
+int sym_flat_encode_ex2(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const void* const* d_cols,
+                        const uint64_t* const* d_offs, const uint64_t* const* d_items, uint32_t service_id,
+                        uint32_t method_id, int framed, uint8_t* d_out, uint64_t* d_out_off, void* stream) {
     if (!ctx) return fail(SYM_ERR_INVALID, "sym_flat_encode: ctx is NULL");
     int rc = flat_check("sym_flat_encode", fields, nfields, d_items != nullptr);
     if (rc != SYM_OK) return rc;
@@ -690,7 +698,7 @@ int sym_flat_encode_ex(sym_ctx* ctx, const sym_field* fields, int nfields, uint6
         return e == hipSuccess ? SYM_OK : hip_fail(e, "hipMemsetAsync");
     }
     hipError_t e = symhip::launch_flat_encode(fields, nfields, n, d_cols, d_offs, d_items, service_id, method_id,
-                                              d_out, d_out_off, ctx->err, (hipStream_t)stream);
+                                              framed != 0, d_out, d_out_off, ctx->err, (hipStream_t)stream);
     return e == hipSuccess ? SYM_OK : hip_fail(e, "flat encode launch");
 }
 
@@ -701,11 +709,11 @@ int sym_flat_encode(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t
                               d_out_off, stream);
 }
 
-int sym_flat_decode_ex2(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const uint8_t* d_in,
-                        const uint64_t* d_rec_src, const uint64_t* d_rec_len, const uint64_t* d_lo,
-                        const uint64_t* d_hi, void* const* d_cols, const uint64_t* caps, uint64_t* const* d_offs,
-                        uint64_t* const* d_items, uint64_t* const* d_item_len, const uint64_t* item_caps,
-                        uint8_t* d_status, uint8_t* d_fail, void* stream) {
+int sym_flat_decode_ex3(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const uint64_t* d_n,
+                        const uint8_t* d_in, const uint64_t* d_rec_src, const uint64_t* d_rec_len,
+                        const uint64_t* d_lo, const uint64_t* d_hi, void* const* d_cols, const uint64_t* caps,
+                        uint64_t* const* d_offs, uint64_t* const* d_items, uint64_t* const* d_item_len,
+                        const uint64_t* item_caps, uint8_t* d_status, uint8_t* d_fail, void* stream) {
     if (!ctx) return fail(SYM_ERR_INVALID, "sym_flat_decode: ctx is NULL");
     const bool lists = d_items != nullptr;
     int rc = flat_check("sym_flat_decode", fields, nfields, lists);
@@ -737,10 +745,19 @@ int sym_flat_decode_ex2(sym_ctx* ctx, const sym_field* fields, int nfields, uint
     }
     if ((rc = ensure_scratch(ctx, symhip::flat_ws_bytes(fields, nfields, n, item_caps), "flat decode")) != SYM_OK)
         return rc;
-    hipError_t e = symhip::launch_flat_decode(fields, nfields, n, d_in, d_rec_src, d_rec_len, d_lo, d_hi, d_cols, caps,
-                                              d_offs, d_items, d_item_len, item_caps, d_status, d_fail, ctx->frag,
+    hipError_t e = symhip::launch_flat_decode(fields, nfields, n, d_n, d_in, d_rec_src, d_rec_len, d_lo, d_hi, d_cols,
+                                              caps, d_offs, d_items, d_item_len, item_caps, d_status, d_fail, ctx->frag,
                                               ctx->err, (hipStream_t)stream);
     return e == hipSuccess ? SYM_OK : hip_fail(e, "flat decode launch");
+}
+
+int sym_flat_decode_ex2(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const uint8_t* d_in,
+                        const uint64_t* d_rec_src, const uint64_t* d_rec_len, const uint64_t* d_lo,
+                        const uint64_t* d_hi, void* const* d_cols, const uint64_t* caps, uint64_t* const* d_offs,
+                        uint64_t* const* d_items, uint64_t* const* d_item_len, const uint64_t* item_caps,
+                        uint8_t* d_status, uint8_t* d_fail, void* stream) {
+    return sym_flat_decode_ex3(ctx, fields, nfields, n, nullptr, d_in, d_rec_src, d_rec_len, d_lo, d_hi, d_cols, caps,
+                               d_offs, d_items, d_item_len, item_caps, d_status, d_fail, stream);
 }
 
 int sym_flat_decode_ex(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const uint8_t* d_in,
@@ -761,24 +778,44 @@ int sym_flat_decode(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t
 int sym_flat_nested_status(sym_ctx* ctx, const sym_field* fields, int nfields, int field, uint64_t n,
                            const uint64_t* d_rec_items, const uint8_t* d_item_status, uint8_t* d_status,
                            uint8_t* d_fail, void* stream) {
+    return sym_flat_nested_status2(ctx, fields, nfields, 1, &field, n, nullptr, &d_rec_items, &d_item_status, d_status,
+                                   d_fail, stream);
+}
+
+int sym_flat_nested_status2(sym_ctx* ctx, const sym_field* fields, int nfields, int nk, const int* ks, uint64_t n,
+                            const uint64_t* d_n, const uint64_t* const* d_rec_items,
+                            const uint8_t* const* d_item_status, uint8_t* d_status, uint8_t* d_fail, void* stream) {
     if (!ctx) return fail(SYM_ERR_INVALID, "sym_flat_nested_status: ctx is NULL");
     int rc = flat_check("sym_flat_nested_status", fields, nfields, true);
     if (rc != SYM_OK) return rc;
-    if (field < 0 || field >= nfields || !(fields[field].width & SYM_FIELD_MESSAGE))
-        return fail(SYM_ERR_INVALID, "sym_flat_nested_status: field %d is not a message field", field);
-    if (n && (!d_rec_items || !d_item_status || !d_status || !d_fail))
-        return fail(SYM_ERR_INVALID, "sym_flat_nested_status: NULL argument");
-    uint32_t pos = 0;  // the field's position in unmarshal order: public fields, then private
-    for (int k = 0; k < nfields; ++k)
-        if (fields[k].segment < fields[field].segment || (fields[k].segment == fields[field].segment && k < field)) ++pos;
+    if (nk < 0 || nk > nfields || (nk && (!ks || !d_rec_items || !d_item_status)))
+        return fail(SYM_ERR_INVALID, "sym_flat_nested_status: %d fields", nk);
+    uint32_t pos[SYM_MAX_FLAT_FIELDS];
+    for (int q = 0; q < nk; ++q) {
+        const int field = ks[q];
+        if (field < 0 || field >= nfields || !(fields[field].width & SYM_FIELD_MESSAGE))
+            return fail(SYM_ERR_INVALID, "sym_flat_nested_status: field %d is not a message field", field);
+        if (n && (!d_rec_items[q] || !d_item_status[q] || !d_status || !d_fail))
+            return fail(SYM_ERR_INVALID, "sym_flat_nested_status: NULL argument");
+        pos[q] = 0;  // the field's position in unmarshal order: public fields, then private
+        for (int k = 0; k < nfields; ++k)
+            if (fields[k].segment < fields[field].segment || (fields[k].segment == fields[field].segment && k < field))
+                ++pos[q];
+    }
     DeviceGuard g(ctx->device);
     if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
-    hipError_t e = symhip::launch_nested_status(n, pos, d_rec_items, d_item_status, d_status, d_fail, (hipStream_t)stream);
+    hipError_t e = symhip::launch_nested_status(n, d_n, nk, pos, d_rec_items, d_item_status, d_status, d_fail,
+                                                (hipStream_t)stream);
     return e == hipSuccess ? SYM_OK : hip_fail(e, "nested status launch");
 }
 
 int sym_flat_list_sizes(sym_ctx* ctx, int nl, uint64_t n, const uint64_t* const* d_recs,
                         const uint64_t* const* d_items, const uint64_t* item_caps, uint64_t* d_out, void* stream) {
+    return sym_flat_list_sizes2(ctx, nl, n, nullptr, d_recs, d_items, item_caps, d_out, stream);
+}
+
+int sym_flat_list_sizes2(sym_ctx* ctx, int nl, uint64_t n, const uint64_t* d_n, const uint64_t* const* d_recs,
+                         const uint64_t* const* d_items, const uint64_t* item_caps, uint64_t* d_out, void* stream) {
     if (!ctx) return fail(SYM_ERR_INVALID, "sym_flat_list_sizes: ctx is NULL");
     if (nl < 0 || nl > SYM_MAX_FLAT_FIELDS) return fail(SYM_ERR_INVALID, "sym_flat_list_sizes: %d lists", nl);
     if (nl == 0) return SYM_OK;
@@ -787,7 +824,7 @@ int sym_flat_list_sizes(sym_ctx* ctx, int nl, uint64_t n, const uint64_t* const*
         if (!d_recs[i] || !d_items[i]) return fail(SYM_ERR_INVALID, "sym_flat_list_sizes: list %d is NULL", i);
     DeviceGuard g(ctx->device);
     if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
-    hipError_t e = symhip::launch_list_sizes(nl, n, d_recs, d_items, item_caps, d_out, (hipStream_t)stream);
+    hipError_t e = symhip::launch_list_sizes(nl, n, d_n, d_recs, d_items, item_caps, d_out, (hipStream_t)stream);
     return e == hipSuccess ? SYM_OK : hip_fail(e, "list sizes launch");
 }
 

@@ -178,6 +178,9 @@ hipError_t launch_tile_scan(const raw::Pair* agg, raw::Pair* pre, uint64_t ntile
 // the same over the tiles of a device-side item count (*nlim) only
 hipError_t launch_tile_scan_limited(const raw::Pair* agg, raw::Pair* pre, uint64_t ntiles, const uint64_t* nlim,
                                     hipStream_t stream);
+// `rows` scans at once (one workgroup each): row r from agg + r * agg_stride into pre + r * pre_stride
+hipError_t launch_tile_scan_rows(const raw::Pair* agg, uint64_t agg_stride, raw::Pair* pre, uint64_t pre_stride,
+                                 uint64_t ntiles, int rows, const uint64_t* nlim, hipStream_t stream);
 hipError_t launch_tile_scan_gated(const raw::Pair* agg, raw::Pair* pre, uint64_t ntiles, const unsigned* gate,
                                   hipStream_t stream);
 hipError_t launch_segment_gather(const raw::GatherArgs& a, hipStream_t stream);
@@ -189,19 +192,21 @@ namespace symhip {
 size_t flat_ws_bytes(const sym_field* f, int nf, uint64_t n, const uint64_t* item_caps);
 hipError_t launch_flat_encode(const sym_field* f, int nf, uint64_t n, const void* const* cols,
                               const uint64_t* const* offs, const uint64_t* const* items, uint32_t sid, uint32_t mid,
-                              uint8_t* out, uint64_t* out_off, unsigned* err, hipStream_t stream);
+                              bool framed, uint8_t* out, uint64_t* out_off, unsigned* err, hipStream_t stream);
 // rec_len non-null: record i is in[rec_off[i], + rec_len[i]) (records in place); lo / hi: device
 // values bounding in's readable extent (null: rec_off[0], rec_off[n]); item_len[k] non-null for a
 // message field k: items[k] / item_len[k] receive each item's (offset into in, length), no bytes
-hipError_t launch_flat_decode(const sym_field* f, int nf, uint64_t n, const uint8_t* in, const uint64_t* rec_off,
-                              const uint64_t* rec_len, const uint64_t* lo, const uint64_t* hi, void* const* cols,
-                              const uint64_t* caps, uint64_t* const* offs, uint64_t* const* items,
+// n_ptr (nullable): the record count on the device, n its capacity (flat.hip)
+hipError_t launch_flat_decode(const sym_field* f, int nf, uint64_t n, const uint64_t* n_ptr, const uint8_t* in,
+                              const uint64_t* rec_off, const uint64_t* rec_len, const uint64_t* lo, const uint64_t* hi,
+                              void* const* cols, const uint64_t* caps, uint64_t* const* offs, uint64_t* const* items,
                               uint64_t* const* item_len, const uint64_t* item_caps, uint8_t* status, uint8_t* fail,
                               void* ws, unsigned* err, hipStream_t stream);
-hipError_t launch_list_sizes(int nl, uint64_t n, const uint64_t* const* recs, const uint64_t* const* items,
-                             const uint64_t* caps, uint64_t* out, hipStream_t stream);
-hipError_t launch_nested_status(uint64_t n, uint32_t pos, const uint64_t* rec_items, const uint8_t* item_status,
-                                uint8_t* status, uint8_t* fail, hipStream_t stream);
+hipError_t launch_list_sizes(int nl, uint64_t n, const uint64_t* n_ptr, const uint64_t* const* recs,
+                             const uint64_t* const* items, const uint64_t* caps, uint64_t* out, hipStream_t stream);
+hipError_t launch_nested_status(uint64_t n, const uint64_t* n_ptr, int nk, const uint32_t* pos,
+                                const uint64_t* const* rec_items, const uint8_t* const* item_status, uint8_t* status,
+                                uint8_t* fail, hipStream_t stream);
 
 // ---- batched Raw setters (setters.hip)
 size_t raw_set_ws_bytes(uint64_t n);

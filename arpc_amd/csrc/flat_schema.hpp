@@ -42,7 +42,7 @@ inline Schema make_schema(const sym_field* f, int nf) {
     Schema s{};
     s.nf = nf;
     for (int k = 0; k < nf; ++k) {
-        const int ew = f[k].width & ~(SYM_FIELD_REPEATED | SYM_FIELD_MESSAGE);
+        const int ew = f[k].width & ~(SYM_FIELD_REPEATED | SYM_FIELD_MESSAGE | SYM_FIELD_FRAMED);
         s.seg[k] = f[k].segment;
         s.width[k] = is_payload(f[k]) ? 0 : f[k].width;
         s.list[k] = list_kind(f[k]);

@@ -142,9 +142,13 @@ __global__ __launch_bounds__(256) void firewall_mark_kernel(const uint8_t* in, c
 // takes 4 consecutive tiles, so up to 4096 tiles (2^20 records) take one block-wide scan.
 // nlim (optional): a device count of the scanned items; only its ceil(*nlim / 256) tiles are
 // scanned (an item-capacity launch whose real count is known on the device only).
+// rows > 1 (grid = rows): workgroup r scans row r, agg + r * agg_stride into pre + r * pre_stride.
 __global__ __launch_bounds__(1024) void tile_scan_kernel(const Pair* agg, Pair* pre, u64 ntiles,
-                                                        const unsigned* gate = nullptr, const u64* nlim = nullptr) {
+                                                        const unsigned* gate = nullptr, const u64* nlim = nullptr,
+                                                        u64 agg_stride = 0, u64 pre_stride = 0) {
     if (gate && *gate == 0) return;  // a gated launch (reassembly's general path) with nothing to do
+    agg += blockIdx.x * agg_stride;
+    pre += blockIdx.x * pre_stride;
     if (nlim) ntiles = min(ntiles, (*nlim + 255) / 256);
     constexpr int kPer = 4;
     __shared__ u64 wb[16], wc[16];
@@ -402,6 +406,13 @@ hipError_t launch_segment_gather(const raw::GatherArgs& a, hipStream_t stream) {
 
 hipError_t launch_tile_scan_limited(const raw::Pair* agg, raw::Pair* pre, u64 ntiles, const u64* nlim, hipStream_t stream) {
     hipLaunchKernelGGL(raw::tile_scan_kernel, dim3(1), dim3(1024), 0, stream, agg, pre, ntiles, nullptr, nlim);
+    return hipGetLastError();
+}
+
+hipError_t launch_tile_scan_rows(const raw::Pair* agg, u64 agg_stride, raw::Pair* pre, u64 pre_stride, u64 ntiles,
+                                 int rows, const u64* nlim, hipStream_t stream) {
+    hipLaunchKernelGGL(raw::tile_scan_kernel, dim3((unsigned)rows), dim3(1024), 0, stream, agg, pre, ntiles, nullptr,
+                       nlim, agg_stride, pre_stride);
     return hipGetLastError();
 }
 

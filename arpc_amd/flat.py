@@ -25,6 +25,7 @@ Columns (per field, n records):
 """
 from __future__ import annotations
 
+import ctypes
 from dataclasses import dataclass, field as dc_field
 
 import numpy as np
@@ -99,14 +100,16 @@ class FlatSchema:
     name: str
     fields: tuple
 
-    def c_fields(self):
-        arr = _C_FIELDS.get(self)
+    def c_fields(self, framed: bool = False):
+        """The C field list; framed: message fields flagged SYM_FIELD_FRAMED (encode, their items
+        being the inner level's frames)."""
+        arr = _C_FIELDS.get((self, framed))
         if arr is None:  # built once per schema (a tree walk asks for it at every level)
             arr = (_native.SymField * max(1, len(self.fields)))()
             for k, f in enumerate(self.fields):
                 arr[k].segment = _native.SYM_SEGMENT_PUBLIC if f.public else _native.SYM_SEGMENT_PRIVATE
-                arr[k].width = f.c_width
-            _C_FIELDS[self] = arr
+                arr[k].width = f.c_width | (_native.SYM_FIELD_FRAMED if framed and f.kind == "message" else 0)
+            _C_FIELDS[(self, framed)] = arr
         return arr
 
     @property
@@ -135,34 +138,59 @@ def encode(codec: Codec, schema: FlatSchema, cols: list, service_id: int = 0, me
     buffer must hold the encoded size; it is returned whole.  Message fields are encoded first
     (their own message fields first), with service / method ids 0 as MarshalSymphony writes for
     nested messages.  The whole tree is launched without a host sync; only the returned stream's
-    length (offsets[n]) is read back at the end."""
-    buf, off = _encode(codec, schema, cols, service_id, method_id, stream, n, out)
+    length (offsets[n]) is read back at the end.  A level's message fields are independent
+    subtrees: with two or more, each runs on a branch of the codec (Codec.branch: its own stream)
+    and the level waits for them all."""
+    cur = stream if stream is not None else torch.cuda.current_stream(codec.device)
+    keep: list = []  # every level's temporaries, alive until the tree is queued (see _encode)
+    buf, off = _encode(codec, codec._ctx, schema, cols, service_id, method_id, cur, n, out, False, keep, [0])
     if out is not None:
         return buf, off
     size = int(off[-1].item()) if off.numel() > 1 else 0
     return buf[:size], off
 
 
-def _encode(codec: Codec, schema: FlatSchema, cols: list, service_id: int, method_id: int, stream, n, out):
+def _encode(codec: Codec, ctx, schema: FlatSchema, cols: list, service_id: int, method_id: int, stream, n, out,
+            framed: bool, keep: list, fork: list):
     """encode() without the final read-back: the output buffer is sized from the columns' tensor
     sizes (an upper bound of the encoded size: sym_flat_encoded_size_ex of every byte / item column
-    taken whole), so no level needs a device value on the host."""
+    taken whole), so no level needs a device value on the host.  Inner levels are encoded framed
+    (sym_flat_encode_ex2: [u32 size] before each record), so an outer body is one window of them.
+    Subtrees on other branches free nothing before the whole tree is queued (`keep`): a block freed
+    while a kernel of another branch may still read it could be handed to a concurrent branch;
+    after the walk, later work on any branch is ordered after this tree (branches start by waiting
+    on the caller's stream)."""
     if len(cols) != len(schema.fields):
         raise ValueError(f"{schema.name}: {len(schema.fields)} columns expected")
     if not schema.fields and n is None:
         raise ValueError(f"{schema.name}: a schema without fields needs the record count n")
     ptrs, offs, items, nbytes, nitems, n_arg = [], [], [], [], [], n
-    keep = []  # inner streams must outlive the launch
     n = None if schema.fields else n
-    for f, c in zip(schema.fields, cols):
-        if f.kind == "message":
-            if not isinstance(c, MessageColumn):
-                raise ValueError(f"{f.name}: a MessageColumn expected")
-            # a fieldless inner schema needs its record count: the one host read of a level
-            m_in = (int(c.rec[-1].item() - c.rec[0].item()) if c.rec.numel() > 1 else 0) if not c.cols else None
-            ib, io = _encode(codec, f.message, c.cols, 0, 0, stream, m_in, None)
-            c = ListColumn(ib, io, c.rec)
-            keep.append(c)
+    msg = [k for k, f in enumerate(schema.fields) if f.kind == "message"]
+    for k in msg:
+        if not isinstance(cols[k], MessageColumn):
+            raise ValueError(f"{schema.fields[k].name}: a MessageColumn expected")
+    # independent subtrees: the first on this stream, the others on branches that start after this
+    # stream's work so far and are joined back before this level's kernel
+    runs = [(ctx, stream)]
+    for _ in msg[1:]:
+        b_ctx, b_st = codec.branch(fork[0])
+        fork[0] += 1
+        b_st.wait_stream(stream)
+        runs.append((b_ctx, b_st))
+    inner = {}
+    for (r_ctx, r_st), k in zip(runs, msg):
+        c = cols[k]
+        # a fieldless inner schema needs its record count: the one host read of a level
+        m_in = (int(c.rec[-1].item() - c.rec[0].item()) if c.rec.numel() > 1 else 0) if not c.cols else None
+        ib, io = _encode(codec, r_ctx, schema.fields[k].message, c.cols, 0, 0, r_st, m_in, None, True, keep, fork)
+        inner[k] = ListColumn(ib, io, c.rec)
+        keep.append(inner[k])
+    for _, r_st in runs[1:]:
+        stream.wait_stream(r_st)
+    for k, (f, c) in enumerate(zip(schema.fields, cols)):
+        if k in inner:
+            c = inner[k]
         if f.list_like:
             _check_col(c.bytes, torch.uint8, f.name, codec.device)
             _check_col(c.item_off, torch.int64, f.name + " item offsets", codec.device)
@@ -198,10 +226,10 @@ def _encode(codec: Codec, schema: FlatSchema, cols: list, service_id: int, metho
     if n_arg is not None and n is not None and n != n_arg:
         raise ValueError("columns disagree with n")
     n = n or 0
-    cf = schema.c_fields()
+    cf = schema.c_fields(framed=True)  # (the flag only matters for message fields, whose items are frames)
     if out is None:
         size = codec._lib.sym_flat_encoded_size_ex(cf, len(schema.fields), n, _native.u64_array(nbytes or [0]),
-                                                   _native.u64_array(nitems or [0]))
+                                                   _native.u64_array(nitems or [0])) + (4 * n if framed else 0)
         out = torch.empty(max(1, size), dtype=torch.uint8, device=codec.device)
         off = torch.empty(n + 1, dtype=torch.int64, device=codec.device)
     else:
@@ -211,11 +239,10 @@ def _encode(codec: Codec, schema: FlatSchema, cols: list, service_id: int, metho
         if off.numel() != n + 1:
             raise ValueError("out offsets: n + 1 entries expected")
     lists = schema.has_lists
-    _native.check(codec._lib.sym_flat_encode_ex(codec._ctx, cf, len(schema.fields), n, _native.ptr_array(ptrs),
-                                               _native.ptr_array(offs), _native.ptr_array(items) if lists else None,
-                                               service_id, method_id, _dptr(out), _dptr(off),
-                                               _stream_handle(codec.device, stream)), "sym_flat_encode_ex")
-    del keep
+    _native.check(codec._lib.sym_flat_encode_ex2(ctx, cf, len(schema.fields), n, _native.ptr_array(ptrs),
+                                                _native.ptr_array(offs), _native.ptr_array(items) if lists else None,
+                                                service_id, method_id, 1 if framed else 0, _dptr(out), _dptr(off),
+                                                stream.cuda_stream), "sym_flat_encode_ex2")
     return out, off
 
 
@@ -225,10 +252,15 @@ def decode(codec: Codec, schema: FlatSchema, data: torch.Tensor, rec_off: torch.
     """UnmarshalSymphony into fresh structs -> (cols, status) (with_fail: (cols, status, fail)); cols
     per the module docstring, message fields decoded recursively with their items' statuses folded
     into `status` (SYM_STATUS_NESTED).  span = rec_off[n] - rec_off[0] when the caller knows it
-    (skips a device sync).  Inner levels are decoded in place (sym_flat_decode_ex2): a message
+    (skips a device sync).  Inner levels are decoded in place (sym_flat_decode_ex3): a message
     field's items stay where they are in `data` -- rec_off holds their offsets, rec_len their
     lengths, extent the device pointers bounding data's readable bytes, span an upper bound of their
-    bytes -- so no level copies its inner messages out."""
+    bytes -- so no level copies its inner messages out.  The whole tree is queued without a host
+    sync: an inner level's record count stays on the device (the outer level's item count, from
+    sym_flat_list_sizes2) and its columns are sized for a capacity; every level's list sizes are
+    read back once, at the end, and the columns cut to them.  A level's message fields are
+    independent subtrees: with two or more, each runs on a branch of the codec (Codec.branch: its
+    own stream and context, the decode workspace being per context)."""
     _check_col(data, torch.uint8, "data", codec.device)
     _check_col(rec_off, torch.int64, "rec_off", codec.device)
     if rec_len is not None:
@@ -236,15 +268,41 @@ def decode(codec: Codec, schema: FlatSchema, data: torch.Tensor, rec_off: torch.
         if rec_len.numel() and (extent is None or span is None):
             raise ValueError("records in place need extent and span")
     n = rec_off.numel() - 1 if rec_len is None else rec_len.numel()
-    in_place = rec_len is not None and n > 0
     if span is None:
         span = int(rec_off[-1].item() - rec_off[0].item()) if n else 0
-    if extent is None and n:  # data's readable extent: rec_off[0], rec_off[n] (device values)
-        extent = (_dptr(rec_off), _dptr(rec_off) + 8 * n)
+    pend: list = []  # every level's device list sizes, read back together
+    cur = stream if stream is not None else torch.cuda.current_stream(codec.device)
+    lvl = _decode_level(codec, codec._ctx, schema, data, rec_off, rec_len, n, None, span, extent, cur, pend, [0])
+    sizes = torch.cat(pend).tolist() if pend else []  # the tree's one host read
+    out, st, fail = _finish_level(lvl, n, sizes)
+    return (out, st, fail) if with_fail else (out, st)
+
+
+@dataclass
+class _Level:
+    """A decode level queued on the device (_decode_level), to be cut to its sizes (_finish_level)."""
+    schema: FlatSchema
+    cols: list
+    st: torch.Tensor
+    fail: torch.Tensor
+    lk: list        # list-like field indices
+    at: int         # their (items, item bytes) pairs' position in the tree's size list
+    inner: dict     # message field index -> _Level
+
+
+def _decode_level(codec: Codec, ctx, schema: FlatSchema, data, rec_src, rec_len, ncap: int, n_dev, span: int, extent,
+                  stream, pend: list, fork: list) -> _Level:
+    """Queues one level over `ncap` records (n_dev: a device u64 address holding the real count,
+    <= ncap; None: ncap is the count) on `stream` with context `ctx` and, recursively, its message
+    fields' levels (two or more on branches, joined back before the statuses are folded in)."""
+    hs = stream.cuda_stream
+    in_place = rec_len is not None and ncap > 0
+    if extent is None and ncap:  # data's readable extent: rec_off[0], rec_off[n] (device values)
+        extent = (_dptr(rec_src), _dptr(rec_src) + 8 * ncap)
     cols, ptrs, caps, offs, items, ilens, icaps = [], [], [], [], [], [], []
     for f in schema.fields:
         if f.width:
-            c = torch.empty(max(1, n), dtype=DTYPE[f.kind], device=codec.device)
+            c = torch.empty(max(1, ncap), dtype=DTYPE[f.kind], device=codec.device)
             cols.append(c)
             ptrs.append(_dptr(c))
             caps.append(0)
@@ -253,12 +311,12 @@ def decode(codec: Codec, schema: FlatSchema, data: torch.Tensor, rec_off: torch.
             ilens.append(0)
             icaps.append(0)
         elif f.list_like:
-            icap = n if (f.kind == "message" and not f.repeated) else span // 4 + 1  # items hold a [u32 len] each
+            icap = ncap if (f.kind == "message" and not f.repeated) else span // 4 + 1  # items hold a [u32 len] each
             msg = f.kind == "message"  # items left in place: (offset into data, length)
             b = torch.empty(1 if msg else max(1, span), dtype=torch.uint8, device=codec.device)
             io = torch.empty(icap + 1, dtype=torch.int64, device=codec.device)
             il = torch.empty(max(1, icap), dtype=torch.int64, device=codec.device) if msg else None
-            rec = torch.empty(n + 1, dtype=torch.int64, device=codec.device)
+            rec = torch.empty(ncap + 1, dtype=torch.int64, device=codec.device)
             lc = ListColumn(b, io, rec)
             lc.item_len = il
             cols.append(lc)
@@ -270,7 +328,7 @@ def decode(codec: Codec, schema: FlatSchema, data: torch.Tensor, rec_off: torch.
             icaps.append(icap)
         else:
             b = torch.empty(max(1, span), dtype=torch.uint8, device=codec.device)
-            o = torch.empty(n + 1, dtype=torch.int64, device=codec.device)
+            o = torch.empty(ncap + 1, dtype=torch.int64, device=codec.device)
             cols.append((b, o))
             ptrs.append(_dptr(b))
             caps.append(span)
@@ -278,50 +336,80 @@ def decode(codec: Codec, schema: FlatSchema, data: torch.Tensor, rec_off: torch.
             items.append(0)
             ilens.append(0)
             icaps.append(0)
-    st = torch.empty(max(1, n), dtype=torch.uint8, device=codec.device)
-    fail = torch.empty(max(1, n), dtype=torch.uint8, device=codec.device)
+    st = torch.empty(max(1, ncap), dtype=torch.uint8, device=codec.device)
+    fail = torch.empty(max(1, ncap), dtype=torch.uint8, device=codec.device)
     cf = schema.c_fields()
     lists = schema.has_lists
-    hs = _stream_handle(codec.device, stream)
     lo, hi = extent if in_place else (0, 0)
-    _native.check(codec._lib.sym_flat_decode_ex2(codec._ctx, cf, len(schema.fields), n, _dptr(data) or 1,
-                                                _dptr(rec_off) or 1, _dptr(rec_len) if in_place else 0, lo, hi,
+    _native.check(codec._lib.sym_flat_decode_ex3(ctx, cf, len(schema.fields), ncap, n_dev, _dptr(data) or 1,
+                                                _dptr(rec_src) or 1, _dptr(rec_len) if in_place else 0, lo, hi,
                                                 _native.ptr_array(ptrs), _native.u64_array(caps),
                                                 _native.ptr_array(offs), _native.ptr_array(items) if lists else None,
                                                 _native.ptr_array(ilens) if lists else None,
                                                 _native.u64_array(icaps) if lists else None, _dptr(st), _dptr(fail),
-                                                hs), "sym_flat_decode_ex2")
-    # every list field's item count and item bytes in ONE read-back per level
+                                                hs), "sym_flat_decode_ex3")
     lk = [k for k, f in enumerate(schema.fields) if f.list_like]
-    sizes = {}
-    if lk and n:
-        sz = torch.empty(2 * len(lk), dtype=torch.int64, device=codec.device)
-        _native.check(codec._lib.sym_flat_list_sizes(codec._ctx, len(lk), n,
-                                                     _native.ptr_array([_dptr(cols[k].rec) for k in lk]),
-                                                     _native.ptr_array([_dptr(cols[k].item_off) for k in lk]),
-                                                     _native.u64_array([icaps[k] for k in lk]), _dptr(sz), hs),
-                      "sym_flat_list_sizes")
-        v = sz.tolist()
-        sizes = {k: (int(v[2 * i]), int(v[2 * i + 1])) for i, k in enumerate(lk)}
-    for k, f in enumerate(schema.fields):
-        if not f.list_like:
-            continue
+    lvl = _Level(schema, cols, st, fail, lk, sum(t.numel() for t in pend), {})
+    if not ncap:  # no records: empty inner levels
+        for k in lk:
+            if schema.fields[k].kind == "message":
+                lc = cols[k]
+                lvl.inner[k] = _decode_level(codec, ctx, schema.fields[k].message, data, lc.item_off[:0],
+                                             lc.item_len[:0], 0, None, span, extent, stream, pend, fork)
+        return lvl
+    if not lk:
+        return lvl
+    # every list field's item count and item bytes, on the device (read back with the whole tree's)
+    sz = torch.empty(2 * len(lk), dtype=torch.int64, device=codec.device)
+    _native.check(codec._lib.sym_flat_list_sizes2(ctx, len(lk), ncap, n_dev,
+                                                  _native.ptr_array([_dptr(cols[k].rec) for k in lk]),
+                                                  _native.ptr_array([_dptr(cols[k].item_off) for k in lk]),
+                                                  _native.u64_array([icaps[k] for k in lk]), _dptr(sz), hs),
+                  "sym_flat_list_sizes2")
+    pend.append(sz)
+    msg = [(i, k) for i, k in enumerate(lk) if schema.fields[k].kind == "message"]
+    runs = [(ctx, stream)]
+    for _ in msg[1:]:  # branches start after this level's kernels (they read sz and the item tables)
+        b_ctx, b_st = codec.branch(fork[0])
+        fork[0] += 1
+        b_st.wait_stream(stream)
+        runs.append((b_ctx, b_st))
+    for (r_ctx, r_st), (i, k) in zip(runs, msg):
         lc = cols[k]
-        m, nb = sizes.get(k, (0, 0))
-        if f.kind == "message":
-            # the items are the inner records, in place in `data`: decode them, fold their statuses in
-            inner_cols, inner_st = decode(codec, f.message, data, lc.item_off[:m], stream=stream, span=span,
-                                          rec_len=lc.item_len[:m], extent=extent)
-            if n:
-                _native.check(codec._lib.sym_flat_nested_status(codec._ctx, cf, len(schema.fields), k, n,
-                                                                 _dptr(lc.rec), _dptr(inner_st) or 1, _dptr(st),
-                                                                 _dptr(fail), hs), "sym_flat_nested_status")
-            cols[k] = MessageColumn(inner_cols, lc.rec, inner_st, m)
+        # the items are the inner records, in place in `data`: their count is sz[2i] on the device
+        lvl.inner[k] = _decode_level(codec, r_ctx, schema.fields[k].message, data, lc.item_off, lc.item_len, icaps[k],
+                                     _dptr(sz) + 16 * i, span, extent, r_st, pend, fork)
+    for _, r_st in runs[1:]:
+        stream.wait_stream(r_st)
+    if lvl.inner:  # the inner statuses folded into this level's, every message field in one launch
+        ks = sorted(lvl.inner)
+        _native.check(codec._lib.sym_flat_nested_status2(
+            ctx, cf, len(schema.fields), len(ks), (ctypes.c_int * len(ks))(*ks), ncap, n_dev,
+            _native.ptr_array([_dptr(cols[k].rec) for k in ks]),
+            _native.ptr_array([_dptr(lvl.inner[k].st) or 1 for k in ks]), _dptr(st), _dptr(fail), hs),
+            "sym_flat_nested_status2")
+    return lvl
+
+
+def _finish_level(lvl: _Level, n: int, sizes: list):
+    """The level's columns cut to its n records and its lists' sizes -> (cols, status, fail)."""
+    cols = list(lvl.cols)
+    for i, k in enumerate(lvl.lk):
+        m, nb = (int(sizes[lvl.at + 2 * i]), int(sizes[lvl.at + 2 * i + 1])) if n else (0, 0)
+        lc = cols[k]
+        if k in lvl.inner:
+            inner_cols, inner_st, _ = _finish_level(lvl.inner[k], m, sizes)
+            cols[k] = MessageColumn(inner_cols, lc.rec[:n + 1], inner_st, m)
             continue
         lc.item_off = lc.item_off[:m + 1]
         lc.bytes = lc.bytes[:nb if m else 0]
-    out = [c[:n] if isinstance(c, torch.Tensor) else c for c in cols]
-    return (out, st[:n], fail[:n]) if with_fail else (out, st[:n])
+        lc.rec = lc.rec[:n + 1]
+    for k, c in enumerate(cols):
+        if isinstance(c, torch.Tensor):
+            cols[k] = c[:n]
+        elif isinstance(c, tuple):
+            cols[k] = (c[0], c[1][:n + 1])
+    return cols, lvl.st[:n], lvl.fail[:n]
 
 
 def _c_fields(fields):

@@ -433,6 +433,8 @@ int sym_decrypt(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_off, ui
 #define SYM_MAX_FLAT_FIELDS 16
 #define SYM_FIELD_REPEATED 0x80 /* or'ed into sym_field.width: repeated fixed-width field */
 #define SYM_FIELD_MESSAGE 0x40  /* nested message; | SYM_FIELD_REPEATED: repeated message (sym_flat_*_ex) */
+#define SYM_FIELD_FRAMED 0x20   /* | SYM_FIELD_MESSAGE, encode: the items already carry their [u32 len] (the
+                                   inner level was encoded with framed output, sym_flat_encode_ex2) */
 
 typedef struct sym_field {
     uint8_t segment; /* SYM_SEGMENT_PUBLIC / SYM_SEGMENT_PRIVATE */
@@ -484,12 +486,27 @@ uint64_t sym_flat_encoded_size(const sym_field* fields, int nfields, uint64_t n,
  *                    d_recs[i], n + 1 entries; item offsets d_items[i], item_caps[i] + 1): item count
  *                    m_i = d_recs[i][n] - d_recs[i][0] (clamped to item_caps[i]) and item bytes
  *                    d_items[i][m_i] into d_out[2i], d_out[2i + 1] (device memory), in one launch,
- *                    so a host walking a message tree reads back one small array per level. */
+ *                    so a host walking a message tree reads back one small array per level.
+ *   sym_flat_decode_ex3 / sym_flat_nested_status2 / sym_flat_list_sizes2  the same three with the
+ *                    record count on the device: d_n (nullable) holds it, n is its capacity (an inner
+ *                    level of a tree walk, whose count is the outer level's item count from
+ *                    sym_flat_list_sizes2, d_out[2i]).  Columns are sized for the capacity; every
+ *                    launch strides over the tiles of the count, so a tree decodes with no host read
+ *                    until its end (arpc_amd/flat.py reads all levels' sizes back at once).
+ *                    sym_flat_nested_status2 folds nk message fields ks[q] (item ranges
+ *                    d_rec_items[q], statuses d_item_status[q]) in one launch. */
 uint64_t sym_flat_encoded_size_ex(const sym_field* fields, int nfields, uint64_t n, const uint64_t* bytes,
                                   const uint64_t* items);
 int sym_flat_encode_ex(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const void* const* d_cols,
                        const uint64_t* const* d_offs, const uint64_t* const* d_items, uint32_t service_id,
                        uint32_t method_id, uint8_t* d_out, uint64_t* d_out_off, void* stream);
+/* sym_flat_encode_ex2: as sym_flat_encode_ex; framed != 0 writes each record as [u32 size][record] (what
+ * the outer level's body holds for one item: d_out_off are the frames' offsets, 4n more bytes), so an
+ * outer message field takes the items with SYM_FIELD_FRAMED and its bodies become one window each
+ * ([u32 count] and the items' frames for a repeated field; the frame for a nested one). */
+int sym_flat_encode_ex2(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const void* const* d_cols,
+                        const uint64_t* const* d_offs, const uint64_t* const* d_items, uint32_t service_id,
+                        uint32_t method_id, int framed, uint8_t* d_out, uint64_t* d_out_off, void* stream);
 int sym_flat_decode_ex(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const uint8_t* d_in,
                        const uint64_t* d_rec_off, void* const* d_cols, const uint64_t* caps, uint64_t* const* d_offs,
                        uint64_t* const* d_items, const uint64_t* item_caps, uint8_t* d_status, uint8_t* d_fail,
@@ -504,6 +521,16 @@ int sym_flat_nested_status(sym_ctx* ctx, const sym_field* fields, int nfields, i
                            uint8_t* d_fail, void* stream);
 int sym_flat_list_sizes(sym_ctx* ctx, int nl, uint64_t n, const uint64_t* const* d_recs,
                         const uint64_t* const* d_items, const uint64_t* item_caps, uint64_t* d_out, void* stream);
+int sym_flat_decode_ex3(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const uint64_t* d_n,
+                        const uint8_t* d_in, const uint64_t* d_rec_src, const uint64_t* d_rec_len,
+                        const uint64_t* d_lo, const uint64_t* d_hi, void* const* d_cols, const uint64_t* caps,
+                        uint64_t* const* d_offs, uint64_t* const* d_items, uint64_t* const* d_item_len,
+                        const uint64_t* item_caps, uint8_t* d_status, uint8_t* d_fail, void* stream);
+int sym_flat_nested_status2(sym_ctx* ctx, const sym_field* fields, int nfields, int nk, const int* ks, uint64_t n,
+                            const uint64_t* d_n, const uint64_t* const* d_rec_items,
+                            const uint8_t* const* d_item_status, uint8_t* d_status, uint8_t* d_fail, void* stream);
+int sym_flat_list_sizes2(sym_ctx* ctx, int nl, uint64_t n, const uint64_t* d_n, const uint64_t* const* d_recs,
+                         const uint64_t* const* d_items, const uint64_t* item_caps, uint64_t* d_out, void* stream);
 
 /* ---- Batched Raw setters ----------------------------------------------------
  * XxxRaw.SetF(v_i) on buffer i of a flat schema (generator main.go:1038-1093 assertions,
