@@ -59,7 +59,7 @@ enum SlotState { kFree = 0, kClosed = 1, kRunning = 2, kDone = 3 };
 
 struct BSlot {
     char* pin = nullptr;  // hipHostMalloc'd: the kernels read and write it in place
-    // encode: inputs fixed / offs / bytes, outputs rec (stream) / rec_off, per-record ids
+    // encode: inputs fixed / offs / bytes, outputs rec (stream) / rec_off (the IDs are patched at copy-out)
     // decode: inputs rec / rec_off, outputs status / fixed / offs / bytes
     int32_t* fixed[symhip::kMaxFixed] = {};
     uint64_t* offs[symhip::kMaxVar] = {};
@@ -67,7 +67,6 @@ struct BSlot {
     uint8_t* rec = nullptr;
     uint64_t* rec_off = nullptr;
     uint8_t* status = nullptr;
-    uint32_t* ids = nullptr;  // [2 * R]: service_id, method_id of each record (encode)
     uint64_t n = 0;
     uint64_t used = 0;  // record bytes in the batch (encode: encoded sizes; decode: input bytes)
     int state = kFree;
@@ -135,8 +134,6 @@ int slot_alloc(sym_batcher* b, int dir, BSlot& s) {
     o = a256(o + 8 * (R + 1));
     const size_t at_status = o;
     o = a256(o + R);
-    const size_t at_ids = o;
-    o = a256(o + 8 * R);
     hipError_t e = hipHostMalloc((void**)&s.pin, o, hipHostMallocDefault);
     if (e != hipSuccess) return fail(SYM_ERR_NOMEM, "sym_batcher_create: %zu pinned bytes: %s", o, hipGetErrorString(e));
     memset(s.pin, 0, o);
@@ -148,7 +145,6 @@ int slot_alloc(sym_batcher* b, int dir, BSlot& s) {
     s.rec = (uint8_t*)(s.pin + at_rec);
     s.rec_off = (uint64_t*)(s.pin + at_roff);
     s.status = (uint8_t*)(s.pin + at_status);
-    s.ids = (uint32_t*)(s.pin + at_ids);
     (void)dir;
     return SYM_OK;
 }
@@ -483,8 +479,6 @@ int sym_batcher_encode_one(sym_batcher* b, const int32_t* fixed, const uint8_t* 
         if (lens[f]) memcpy(s.bytes[f] + at, fields[f], lens[f]);
         s.offs[f][i + 1] = at + lens[f];
     }
-    s.ids[2 * i] = service_id;
-    s.ids[2 * i + 1] = method_id;
     s.used += size;
     await(b, 0, lk, s);
     const int rc = s.rc;

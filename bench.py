@@ -211,7 +211,7 @@ def decode_kernel_name(s, mixed: bool = False) -> str:
 
 
 ENCODE_KERNEL = "encode_kernel<0, 2, 1, false, 4, false, 64>"
-ENCODE_MIXED_KERNEL = "encode_pipe_kernel<false, 1>"
+ENCODE_MIXED_KERNEL = "encode_pipe_kernel<false, 1, 64>"
 
 
 def load_traffic(kernel: str, workload: str):
