@@ -150,6 +150,21 @@ def encode(codec: Codec, schema: FlatSchema, cols: list, service_id: int = 0, me
     return buf[:size], off
 
 
+_BRANCH_MIN = 1 << 16  # records of a level below which its subtrees stay on its stream (forks cost host time)
+
+
+def _rows(cols: list, schema: FlatSchema) -> int:
+    """A level's record count as far as the host knows it (column sizes, no device read)."""
+    for f, c in zip(schema.fields, cols):
+        if isinstance(c, MessageColumn) or isinstance(c, ListColumn):
+            return c.rec.numel() - 1
+        if isinstance(c, tuple):
+            return c[1].numel() - 1
+        if isinstance(c, torch.Tensor):
+            return c.numel()
+    return 0
+
+
 def _encode(codec: Codec, ctx, schema: FlatSchema, cols: list, service_id: int, method_id: int, stream, n, out,
             framed: bool, keep: list, fork: list):
     """encode() without the final read-back: the output buffer is sized from the columns' tensor
@@ -173,12 +188,13 @@ def _encode(codec: Codec, ctx, schema: FlatSchema, cols: list, service_id: int, 
     # independent subtrees: the first on this stream, the others on branches that start after this
     # stream's work so far and are joined back before this level's kernel
     runs = [(ctx, stream)]
-    for _ in msg[1:]:
+    for _ in (msg[1:] if _rows(cols, schema) >= _BRANCH_MIN else []):
         b_ctx, b_st = codec.branch(fork[0])
         fork[0] += 1
         b_st.wait_stream(stream)
         runs.append((b_ctx, b_st))
     inner = {}
+    runs += [(ctx, stream)] * (len(msg) - len(runs))  # small levels: every subtree on this stream
     for (r_ctx, r_st), k in zip(runs, msg):
         c = cols[k]
         # a fieldless inner schema needs its record count: the one host read of a level
@@ -369,11 +385,12 @@ def _decode_level(codec: Codec, ctx, schema: FlatSchema, data, rec_src, rec_len,
     pend.append(sz)
     msg = [(i, k) for i, k in enumerate(lk) if schema.fields[k].kind == "message"]
     runs = [(ctx, stream)]
-    for _ in msg[1:]:  # branches start after this level's kernels (they read sz and the item tables)
+    for _ in (msg[1:] if ncap >= _BRANCH_MIN else []):  # branches start after this level's kernels
         b_ctx, b_st = codec.branch(fork[0])
         fork[0] += 1
         b_st.wait_stream(stream)
         runs.append((b_ctx, b_st))
+    runs += [(ctx, stream)] * (len(msg) - len(runs))  # small levels: every subtree on this stream
     for (r_ctx, r_st), (i, k) in zip(runs, msg):
         lc = cols[k]
         # the items are the inner records, in place in `data`: their count is sz[2i] on the device
