@@ -73,7 +73,7 @@ SIGNATURES = {
     "sym_flat_decode": (_int, [_ctx, _vp, _int, _u64, _u8p, _u64p, _vp, _vp, _vp, _u8p, _vp]),
     "sym_flat_encoded_size_ex": (_u64, [_vp, _int, _u64, _vp, _vp]),
     "sym_flat_encode_ex": (_int, [_ctx, _vp, _int, _u64, _vp, _vp, _vp, _u32, _u32, _u8p, _u64p, _vp]),
-    "sym_flat_encode_ex2": (_int, [_ctx, _vp, _int, _u64, _vp, _vp, _vp, _u32, _u32, _int, _u8p, _u64p, _vp]),
+    "sym_flat_encode_ex2": (_int, [_ctx, _vp, _int, _u64, _vp, _vp, _vp, _u32, _u32, _int, _u64, _u8p, _u64p, _vp]),
     "sym_flat_decode_ex": (_int, [_ctx, _vp, _int, _u64, _u8p, _u64p, _vp, _vp, _vp, _vp, _vp, _u8p, _u8p, _vp]),
     "sym_flat_decode_ex2": (_int, [_ctx, _vp, _int, _u64, _u8p, _u64p, _u64p, _u64p, _u64p, _vp, _vp, _vp, _vp, _vp,
                                    _vp, _u8p, _u8p, _vp]),

@@ -673,13 +673,14 @@ uint64_t sym_flat_encoded_size_ex(const sym_field* fields, int nfields, uint64_t
 int sym_flat_encode_ex(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const void* const* d_cols,
                        const uint64_t* const* d_offs, const uint64_t* const* d_items, uint32_t service_id,
                        uint32_t method_id, uint8_t* d_out, uint64_t* d_out_off, void* stream) {
-    return sym_flat_encode_ex2(ctx, fields, nfields, n, d_cols, d_offs, d_items, service_id, method_id, 0, d_out,
+    return sym_flat_encode_ex2(ctx, fields, nfields, n, d_cols, d_offs, d_items, service_id, method_id, 0, 0, d_out,
                                d_out_off, stream);
 }
 
 int sym_flat_encode_ex2(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const void* const* d_cols,
                         const uint64_t* const* d_offs, const uint64_t* const* d_items, uint32_t service_id,
-                        uint32_t method_id, int framed, uint8_t* d_out, uint64_t* d_out_off, void* stream) {
+                        uint32_t method_id, int framed, uint64_t string_bytes, uint8_t* d_out, uint64_t* d_out_off,
+                        void* stream) {
     if (!ctx) return fail(SYM_ERR_INVALID, "sym_flat_encode: ctx is NULL");
     int rc = flat_check("sym_flat_encode", fields, nfields, d_items != nullptr);
     if (rc != SYM_OK) return rc;
@@ -698,7 +699,8 @@ int sym_flat_encode_ex2(sym_ctx* ctx, const sym_field* fields, int nfields, uint
         return e == hipSuccess ? SYM_OK : hip_fail(e, "hipMemsetAsync");
     }
     hipError_t e = symhip::launch_flat_encode(fields, nfields, n, d_cols, d_offs, d_items, service_id, method_id,
-                                              framed != 0, d_out, d_out_off, ctx->err, (hipStream_t)stream);
+                                              framed != 0, string_bytes, d_out, d_out_off, ctx->err,
+                                              (hipStream_t)stream);
     return e == hipSuccess ? SYM_OK : hip_fail(e, "flat encode launch");
 }
 

@@ -180,6 +180,7 @@ def _encode(codec: Codec, ctx, schema: FlatSchema, cols: list, service_id: int, 
     if not schema.fields and n is None:
         raise ValueError(f"{schema.name}: a schema without fields needs the record count n")
     ptrs, offs, items, nbytes, nitems, n_arg = [], [], [], [], [], n
+    string_bytes = 0
     n = None if schema.fields else n
     msg = [k for k, f in enumerate(schema.fields) if f.kind == "message"]
     for k in msg:
@@ -232,6 +233,7 @@ def _encode(codec: Codec, ctx, schema: FlatSchema, cols: list, service_id: int, 
             _check_col(o, torch.int64, f.name + " offsets", codec.device)
             m = o.numel() - 1
             nbytes.append(b.numel())
+            string_bytes += b.numel()  # (the kernel's choice of windows per chunk: a size hint)
             nitems.append(0)
             ptrs.append(_dptr(b) or 1)
             offs.append(_dptr(o))
@@ -257,8 +259,8 @@ def _encode(codec: Codec, ctx, schema: FlatSchema, cols: list, service_id: int, 
     lists = schema.has_lists
     _native.check(codec._lib.sym_flat_encode_ex2(ctx, cf, len(schema.fields), n, _native.ptr_array(ptrs),
                                                 _native.ptr_array(offs), _native.ptr_array(items) if lists else None,
-                                                service_id, method_id, 1 if framed else 0, _dptr(out), _dptr(off),
-                                                stream.cuda_stream), "sym_flat_encode_ex2")
+                                                service_id, method_id, 1 if framed else 0, string_bytes, _dptr(out),
+                                                _dptr(off), stream.cuda_stream), "sym_flat_encode_ex2")
     return out, off
 
 

@@ -503,10 +503,13 @@ int sym_flat_encode_ex(sym_ctx* ctx, const sym_field* fields, int nfields, uint6
 /* sym_flat_encode_ex2: as sym_flat_encode_ex; framed != 0 writes each record as [u32 size][record] (what
  * the outer level's body holds for one item: d_out_off are the frames' offsets, 4n more bytes), so an
  * outer message field takes the items with SYM_FIELD_FRAMED and its bodies become one window each
- * ([u32 count] and the items' frames for a repeated field; the frame for a nested one). */
+ * ([u32 count] and the items' frames for a repeated field; the frame for a nested one).
+ * string_bytes: the caller's estimate of the string / bytes fields' payload bytes (0: unknown); a
+ * level of short strings is then written with more payload windows per 16-byte chunk. */
 int sym_flat_encode_ex2(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const void* const* d_cols,
                         const uint64_t* const* d_offs, const uint64_t* const* d_items, uint32_t service_id,
-                        uint32_t method_id, int framed, uint8_t* d_out, uint64_t* d_out_off, void* stream);
+                        uint32_t method_id, int framed, uint64_t string_bytes, uint8_t* d_out, uint64_t* d_out_off,
+                        void* stream);
 int sym_flat_decode_ex(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const uint8_t* d_in,
                        const uint64_t* d_rec_off, void* const* d_cols, const uint64_t* caps, uint64_t* const* d_offs,
                        uint64_t* const* d_items, const uint64_t* item_caps, uint8_t* d_status, uint8_t* d_fail,

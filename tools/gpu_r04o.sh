@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 4: flat decode: fused emit kernel (string gathers + list item passes of a level in one launch).
+# Round 4: flat encode: 4 payload windows per chunk for levels of short strings (string_bytes hint).
 set -u
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest tests/test_nested.py tests/test_boutique.py tests/test_flat.py tests/test_wide_schema_entry_points.py tests/test_raw_setters.py tests/test_raw_fields.py tests/test_reassembly.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r04o_tests.log 2>&1 || { echo TESTS FAILED; tail -30 gpurun_out/r04o_tests.log; exit 1; }
