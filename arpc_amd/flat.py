@@ -143,7 +143,7 @@ def encode(codec: Codec, schema: FlatSchema, cols: list, service_id: int = 0, me
     and the level waits for them all."""
     cur = stream if stream is not None else torch.cuda.current_stream(codec.device)
     keep: list = []  # every level's temporaries, alive until the tree is queued (see _encode)
-    buf, off = _encode(codec, codec._ctx, schema, cols, service_id, method_id, cur, n, out, False, keep, [0])
+    buf, off = _encode(codec, codec._ctx, schema, cols, service_id, method_id, cur, n, out, False, keep, [0, _BRANCH_MIN])
     if out is not None:
         return buf, off
     size = int(off[-1].item()) if off.numel() > 1 else 0
@@ -151,6 +151,7 @@ def encode(codec: Codec, schema: FlatSchema, cols: list, service_id: int = 0, me
 
 
 _BRANCH_MIN = 1 << 16  # records of a level below which its subtrees stay on its stream (forks cost host time)
+_NO_BRANCH = 1 << 62  # graph captures: every subtree on the capturing stream (see _capture)
 
 
 def _rows(cols: list, schema: FlatSchema) -> int:
@@ -189,7 +190,7 @@ def _encode(codec: Codec, ctx, schema: FlatSchema, cols: list, service_id: int, 
     # independent subtrees: the first on this stream, the others on branches that start after this
     # stream's work so far and are joined back before this level's kernel
     runs = [(ctx, stream)]
-    for _ in (msg[1:] if _rows(cols, schema) >= _BRANCH_MIN else []):
+    for _ in (msg[1:] if _rows(cols, schema) >= fork[1] else []):
         b_ctx, b_st = codec.branch(fork[0])
         fork[0] += 1
         b_st.wait_stream(stream)
@@ -290,7 +291,7 @@ def decode(codec: Codec, schema: FlatSchema, data: torch.Tensor, rec_off: torch.
         span = int(rec_off[-1].item() - rec_off[0].item()) if n else 0
     pend: list = []  # every level's device list sizes, read back together
     cur = stream if stream is not None else torch.cuda.current_stream(codec.device)
-    lvl = _decode_level(codec, codec._ctx, schema, data, rec_off, rec_len, n, None, span, extent, cur, pend, [0])
+    lvl = _decode_level(codec, codec._ctx, schema, data, rec_off, rec_len, n, None, span, extent, cur, pend, [0, _BRANCH_MIN])
     sizes = torch.cat(pend).tolist() if pend else []  # the tree's one host read
     out, st, fail = _finish_level(lvl, n, sizes)
     return (out, st, fail) if with_fail else (out, st)
@@ -387,7 +388,7 @@ def _decode_level(codec: Codec, ctx, schema: FlatSchema, data, rec_src, rec_len,
     pend.append(sz)
     msg = [(i, k) for i, k in enumerate(lk) if schema.fields[k].kind == "message"]
     runs = [(ctx, stream)]
-    for _ in (msg[1:] if ncap >= _BRANCH_MIN else []):  # branches start after this level's kernels
+    for _ in (msg[1:] if ncap >= fork[1] else []):  # branches start after this level's kernels
         b_ctx, b_st = codec.branch(fork[0])
         fork[0] += 1
         b_st.wait_stream(stream)
@@ -411,7 +412,8 @@ def _decode_level(codec: Codec, ctx, schema: FlatSchema, data, rec_src, rec_len,
 
 
 def _finish_level(lvl: _Level, n: int, sizes: list):
-    """The level's columns cut to its n records and its lists' sizes -> (cols, status, fail)."""
+    """The level's columns cut to its n records and its lists' sizes -> (cols, status, fail); the
+    level itself is left whole (a DecodeGraph cuts the same level after every replay)."""
     cols = list(lvl.cols)
     for i, k in enumerate(lvl.lk):
         m, nb = (int(sizes[lvl.at + 2 * i]), int(sizes[lvl.at + 2 * i + 1])) if n else (0, 0)
@@ -420,15 +422,104 @@ def _finish_level(lvl: _Level, n: int, sizes: list):
             inner_cols, inner_st, _ = _finish_level(lvl.inner[k], m, sizes)
             cols[k] = MessageColumn(inner_cols, lc.rec[:n + 1], inner_st, m)
             continue
-        lc.item_off = lc.item_off[:m + 1]
-        lc.bytes = lc.bytes[:nb if m else 0]
-        lc.rec = lc.rec[:n + 1]
+        cols[k] = ListColumn(lc.bytes[:nb if m else 0], lc.item_off[:m + 1], lc.rec[:n + 1])
     for k, c in enumerate(cols):
         if isinstance(c, torch.Tensor):
             cols[k] = c[:n]
         elif isinstance(c, tuple):
             cols[k] = (c[0], c[1][:n + 1])
     return cols, lvl.st[:n], lvl.fail[:n]
+
+
+_GRAPH_TRACE = bool(int(__import__("os").environ.get("SYMHIP_GRAPH_TRACE", "0")))
+
+
+def _capture(codec: Codec, run):
+    """run(stream) queued once on a side stream (its workspaces, branch contexts and streams
+    created), then captured as a HIP graph on that stream (torch.cuda.CUDAGraph: stream capture,
+    torch's graph pool holding every buffer the walk allocates) -> (graph, stream, run's result of
+    the capture).  Nothing in a tree walk syncs the host, so the whole walk is one graph.  The walk
+    is captured on one stream: with branch streams forked and joined inside the capture, ROCm 7.0's
+    hipStreamEndCapture crashes (tools/graph_stages.py, stage 5; `profiles/r04_graph_stages.txt`)."""
+    s = torch.cuda.Stream(codec.device)
+    s.wait_stream(torch.cuda.current_stream(codec.device))
+    run(s)
+    codec.check(s)
+    if _GRAPH_TRACE:
+        print("graph: warm-up run done", flush=True)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        res = run(s)
+    if _GRAPH_TRACE:
+        print("graph: captured", flush=True)
+    return g, s, res
+
+
+class EncodeGraph:
+    """encode() of one schema over bound input columns, captured once as a HIP graph and replayed:
+    one graph launch instead of the walk's ~50 kernel launches and its host work (the boutique
+    tree walk is launch-bound: its kernels take about half of an eager call).  The caller refills
+    the bound columns in place between calls (same shapes: the walk's grids and the output's
+    capacity follow the column sizes, as in encode()); every replay encodes their current contents.
+    The returned stream and offsets are the graph's own buffers, overwritten by the next replay.
+    The graph has its own Codec (contexts whose workspaces stay where the graph saw them)."""
+
+    def __init__(self, device, schema: FlatSchema, cols: list, service_id: int = 0, method_id: int = 0,
+                 n: int | None = None):
+        self.codec = Codec(device)
+        self.cols = cols
+
+        def run(s):
+            keep: list = []
+            res = _encode(self.codec, self.codec._ctx, schema, cols, service_id, method_id, s, n, None, False,
+                          keep, [0, _NO_BRANCH])
+            return res, keep
+        self.graph, self.stream, ((self.buf, self.off), self._keep) = _capture(self.codec, run)
+
+    def replay(self, stream=None):
+        """-> (stream uint8, offsets int64 [n+1]) of the bound columns' current contents; one host
+        read (the stream's length).  `stream` (default: the current one) is ordered after it."""
+        cur = stream if stream is not None else torch.cuda.current_stream(self.codec.device)
+        self.stream.wait_stream(cur)
+        self.graph.replay()
+        cur.wait_stream(self.stream)
+        with torch.cuda.stream(cur):
+            size = int(self.off[-1].item()) if self.off.numel() > 1 else 0
+        return self.buf[:size], self.off
+
+
+class DecodeGraph:
+    """decode() of one schema over bound input buffers (data, rec_off), captured once as a HIP graph
+    and replayed (see EncodeGraph).  Every level's columns are sized from n and `span` alone (inner
+    record counts stay on the device), so one graph decodes any batch of n records whose bytes fit
+    in `span`: the caller refills data and rec_off in place between calls.  Results are views of the
+    graph's own buffers, cut to the replay's sizes (one host read), overwritten by the next replay."""
+
+    def __init__(self, device, schema: FlatSchema, data: torch.Tensor, rec_off: torch.Tensor, span: int | None = None):
+        self.codec = Codec(device)
+        _check_col(data, torch.uint8, "data", self.codec.device)
+        _check_col(rec_off, torch.int64, "rec_off", self.codec.device)
+        self.n = n = rec_off.numel() - 1
+        self.data, self.rec_off = data, rec_off
+        span = data.numel() if span is None else span
+
+        def run(s):
+            pend: list = []
+            lvl = _decode_level(self.codec, self.codec._ctx, schema, data, rec_off, None, n, None, span, None, s,
+                                pend, [0, _NO_BRANCH])
+            return lvl, (torch.cat(pend) if pend else None)
+        self.graph, self.stream, (self._lvl, self._sizes) = _capture(self.codec, run)
+
+    def replay(self, stream=None, with_fail: bool = False):
+        """-> (cols, status) (with_fail: (cols, status, fail)) of the bound buffers' current contents."""
+        cur = stream if stream is not None else torch.cuda.current_stream(self.codec.device)
+        self.stream.wait_stream(cur)
+        self.graph.replay()
+        cur.wait_stream(self.stream)
+        with torch.cuda.stream(cur):
+            sizes = self._sizes.tolist() if self._sizes is not None else []
+        out, st, fail = _finish_level(self._lvl, self.n, sizes)
+        return (out, st, fail) if with_fail else (out, st)
 
 
 def _c_fields(fields):
