@@ -439,8 +439,10 @@ def _capture(codec: Codec, run):
     created), then captured as a HIP graph on that stream (torch.cuda.CUDAGraph: stream capture,
     torch's graph pool holding every buffer the walk allocates) -> (graph, stream, run's result of
     the capture).  Nothing in a tree walk syncs the host, so the whole walk is one graph.  The walk
-    is captured on one stream: with branch streams forked and joined inside the capture, ROCm 7.0's
-    hipStreamEndCapture crashes (tools/graph_stages.py, stage 5; `profiles/r04_graph_stages.txt`)."""
+    is captured on one stream: with branch streams forked and joined inside the capture this ROCm's
+    hipStreamEndCapture crashes -- the tree walk's forks (tools/graph_stages.py, stage 5), a fork of
+    a fork with torch ops alone (tools/graph_fork.py, stage 2; `profiles/r04_graph_fork.txt`), and
+    the walk with forks from the capturing stream only, one fork point open at a time."""
     s = torch.cuda.Stream(codec.device)
     s.wait_stream(torch.cuda.current_stream(codec.device))
     run(s)
@@ -457,8 +459,8 @@ def _capture(codec: Codec, run):
 
 class EncodeGraph:
     """encode() of one schema over bound input columns, captured once as a HIP graph and replayed:
-    one graph launch instead of the walk's ~50 kernel launches and its host work (the boutique
-    tree walk is launch-bound: its kernels take about half of an eager call).  The caller refills
+    one graph launch instead of the walk's kernel launches and its host work (the walk's Python,
+    the C-ABI calls and ~5 us of launch cost per kernel).  The caller refills
     the bound columns in place between calls (same shapes: the walk's grids and the output's
     capacity follow the column sizes, as in encode()); every replay encodes their current contents.
     The returned stream and offsets are the graph's own buffers, overwritten by the next replay.

@@ -497,6 +497,23 @@ def boutique_leg(codec: Codec, dev, reps: int, n: int = 1 << 18) -> dict:
 
     enc_ms, enc_all = timed(lambda: flat.encode(codec, sch, cols))
     dec_ms, dec_all = timed(lambda: flat.decode(codec, sch, data, off, span=data.numel()))
+    # the same two walks captured once as HIP graphs over the same buffers (flat.EncodeGraph /
+    # DecodeGraph) and replayed; checked against the eager results first
+    eg = flat.EncodeGraph(dev, sch, cols)
+    dg = flat.DecodeGraph(dev, sch, data, off)
+    gd, go = eg.replay()
+    gcols, gst = dg.replay()
+    gd2, go2 = flat.encode(codec, sch, gcols)
+    torch.cuda.synchronize()
+    eg.codec.check()
+    dg.codec.check()
+    g_ok = bool(torch.equal(gd, data)) and bool(torch.equal(go, off)) and bool(torch.equal(gd2, data)) \
+        and bool((gst == 0).all().item())
+    genc_ms, genc_all = timed(eg.replay)
+    gdec_ms, gdec_all = timed(dg.replay)
+    eg.codec.close()
+    dg.codec.close()
+    del eg, dg, gd, go, gcols, gst, gd2, go2
     sb = int(off[-1].item())
     msgs = 4 * n + 3 * inner  # PlaceOrderResponse, OrderResult, Money, Address; per item OrderItem, CartItem, Money
     return {"schema": sch.name, "records": n, "order_items": inner, "messages_per_batch": msgs, "stream_bytes": sb,
@@ -507,6 +524,10 @@ def boutique_leg(codec: Codec, dev, reps: int, n: int = 1 << 18) -> dict:
             "stream_gbps_encode": round(sb / (enc_ms * 1e-3) / 1e9, 1),
             "stream_gbps_decode": round(sb / (dec_ms * 1e-3) / 1e9, 1),
             "reference_readme_ns_per_op": {"write": 2079, "read": 2939},
+            "graph": {"round_trip_ok": g_ok, "encode_ms": round(genc_ms, 3), "decode_ms": round(gdec_ms, 3),
+                      "encode_ms_each": genc_all, "decode_ms_each": gdec_all,
+                      "note": "flat.EncodeGraph / DecodeGraph: each walk captured once as a HIP graph (one stream) "
+                              "over the same bound buffers and replayed; host clock around replay + its one read"},
             "note": "host clock around the whole tree call (one launch set per level, inner levels' counts on "
                     "the device, one read of all levels' sizes at the end; one untimed call first, median "
                     "of the rest); synthetic payloads, not the reference's trace"}

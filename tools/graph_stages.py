@@ -1,8 +1,9 @@
 """Which tree walks capture as a HIP graph: flat encode / decode, then the boutique encode without and
 with branch streams, each stage printed before it starts (a crash names its stage).  Its round-4 run
 (profiles/r04_graph_stages.txt) crashed in hipStreamEndCapture at stage 5, the only one whose walk
-forked branch streams inside the capture; captures now keep every subtree on the capturing stream
-(arpc_amd/flat.py _capture), and stage 5 is gone."""
+forked branch streams inside the capture (a fork of a fork crashes it with torch ops alone:
+tools/graph_fork.py); captures now keep every subtree on the capturing stream (arpc_amd/flat.py
+_capture), and stage 5 is gone."""
 from __future__ import annotations
 
 import os
