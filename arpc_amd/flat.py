@@ -457,7 +457,33 @@ def _capture(codec: Codec, run):
     return g, s, res
 
 
-class EncodeGraph:
+class _Replayed:
+    """A captured walk's replay, split in two so that many graphs can be queued before any result
+    is read: launch() queues the graph (ordered after `stream`, the current one by default, which
+    is ordered after it) and the copy of its sizes into pinned host memory; result() waits for that
+    copy alone."""
+
+    def _bind_sizes(self, sizes):
+        self._dev_sizes = sizes
+        self._host = torch.empty(sizes.numel(), dtype=torch.int64, pin_memory=True) if sizes is not None else None
+        self._done = torch.cuda.Event()
+
+    def launch(self, stream=None):
+        cur = stream if stream is not None else torch.cuda.current_stream(self.codec.device)
+        self.stream.wait_stream(cur)
+        self.graph.replay()
+        cur.wait_stream(self.stream)
+        if self._host is not None:
+            with torch.cuda.stream(cur):
+                self._host.copy_(self._dev_sizes, non_blocking=True)
+        self._done.record(cur)
+
+    def _sizes_read(self) -> list:
+        self._done.synchronize()
+        return self._host.tolist() if self._host is not None else []
+
+
+class EncodeGraph(_Replayed):
     """encode() of one schema over bound input columns, captured once as a HIP graph and replayed:
     one graph launch instead of the walk's kernel launches and its host work (the walk's Python,
     the C-ABI calls and ~5 us of launch cost per kernel).  The caller refills
@@ -477,20 +503,20 @@ class EncodeGraph:
                           keep, [0, _NO_BRANCH])
             return res, keep
         self.graph, self.stream, ((self.buf, self.off), self._keep) = _capture(self.codec, run)
+        self._bind_sizes(self.off[-1:] if self.off.numel() > 1 else None)
+
+    def result(self):
+        """-> (stream uint8, offsets int64 [n+1]) of the last launch()."""
+        sz = self._sizes_read()
+        return self.buf[:int(sz[0]) if sz else 0], self.off
 
     def replay(self, stream=None):
-        """-> (stream uint8, offsets int64 [n+1]) of the bound columns' current contents; one host
-        read (the stream's length).  `stream` (default: the current one) is ordered after it."""
-        cur = stream if stream is not None else torch.cuda.current_stream(self.codec.device)
-        self.stream.wait_stream(cur)
-        self.graph.replay()
-        cur.wait_stream(self.stream)
-        with torch.cuda.stream(cur):
-            size = int(self.off[-1].item()) if self.off.numel() > 1 else 0
-        return self.buf[:size], self.off
+        """launch() then result(): the bound columns' current contents encoded."""
+        self.launch(stream)
+        return self.result()
 
 
-class DecodeGraph:
+class DecodeGraph(_Replayed):
     """decode() of one schema over bound input buffers (data, rec_off), captured once as a HIP graph
     and replayed (see EncodeGraph).  Every level's columns are sized from n and `span` alone (inner
     record counts stay on the device), so one graph decodes any batch of n records whose bytes fit
@@ -510,18 +536,18 @@ class DecodeGraph:
             lvl = _decode_level(self.codec, self.codec._ctx, schema, data, rec_off, None, n, None, span, None, s,
                                 pend, [0, _NO_BRANCH])
             return lvl, (torch.cat(pend) if pend else None)
-        self.graph, self.stream, (self._lvl, self._sizes) = _capture(self.codec, run)
+        self.graph, self.stream, (self._lvl, sizes) = _capture(self.codec, run)
+        self._bind_sizes(sizes)
+
+    def result(self, with_fail: bool = False):
+        """-> (cols, status) (with_fail: (cols, status, fail)) of the last launch()."""
+        out, st, fail = _finish_level(self._lvl, self.n, self._sizes_read())
+        return (out, st, fail) if with_fail else (out, st)
 
     def replay(self, stream=None, with_fail: bool = False):
-        """-> (cols, status) (with_fail: (cols, status, fail)) of the bound buffers' current contents."""
-        cur = stream if stream is not None else torch.cuda.current_stream(self.codec.device)
-        self.stream.wait_stream(cur)
-        self.graph.replay()
-        cur.wait_stream(self.stream)
-        with torch.cuda.stream(cur):
-            sizes = self._sizes.tolist() if self._sizes is not None else []
-        out, st, fail = _finish_level(self._lvl, self.n, sizes)
-        return (out, st, fail) if with_fail else (out, st)
+        """launch() then result(): the bound buffers' current contents decoded."""
+        self.launch(stream)
+        return self.result(with_fail)
 
 
 def _c_fields(fields):

@@ -573,9 +573,40 @@ def boutique_payloads_leg(codec: Codec, dev, reps: int) -> dict:
 
     te = timed(lambda: [flat.encode(codec, s, cols, n=n) for s, n, cols in batches])
     td = timed(lambda: [flat.decode(codec, s, d, o, span=d.numel()) for (s, n, _), (d, o) in zip(batches, enc)])
+    # the same 30 walks each captured as a HIP graph (flat.EncodeGraph / DecodeGraph over the same
+    # buffers), all 30 launched before any result is read; checked against the eager results first
+    graphs = [(flat.EncodeGraph(dev, s, cols, n=n), flat.DecodeGraph(dev, s, d, o))
+              for (s, n, cols), (d, o) in zip(batches, enc)]
+    g_ok = True
+    for (s, n, _), (d, o), (eg, dg) in zip(batches, enc, graphs):
+        gd, go = eg.replay()
+        gcols, gst = dg.replay()
+        rd, ro = flat.encode(codec, s, gcols, n=n)
+        g_ok &= bool(torch.equal(gd, d)) and bool(torch.equal(go, o)) and bool(torch.equal(rd, d)) \
+            and bool((gst == 0).all().item())
+    torch.cuda.synchronize()
+    for eg, dg in graphs:
+        eg.codec.check()
+        dg.codec.check()
+
+    def replay_all(k):
+        for g in graphs:
+            g[k].launch()
+        for g in graphs:
+            g[k].result()
+    tge = timed(lambda: replay_all(0))
+    tgd = timed(lambda: replay_all(1))
+    for eg, dg in graphs:
+        eg.codec.close()
+        dg.codec.close()
+    del graphs
     return {"types": len(batches), "messages": nmsg, "stream_bytes": stream_b, "all_ok": ok,
             "encode_ms": round(te * 1e3, 3), "decode_ms": round(td * 1e3, 3),
             "encode_msg_per_s": round(nmsg / te), "decode_msg_per_s": round(nmsg / td),
+            "graph": {"all_ok": g_ok, "encode_ms": round(tge * 1e3, 3), "decode_ms": round(tgd * 1e3, 3),
+                      "encode_msg_per_s": round(nmsg / tge), "decode_msg_per_s": round(nmsg / tgd),
+                      "note": "each type's walk captured once as a HIP graph over the same buffers; all 30 "
+                              "launched, then their sizes read (host clock around both)"},
             "reference_readme_msg_per_s": {"write": 481109, "read": 340225},
             "note": "all 30 payload files, one batch per type (30 encode and 30 decode tree walks), host clock; "
                     "the reference README's numbers are Go, one message per call, one core"}
