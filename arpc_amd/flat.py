@@ -459,9 +459,8 @@ def _capture(codec: Codec, run):
 
 class _Replayed:
     """A captured walk's replay, split in two so that many graphs can be queued before any result
-    is read: launch() queues the graph (ordered after `stream`, the current one by default, which
-    is ordered after it) and the copy of its sizes into pinned host memory; result() waits for that
-    copy alone."""
+    is read: launch() queues the graph on `stream` (the current one by default) and the copy of its
+    sizes into pinned host memory; result() waits for that copy alone."""
 
     def _bind_sizes(self, sizes):
         self._dev_sizes = sizes
@@ -470,13 +469,11 @@ class _Replayed:
 
     def launch(self, stream=None):
         cur = stream if stream is not None else torch.cuda.current_stream(self.codec.device)
-        self.stream.wait_stream(cur)
-        self.graph.replay()
-        cur.wait_stream(self.stream)
-        if self._host is not None:
-            with torch.cuda.stream(cur):
+        with torch.cuda.stream(cur):  # a graph replays on the current stream, not the one it was captured on
+            self.graph.replay()
+            if self._host is not None:
                 self._host.copy_(self._dev_sizes, non_blocking=True)
-        self._done.record(cur)
+            self._done.record(cur)
 
     def _sizes_read(self) -> list:
         self._done.synchronize()
