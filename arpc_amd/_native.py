@@ -89,6 +89,7 @@ SIGNATURES = {
     "sym_batcher_encode_one": (_int, [_vp, _vp, _vp, _vp, _u32, _u32, _u8p, _u64, _u64p]),
     "sym_batcher_decode_one": (_int, [_vp, _u8p, _u64, _vp, _vp, _vp, _vp, _u8p]),
     "sym_batcher_stats": (_int, [_vp, _u64p, _u64p, _u64p, _u64p]),
+    "sym_batcher_quiesce": (_int, [_vp]),
     "sym_encrypt": (_int, [_ctx, _u8p, _u64p, _u64, ctypes.c_char_p, ctypes.c_char_p, _u8p, _u8p, _u64p, _u8p, _vp]),
     "sym_decrypt": (_int, [_ctx, _u8p, _u64p, _u64, ctypes.c_char_p, ctypes.c_char_p, _u8p, _u64p, _u8p, _vp]),
 }

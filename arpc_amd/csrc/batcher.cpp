@@ -27,9 +27,14 @@
 //
 // Records up to kRingRecordMax bytes (every kv / echo request an RPC carries in practice) take the
 // ring instead (record_worker.hip): no launch per record or batch, one persistent single-workgroup
-// worker per queue serving tickets in place in coherent pinned slots; a record is published with one
-// store, served within a few microseconds, and read back as soon as its own flag is set.  Larger
-// records keep the batched path above.  Both give the same bytes and statuses.
+// worker per device -- shared by every batcher on the device and both directions, each slot carrying
+// its record's direction and layout -- serving tickets in place in coherent pinned slots; a record is
+// published with one store, served within a few microseconds, and read back as soon as its own flag
+// is set.  One worker per device, not per batcher and direction: a persistent kernel holds the
+// hardware queue its stream maps to (GPU_MAX_HW_QUEUES, 4 by default), and a launch of another stream
+// on that queue waits behind it; the worker also hands over to a fresh launch every kLifeTicks (2 ms)
+// while busy, so such a launch (a batch of large records, a caller's own kernels) waits at most that
+// long.  Larger records keep the batched path above.  Both give the same bytes and statuses.
 #include <hip/hip_runtime.h>
 
 #include <immintrin.h>
@@ -78,16 +83,23 @@ struct BSlot {
     std::condition_variable cv;  // the slot's callers: DONE, or "lead me"
 };
 
-// The ring of one queue (record_worker.hpp): coherent mapped pinned memory, the callers' ticket
-// counter, and the worker's generation (relaunched under `mu` when one has exited).
+// The ring of one device (record_worker.hpp): coherent mapped pinned memory (the callers' ticket
+// counter in it), the worker's generation (relaunched under `mu` when one has exited), and the
+// batchers using it.
 struct Ring {
+    int device = 0;
+    int refs = 0;  // batchers on the device (under g_rings_mu)
+    bool id_used[symhip::kMaxBatchers] = {};  // batcher ids on the ring (under g_rings_mu)
     symhip::RingCtl* ctl = nullptr;
     uint8_t* slots = nullptr;
-    std::atomic<uint64_t> ticket{0};
     std::atomic<uint64_t> gen{0};
     std::mutex mu;
     hipStream_t stream = nullptr;
 };
+
+constexpr int kMaxDevices = 64;
+std::mutex g_rings_mu;
+Ring* g_rings[kMaxDevices] = {};
 
 struct Queue {
     sym_ctx* ctx = nullptr;
@@ -111,7 +123,10 @@ struct sym_batcher {
     uint64_t B = 0;  // record bytes per batch
     uint32_t wait_us = 0;
     Queue q[2];      // 0 encode, 1 decode
-    Ring ring[2];    // 0 encode, 1 decode: records up to kRingRecordMax bytes
+    Ring* ring = nullptr;  // the device's ring: records up to kRingRecordMax bytes
+    int bid = -1;          // this batcher's id on the ring (its records' kind; its pass counters)
+    uint64_t pass_base[2] = {};  // the ring's pass counters of this id when the batcher took it
+    std::atomic<uint64_t> ring_recs[2] = {};  // this batcher's ring records per direction
 };
 
 namespace {
@@ -265,48 +280,106 @@ void release(Queue& q, std::unique_lock<std::mutex>& lk, BSlot& s) {
 }
 
 // ---- the ring path (record_worker.hip) ----
-int ring_launch(sym_batcher* b, int dir, Ring& r, uint64_t gen) {
-    DeviceGuard g(b->device);
+int ring_launch(Ring& r, uint64_t gen) {
+    DeviceGuard g(r.device);
     if (g.err != hipSuccess) return hip_fail(g.err, "sym_batcher: hipSetDevice");
-    hipError_t e = symhip::launch_record_worker(r.ctl, r.slots, b->lay, dir, gen, r.stream);
+    hipError_t e = symhip::launch_record_worker(r.ctl, r.slots, gen, r.stream);
     return e == hipSuccess ? SYM_OK : hip_fail(e, "sym_batcher: record worker launch");
 }
 
-int ring_create(sym_batcher* b, int dir, Ring& r) {
-    DeviceGuard g(b->device);
-    if (g.err != hipSuccess) return hip_fail(g.err, "sym_batcher_create: hipSetDevice");
-    const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
-    hipError_t e = hipHostMalloc((void**)&r.ctl, sizeof(symhip::RingCtl), fl);
-    if (e == hipSuccess) e = hipHostMalloc((void**)&r.slots, (size_t)symhip::kRingSlots * symhip::kSlotBytes, fl);
-    if (e != hipSuccess) return fail(SYM_ERR_NOMEM, "sym_batcher_create: ring of %d slots: %s", symhip::kRingSlots,
-                                     hipGetErrorString(e));
-    memset(r.ctl, 0, sizeof(symhip::RingCtl));
-    memset(r.slots, 0, (size_t)symhip::kRingSlots * symhip::kSlotBytes);
-    for (int k = 0; k < symhip::kRingSlots; ++k)
-        ((symhip::SlotCtl*)(r.slots + (size_t)k * symhip::kSlotBytes))->turn = (uint64_t)k;
-    if ((e = hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking)) != hipSuccess)
-        return hip_fail(e, "sym_batcher_create: worker stream");
-    r.gen = 1;
-    return ring_launch(b, dir, r, 1);
-}
-
-void ring_destroy(Ring& r) {
-    if (r.ctl && r.stream) {  // tell the worker to leave, wait until it has
-        __atomic_store_n(&r.ctl->stop, 1, __ATOMIC_SEQ_CST);
+// Tell the worker to leave and wait until it has (r.mu held or no caller active); the next call
+// relaunches it.
+void ring_stop(Ring& r) {
+    if (!r.ctl || !r.stream) return;
+    __atomic_store_n(&r.ctl->stop, 1, __ATOMIC_SEQ_CST);
+    {
+        DeviceGuard g(r.device);
         (void)hipStreamSynchronize(r.stream);
     }
-    if (r.stream) (void)hipStreamDestroy(r.stream);
-    if (r.slots) (void)hipHostFree(r.slots);
-    if (r.ctl) (void)hipHostFree(r.ctl);
-    r.stream = nullptr;
-    r.slots = nullptr;
-    r.ctl = nullptr;
+    __atomic_store_n(&r.ctl->stop, 0, __ATOMIC_SEQ_CST);
 }
 
-// After a record is published: a worker that announced its exit (ctl->quit == its generation) and did
-// not see the record is replaced.  `waited`: the caller has waited long for its record -- a worker
-// that has gone (or whose launch ended) without serving it is replaced as well.
-int ring_ensure_worker(sym_batcher* b, int dir, Ring& r, bool waited) {
+void ring_destroy(Ring* r) {
+    ring_stop(*r);
+    DeviceGuard g(r->device);
+    if (r->stream) (void)hipStreamDestroy(r->stream);
+    if (r->slots) (void)hipHostFree(r->slots);
+    if (r->ctl) (void)hipHostFree(r->ctl);
+    delete r;
+}
+
+int ring_create(int device, Ring** out) {
+    Ring* r = new (std::nothrow) Ring;
+    if (!r) return fail(SYM_ERR_NOMEM, "sym_batcher_create: out of host memory");
+    r->device = device;
+    DeviceGuard g(device);
+    if (g.err != hipSuccess) {
+        delete r;
+        return hip_fail(g.err, "sym_batcher_create: hipSetDevice");
+    }
+    const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
+    hipError_t e = hipHostMalloc((void**)&r->ctl, sizeof(symhip::RingCtl), fl);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&r->slots, (size_t)symhip::kRingSlots * symhip::kSlotBytes, fl);
+    if (e != hipSuccess) {
+        ring_destroy(r);
+        return fail(SYM_ERR_NOMEM, "sym_batcher_create: ring of %d slots: %s", symhip::kRingSlots, hipGetErrorString(e));
+    }
+    memset(r->ctl, 0, sizeof(symhip::RingCtl));
+    memset(r->slots, 0, (size_t)symhip::kRingSlots * symhip::kSlotBytes);
+    for (int k = 0; k < symhip::kRingSlots; ++k)
+        ((symhip::SlotCtl*)(r->slots + (size_t)k * symhip::kSlotBytes))->turn = (uint64_t)k;
+    if ((e = hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking)) != hipSuccess) {
+        ring_destroy(r);
+        return hip_fail(e, "sym_batcher_create: worker stream");
+    }
+    r->gen = 1;
+    const int rc = ring_launch(*r, 1);
+    if (rc != SYM_OK) {
+        ring_destroy(r);
+        return rc;
+    }
+    *out = r;
+    return SYM_OK;
+}
+
+// The device's ring, created with its first batcher, and an id on it for batcher b.  The id's pass
+// counters are the worker's to write; the batcher counts from their value now (every record of the
+// id's previous owner was done before that batcher was destroyed; its pass's counter store follows
+// within microseconds).
+int ring_acquire(sym_batcher* b, int device) {
+    if (device < 0 || device >= kMaxDevices) return fail(SYM_ERR_INVALID, "sym_batcher_create: device %d", device);
+    std::lock_guard<std::mutex> lk(g_rings_mu);
+    if (!g_rings[device]) {
+        const int rc = ring_create(device, &g_rings[device]);
+        if (rc != SYM_OK) return rc;
+    }
+    Ring* r = g_rings[device];
+    int id = 0;
+    while (id < symhip::kMaxBatchers && r->id_used[id]) ++id;
+    if (id == symhip::kMaxBatchers)
+        return fail(SYM_ERR_INVALID, "sym_batcher_create: %d batchers on device %d already", symhip::kMaxBatchers, device);
+    r->id_used[id] = true;
+    ++r->refs;
+    b->ring = r;
+    b->bid = id;
+    for (int d = 0; d < 2; ++d) b->pass_base[d] = __atomic_load_n(&r->ctl->bpasses[id][d], __ATOMIC_ACQUIRE);
+    return SYM_OK;
+}
+
+// The device's last batcher stops the worker and frees the ring.
+void ring_release(Ring* r, int bid) {
+    std::lock_guard<std::mutex> lk(g_rings_mu);
+    if (bid >= 0) r->id_used[bid] = false;
+    if (--r->refs > 0) return;
+    g_rings[r->device] = nullptr;
+    ring_destroy(r);
+}
+
+// After a record is published: a worker that announced its exit (ctl->quit == its generation) is
+// replaced once it has gone.  `waited`: the caller has waited long for its record -- a worker whose
+// launch ended without serving it is replaced as well (a safety net: the announced exit serves every
+// record it owes, record_worker.hip).
+int ring_ensure_worker(Ring& r, bool waited) {
     const uint64_t gen = r.gen.load(std::memory_order_acquire);
     const uint64_t q = __atomic_load_n(&r.ctl->quit, __ATOMIC_SEQ_CST);
     bool gone = __atomic_load_n(&r.ctl->gone, __ATOMIC_ACQUIRE) == gen;
@@ -314,23 +387,23 @@ int ring_ensure_worker(sym_batcher* b, int dir, Ring& r, bool waited) {
     std::lock_guard<std::mutex> lk(r.mu);
     if (r.gen.load(std::memory_order_acquire) != gen) return SYM_OK;  // another caller relaunched it
     if (!gone && waited && q != gen) {  // a long wait: has the worker's launch ended anyway?
-        DeviceGuard g(b->device);
+        DeviceGuard g(r.device);
         const hipError_t e = hipStreamQuery(r.stream);
         if (e == hipErrorNotReady) return SYM_OK;
         if (e != hipSuccess) return hip_fail(e, "sym_batcher: record worker");
         gone = true;
     }
-    // the worker either takes the announcement back (it saw a record) or leaves
-    while (!gone && __atomic_load_n(&r.ctl->quit, __ATOMIC_ACQUIRE) == gen)
+    while (!gone) {  // announced: it serves what it owes, then leaves
+        _mm_pause();
         gone = __atomic_load_n(&r.ctl->gone, __ATOMIC_ACQUIRE) == gen;
-    if (!gone) return SYM_OK;
+    }
     r.gen.store(gen + 1, std::memory_order_release);
-    return ring_launch(b, dir, r, gen + 1);
+    return ring_launch(r, gen + 1);
 }
 
 // Spin until *p == want (a pause first, then yielding the CPU: there may be more callers than cores);
 // every ~10 ms make sure a worker runs.
-int ring_wait(sym_batcher* b, int dir, Ring& r, const uint64_t* p, uint64_t want) {
+int ring_wait(Ring& r, const uint64_t* p, uint64_t want) {
     for (uint64_t i = 0; __atomic_load_n(p, __ATOMIC_ACQUIRE) != want; ++i) {
         if (i < 256) {
             _mm_pause();
@@ -338,7 +411,7 @@ int ring_wait(sym_batcher* b, int dir, Ring& r, const uint64_t* p, uint64_t want
         }
         sched_yield();
         if ((i & 4095) == 0) {
-            const int rc = ring_ensure_worker(b, dir, r, true);
+            const int rc = ring_ensure_worker(r, true);
             if (rc != SYM_OK) return rc;
         }
     }
@@ -349,21 +422,22 @@ int ring_wait(sym_batcher* b, int dir, Ring& r, const uint64_t* p, uint64_t want
 // worker, `drain` the out area, free the slot.
 template <typename Fill, typename Drain>
 int ring_call(sym_batcher* b, int dir, uint64_t in_len, Fill&& fill, Drain&& drain) {
-    Ring& r = b->ring[dir];
-    const uint64_t t = r.ticket.fetch_add(1, std::memory_order_relaxed);
+    Ring& r = *b->ring;
+    const uint64_t t = __atomic_fetch_add(&r.ctl->ticket, 1, __ATOMIC_SEQ_CST);
     uint8_t* slot = r.slots + (size_t)(t % symhip::kRingSlots) * symhip::kSlotBytes;
     symhip::SlotCtl* sc = (symhip::SlotCtl*)slot;
-    int rc = ring_wait(b, dir, r, &sc->turn, t);
+    int rc = ring_wait(r, &sc->turn, t);
     if (rc != SYM_OK) return rc;
     fill(slot + symhip::kSlotInAt);
-    sc->in_len = in_len;
+    sc->in_len = in_len | symhip::slot_kind(dir, b->lay, b->bid);
     __atomic_store_n(&sc->req, t + 1, __ATOMIC_RELEASE);
     __atomic_fetch_add(&r.ctl->posted, 1, __ATOMIC_SEQ_CST);  // then look at quit (the worker's hand-shake)
-    rc = ring_ensure_worker(b, dir, r, false);
-    if (rc == SYM_OK) rc = ring_wait(b, dir, r, &sc->done, t + 1);
+    rc = ring_ensure_worker(r, false);
+    if (rc == SYM_OK) rc = ring_wait(r, &sc->done, t + 1);
     if (rc != SYM_OK) return rc;  // (the slot stays taken: the device failed)
     drain(slot + symhip::kSlotOutAt);
     __atomic_store_n(&sc->turn, t + symhip::kRingSlots, __ATOMIC_RELEASE);
+    b->ring_recs[dir].fetch_add(1, std::memory_order_relaxed);
     return SYM_OK;
 }
 
@@ -415,8 +489,8 @@ int sym_batcher_create(int device, int schema, uint32_t max_records, uint64_t ma
         }
         if (rc != SYM_OK) break;
         for (BSlot& s : q.slot) slot_reset(s, b->lay.nvar);
-        rc = ring_create(b, dir, b->ring[dir]);
     }
+    if (rc == SYM_OK) rc = ring_acquire(b, device);
     if (rc != SYM_OK) {
         sym_batcher_destroy(b);
         return rc;
@@ -427,7 +501,7 @@ int sym_batcher_create(int device, int schema, uint32_t max_records, uint64_t ma
 
 int sym_batcher_destroy(sym_batcher* b) {
     if (!b) return SYM_OK;
-    for (Ring& r : b->ring) ring_destroy(r);
+    if (b->ring) ring_release(b->ring, b->bid);
     for (Queue& q : b->q) destroy_queue(q);
     delete b;
     return SYM_OK;
@@ -561,14 +635,22 @@ int sym_batcher_stats(sym_batcher* b, uint64_t* enc_batches, uint64_t* enc_recor
     uint64_t v[4];
     for (int dir = 0; dir < 2; ++dir) {  // batches: the batched path's launches + the ring worker's passes
         std::lock_guard<std::mutex> lk(b->q[dir].mu);
-        const symhip::RingCtl* c = b->ring[dir].ctl;
-        v[2 * dir] = b->q[dir].batches + (c ? __atomic_load_n(&c->passes, __ATOMIC_ACQUIRE) : 0);
-        v[2 * dir + 1] = b->q[dir].records + (c ? __atomic_load_n(&c->served, __ATOMIC_ACQUIRE) : 0);
+        const uint64_t passes = b->ring ? __atomic_load_n(&b->ring->ctl->bpasses[b->bid][dir], __ATOMIC_ACQUIRE) : 0;
+        v[2 * dir] = b->q[dir].batches + (b->ring ? passes - b->pass_base[dir] : 0);
+        v[2 * dir + 1] = b->q[dir].records + b->ring_recs[dir].load(std::memory_order_relaxed);
     }
     if (enc_batches) *enc_batches = v[0];
     if (enc_records) *enc_records = v[1];
     if (dec_batches) *dec_batches = v[2];
     if (dec_records) *dec_records = v[3];
+    return SYM_OK;
+}
+
+int sym_batcher_quiesce(sym_batcher* b) {
+    if (!b || !b->ring) return fail(SYM_ERR_INVALID, "sym_batcher_quiesce: NULL batcher");
+    Ring& r = *b->ring;
+    std::lock_guard<std::mutex> lk(r.mu);  // no relaunch meanwhile
+    ring_stop(r);
     return SYM_OK;
 }
 

@@ -3,25 +3,28 @@
 // The reference calls Marshal / Unmarshal once per record from many goroutines at once
 // (pkg/rpc/client.go:233-310, :252; pkg/rpc/server.go:152 / :173; pkg/serializer/symphony.go:10-16).
 // A kernel launch plus a synchronisation per call costs ~10 us or more; here one small persistent
-// kernel (one workgroup per queue) serves the records in place in a ring of slots in pinned host
-// memory that is mapped into the GPU's address space and coherent both ways:
+// kernel per device (one workgroup, shared by every batcher on the device and both directions) serves
+// the records in place in a ring of slots in pinned host memory that is mapped into the GPU's address
+// space and coherent both ways:
 //
-//   caller   t = ticket++; wait until slot[t % kRingSlots].turn == t; write the record into the slot;
-//            store req = t + 1; posted += 1; if the worker announced that it is quitting, see that
-//            one runs (batcher.cpp); spin until done == t + 1; copy the result out; turn = t + kRingSlots
+//   caller   t = ticket++; wait until slot[t % kRingSlots].turn == t; write the record and its kind
+//            (direction, layout) into the slot; store req = t + 1; posted += 1; if the worker announced
+//            that it is quitting, see that the next one runs (batcher.cpp); spin until done == t + 1;
+//            copy the result out; turn = t + kRingSlots
 //   worker   poll `posted` (one 8-byte PCIe read) while cold; when it passed the records served -- or
-//            at once while hot (a record within the last 50 us) -- every lane of the first 256 looks at
-//            one slot of the window [e, e + kRingSlots) (req and in_len in one round trip) and the ready
-//            ones are served, one wave per record, 16 at once: the record is read into LDS with
-//            system-scope 8-byte loads and encoded or parsed there exactly as MarshalSymphony /
+//            at once while hot (a record within the last 50 us) -- every lane of the first kRingSlots
+//            looks at one slot of the window [e, e + kRingSlots) (req and in_len|kind in one round trip)
+//            and the ready ones are served, one wave per record, 16 at once: the record is read into
+//            LDS with system-scope 8-byte loads and encoded or parsed there exactly as MarshalSymphony /
 //            UnmarshalSymphony (kv.syn.go:611-745, echo.syn.go:111-263), each 8-byte word of the result
 //            built from LDS and written with a system-scope store, waited for, then done = t + 1
 //
-// The worker exits when told to (sym_batcher_destroy) or after kIdleTicks without a record; before it
-// exits it announces `quit` and looks at `posted` once more (a Dekker hand-shake with the callers,
-// who publish before they look at `quit`), so a record posted meanwhile is either served by this
-// worker or finds the announcement and has the caller launch the next one.  No wave waits on another
-// workgroup, and every wave reaches the exit.
+// The worker exits when told to (the device's last sym_batcher_destroy, sym_batcher_quiesce), after
+// kIdleTicks without a record, or after kLifeTicks of life (a persistent kernel holds its hardware
+// queue: with more streams than queues, a launch that shares the queue waits behind it, so a busy
+// worker hands over to a fresh launch that queues behind that launch).  The exit is announced and
+// the records owed are served first (worker_kernel), so no caller is left waiting.  No wave waits on
+// another workgroup, and every wave reaches the exit.
 #include <hip/hip_runtime.h>
 
 #include "../../include/symphony_hip.h"
@@ -45,9 +48,14 @@ struct alignas(16) Lds {
     u64 served[kRingSlots];  // served[t % kRingSlots] == t + 1: ticket t was served by a worker
     int list[kRingSlots];    // ready tickets of this pass (offsets from e)
     u32 len[kRingSlots];     // and their in_len
+    u32 kind[kRingSlots];    // and kind (slot_kind >> 32)
     int nlist;
-    int quit;                // 1: leave the loop
+    int owed;                // draining: ready tickets below t0 in this pass
+    int drain;               // 1: the exit is announced (serve what is owed, then leave)
     int hot;                 // 1: records came lately: look at the slots without waiting for `posted`
+    u64 t0;                  // draining: the ticket counter read after the announcement
+    u64 bp[2 * kMaxBatchers];         // ctl->bpasses, kept here (this worker is their only writer)
+    u32 bseen[2 * kMaxBatchers / 32]; // batcher-direction pairs with a record in this pass
 };
 
 __device__ __forceinline__ u32 rd32(const uint8_t* b, u64 q) {
@@ -184,7 +192,16 @@ __device__ void decode_one(const Layout lay, const uint8_t* in, u64 L, uint8_t* 
     });
 }
 
-__global__ __launch_bounds__(kThreads) void worker_kernel(RingCtl* ctl, uint8_t* slots, Layout lay, int dir, u64 gen) {
+// The exit (idle for kIdleTicks, busy for kLifeTicks, or told to stop) is announced, not taken at
+// once: `quit` = this generation, a system fence, then the callers' ticket counter T0 is read.  A
+// caller publishes its record (req, then posted) and only then looks at `quit` (sequentially
+// consistent on the host), so for each record either its caller sees the announcement -- and has
+// the next generation launched once this one is `gone` (batcher.cpp ring_ensure_worker) -- or this
+// worker sees its req in a later window scan, and such a record has a ticket below T0.  So the
+// worker keeps scanning until a pass finds no ready ticket below T0 in its window; a ready ticket
+// below T0 outside the window waits behind a lower one whose caller published after the
+// announcement, and the next generation serves both.
+__global__ __launch_bounds__(kThreads) void worker_kernel(RingCtl* ctl, uint8_t* slots, u64 gen) {
     __shared__ Lds S;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     u64 e = ld_sys(&ctl->e), nproc = ld_sys(&ctl->nproc);  // where the previous worker stopped
@@ -195,67 +212,68 @@ __global__ __launch_bounds__(kThreads) void worker_kernel(RingCtl* ctl, uint8_t*
         const u64 d = ld_sys(&sc->done);
         S.served[t % kRingSlots] = d == t + 1 ? t + 1 : 0;
     }
+    for (int k = tid; k < 2 * kMaxBatchers; k += kThreads) S.bp[k] = ld_sys(&ctl->bpasses[k >> 1][k & 1]);
     if (tid == 0) {
-        S.quit = 0;
+        S.drain = 0;
+        S.t0 = 0;
         S.hot = 0;
     }
     __syncthreads();
-    u64 progress = __builtin_amdgcn_s_memrealtime();  // when a record was last served (every thread)
+    const u64 born = __builtin_amdgcn_s_memrealtime();
+    u64 progress = born;  // when a record was last served (every thread)
     u64 served = tid == 0 ? ld_sys(&ctl->served) : 0, passes = tid == 0 ? ld_sys(&ctl->passes) : 0;
+    auto announce = [&]() {  // (thread 0)
+        st_sys(&ctl->quit, gen);
+        fence_sys();
+        S.t0 = ld_sys(&ctl->ticket);
+        S.drain = 1;
+    };
     for (;;) {
-        // ---- cold: wave 0, lane 0 waits for work on `posted` (one 8-byte PCIe read per look) ----
+        // ---- cold: thread 0 waits for work on `posted` (one 8-byte PCIe read per look) ----
+        if (tid < 2 * kMaxBatchers / 32) S.bseen[tid] = 0;
         if (tid == 0) {
             S.nlist = 0;
-            while (!S.hot) {
-                if (ld_sys(&ctl->stop)) {
-                    S.quit = 1;
-                    break;
-                }
+            S.owed = 0;
+            while (!S.drain && !S.hot) {
                 const u64 posted = ld_sys(&ctl->posted);
-                if (__builtin_amdgcn_s_memrealtime() - progress > kIdleTicks) {
-                    // Nothing served for a while: announce, then look once more.  A caller publishes and
-                    // then looks at `quit`, so either we see its record here or it sees the announcement
-                    // (batcher.cpp ensure_worker); a caller that still waits later finds `gone`.
-                    st_sys(&ctl->quit, gen);
-                    fence_sys();
-                    if (ld_sys(&ctl->posted) != posted) {
-                        st_sys(&ctl->quit, 0);
-                        progress = __builtin_amdgcn_s_memrealtime();
-                        continue;
-                    }
-                    S.quit = 1;
-                    break;
-                }
-                if (posted != nproc) break;  // published records not served yet
-                __builtin_amdgcn_s_sleep(10);
+                if (ld_sys(&ctl->stop) || __builtin_amdgcn_s_memrealtime() - progress > kIdleTicks) announce();
+                else if (posted != nproc) break;  // published records not served yet
+                else __builtin_amdgcn_s_sleep(10);
             }
+            if (!S.drain && (__builtin_amdgcn_s_memrealtime() - born > kLifeTicks || (S.hot && ld_sys(&ctl->stop))))
+                announce();
         }
         __syncthreads();
-        if (S.quit) break;
-        // ---- the window: which tickets are ready and not served yet (req and in_len in one round
-        // trip; hot, the stop flag with them) ----
+        // ---- the window: which tickets are ready and not served yet (req and in_len in one round trip) ----
+        const u64 t0 = S.t0;
+        const bool drain = S.drain;
         if (tid < kRingSlots) {
             const u64 t = e + (u64)tid;
             const SlotCtl* sc = (const SlotCtl*)(slots + (size_t)(t % kRingSlots) * kSlotBytes);
             const u64 rq = ld_sys(&sc->req), il = ld_sys(&sc->in_len);
-            const u64 stop = tid == 0 && S.hot ? ld_sys(&ctl->stop) : 0;
             if (S.served[t % kRingSlots] != t + 1 && rq == t + 1) {
                 const int k = atomicAdd(&S.nlist, 1);
                 S.list[k] = tid;
-                S.len[k] = (u32)min(il, (u64)kRingRecordMax);  // (the caller checked it)
+                S.len[k] = (u32)min(il & 0xffffffffull, (u64)kRingRecordMax);  // (the caller checked it)
+                S.kind[k] = (u32)(il >> 32);
+                const u32 bd = 2 * ((u32)(il >> 56) & 0xffu) + (u32)((il >> 32) & 1);  // batcher, direction
+                atomicOr(&S.bseen[bd >> 5], 1u << (bd & 31));
+                if (drain && t < t0) atomicAdd(&S.owed, 1);
             }
-            if (stop) S.quit = 1;
         }
         __syncthreads();
-        if (S.quit) break;
+        if (drain && S.owed == 0) break;  // every record this generation owes is served
         const int nl = S.nlist;
+        ++passes;
         for (int i = wave; i < nl; i += kWaves) {  // one wave per record
             const u64 t = e + (u64)S.list[i];
             uint8_t* slot = slots + (size_t)(t % kRingSlots) * kSlotBytes;
             SlotCtl* sc = (SlotCtl*)slot;
             uint8_t* in = S.in[wave];
             const u64 in_len = S.len[i];
-            if (dir == 0) {
+            const u32 kind = S.kind[i];
+            const Layout lay{(int)((kind >> 8) & 0xff), (int)((kind >> 16) & 0xff)};
+            if ((kind & 0xff) == 0) {
                 load_in(in, slot + kSlotInAt, sizeof(EncIn) + in_len, lane);
                 wave_sync();
                 encode_one(lay, in, slot + kSlotOutAt, lane);
@@ -267,6 +285,10 @@ __global__ __launch_bounds__(kThreads) void worker_kernel(RingCtl* ctl, uint8_t*
             if (lane == 0) st_sys(&sc->done, t + 1);  // after the wave's stores were performed
             wave_sync();  // the wave's in buffer is read before its next record overwrites it
         }
+        // the pass counters of the batchers served in this pass (issued after the records' done flags,
+        // not waited for: a caller may see its record done a few microseconds before its pass counts)
+        if (tid < 2 * kMaxBatchers && (S.bseen[tid >> 5] >> (tid & 31) & 1u))
+            st_sys(&ctl->bpasses[tid >> 1][tid & 1], ++S.bp[tid]);
         __syncthreads();
         // ---- served: advance the window over its served prefix ----
         for (int i = tid; i < nl; i += kThreads) {
@@ -282,10 +304,11 @@ __global__ __launch_bounds__(kThreads) void worker_kernel(RingCtl* ctl, uint8_t*
             if (tid == 0) {  // (stores only: the counters of earlier workers were read at the start)
                 served += (u64)nl;
                 st_sys(&ctl->served, served);
-                st_sys(&ctl->passes, ++passes);
+                st_sys(&ctl->passes, passes);
                 S.hot = 1;
             }
         } else {
+            --passes;
             if (tid == 0 && now - progress > kHotTicks) S.hot = 0;  // cold again: wait on `posted`
             __builtin_amdgcn_s_sleep(2);
         }
@@ -294,6 +317,7 @@ __global__ __launch_bounds__(kThreads) void worker_kernel(RingCtl* ctl, uint8_t*
     if (tid == 0) {  // where the next worker starts; then gone (the callers' hand-shake)
         st_sys(&ctl->e, e);
         st_sys(&ctl->nproc, nproc);
+        st_sys(&ctl->passes, passes);
         fence_sys();
         st_sys(&ctl->gone, gen);
     }
@@ -301,8 +325,8 @@ __global__ __launch_bounds__(kThreads) void worker_kernel(RingCtl* ctl, uint8_t*
 
 }  // namespace rw
 
-hipError_t launch_record_worker(RingCtl* ctl, uint8_t* slots, Layout lay, int dir, uint64_t gen, hipStream_t stream) {
-    hipLaunchKernelGGL(rw::worker_kernel, dim3(1), dim3(rw::kThreads), 0, stream, ctl, slots, lay, dir, (u64)gen);
+hipError_t launch_record_worker(RingCtl* ctl, uint8_t* slots, uint64_t gen, hipStream_t stream) {
+    hipLaunchKernelGGL(rw::worker_kernel, dim3(1), dim3(rw::kThreads), 0, stream, ctl, slots, (u64)gen);
     return hipGetLastError();
 }
 

@@ -1,5 +1,6 @@
 // record_worker.hpp -- the ring of record slots shared by batcher.cpp (host) and record_worker.hip
-// (the persistent per-record worker).  All of it lives in pinned host memory allocated coherent and
+// (the persistent per-record worker).  One ring and one worker per device, shared by every batcher
+// on it and both directions: each slot says what it holds (slot_kind).  All of it lives in pinned host memory allocated coherent and
 // mapped (hipHostMallocCoherent | hipHostMallocMapped): the callers write and read it with plain
 // stores / loads and C11 atomics, the worker with system-scope 8-byte atomics.
 #pragma once
@@ -11,7 +12,7 @@
 
 namespace symhip {
 
-constexpr int kRingSlots = 256;            // tickets in flight per queue (= the worker's window)
+constexpr int kRingSlots = 512;            // tickets in flight per device ring (= the worker's window)
 constexpr size_t kSlotBytes = 16384;       // one slot: control words, in area, out area
 constexpr size_t kSlotInAt = 64;
 constexpr size_t kSlotIn = 4096 - 64;      // in area bytes
@@ -20,22 +21,36 @@ constexpr size_t kSlotOut = kSlotBytes - kSlotOutAt;
 constexpr uint64_t kRingRecordMax = 4000;  // records (encode: field bytes; decode: record bytes) up to
                                            // this go through the ring; larger ones through batches
 constexpr uint64_t kIdleTicks = 2000000;   // 20 ms without a record (s_memrealtime, 100 MHz): the worker exits
+constexpr int kMaxBatchers = 256;         // batchers per device ring (their pass counters)
+constexpr uint64_t kLifeTicks = 200000;    // 2 ms: a busy worker hands over to a fresh launch, so work queued
+                                           // behind it on a shared hardware queue waits at most this long
 
-struct RingCtl {          // one per queue, written as commented
+struct RingCtl {          // one per device, written as commented
     uint64_t posted;      // callers: records published so far (atomic add after the slot's req store)
-    uint64_t stop;        // host: leave now (sym_batcher_destroy)
+    uint64_t stop;        // host: leave now (last sym_batcher_destroy of the device, sym_batcher_quiesce)
     uint64_t quit;        // worker: the generation that is about to exit (0: none)
     uint64_t gone;        // worker: the generation that has exited
     uint64_t e, nproc;    // worker, at exit: its window base and records served (the next one resumes)
-    uint64_t served;      // worker: records served so far, every pass (sym_batcher_stats)
-    uint64_t passes;      // worker: passes that served records, every pass (sym_batcher_stats)
+    uint64_t served;      // worker: records served so far, every pass
+    uint64_t passes;      // worker: passes that served records, every pass
+    uint64_t ticket;      // callers: the next ticket (atomic fetch-add); the worker reads it when it
+                          // announces its exit: every record it still owes has a smaller ticket
+    uint64_t bpasses[kMaxBatchers][2];  // worker: passes that served records of batcher id b, direction d
+                                        // (stored after those records' done flags; sym_batcher_stats)
 };
+
+// A record's kind, in the high half of SlotCtl::in_len: direction (0 encode, 1 decode), layout and
+// the batcher's id on the ring.
+constexpr uint64_t slot_kind(int dir, Layout lay, int bid) {
+    return ((uint64_t)dir | ((uint64_t)lay.nfixed << 8) | ((uint64_t)lay.nvar << 16) | ((uint64_t)bid << 24)) << 32;
+}
 
 struct SlotCtl {          // the first 64 bytes of a slot
     uint64_t req;         // caller: ticket + 1 once the in area is written
     uint64_t done;        // worker: ticket + 1 once the out area is written
     uint64_t turn;        // caller: the ticket that may use the slot next
-    uint64_t in_len;      // caller: encode: field bytes after EncIn; decode: record bytes
+    uint64_t in_len;      // caller: low half encode: field bytes after EncIn, decode: record bytes; high
+                          // half slot_kind()
     uint64_t pad[4];
 };
 
@@ -60,6 +75,6 @@ static_assert(sizeof(DecOut) <= kDecData, "DecOut layout");
 static_assert(kDecData + 2 * (kRingRecordMax + 16) <= kSlotOut, "decode out area");
 static_assert(sizeof(EncIn) + kRingRecordMax <= kSlotIn, "encode in area");
 
-hipError_t launch_record_worker(RingCtl* ctl, uint8_t* slots, Layout lay, int dir, uint64_t gen, hipStream_t stream);
+hipError_t launch_record_worker(RingCtl* ctl, uint8_t* slots, uint64_t gen, hipStream_t stream);
 
 }  // namespace symhip

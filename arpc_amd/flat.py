@@ -143,7 +143,12 @@ def encode(codec: Codec, schema: FlatSchema, cols: list, service_id: int = 0, me
     and the level waits for them all."""
     cur = stream if stream is not None else torch.cuda.current_stream(codec.device)
     keep: list = []  # every level's temporaries, alive until the tree is queued (see _encode)
-    buf, off = _encode(codec, codec._ctx, schema, cols, service_id, method_id, cur, n, out, False, keep, [0, _BRANCH_MIN])
+    fork_min = _fork_min(cur)
+    if out is None and fork_min == _NO_BRANCH:
+        raise ValueError("encode under a graph capture needs out=(buffer, offsets): the returned stream's length "
+                         "is a host read (or use EncodeGraph)")
+    buf, off = _encode(codec, codec._ctx, schema, cols, service_id, method_id, cur, n, out, False, keep,
+                       [0, fork_min])
     if out is not None:
         return buf, off
     size = int(off[-1].item()) if off.numel() > 1 else 0
@@ -152,6 +157,22 @@ def encode(codec: Codec, schema: FlatSchema, cols: list, service_id: int = 0, me
 
 _BRANCH_MIN = 1 << 16  # records of a level below which its subtrees stay on its stream (forks cost host time)
 _NO_BRANCH = 1 << 62  # graph captures: every subtree on the capturing stream (see _capture)
+
+
+def _capturing(stream) -> bool:
+    """Is `stream` being captured into a HIP graph (a caller's torch.cuda.graph or
+    hipStreamBeginCapture)?  torch asks hipStreamIsCapturing of the current stream."""
+    with torch.cuda.stream(stream):
+        return torch.cuda.is_current_stream_capturing()
+
+
+def _fork_min(stream) -> int:
+    """The walk's branch threshold on `stream`: no branches at all while it is captured.  This ROCm's
+    hipStreamEndCapture segfaults on a capture in which a stream forked from the capturing stream
+    forks again (DESIGN.md section 4 "Graph capture and branch streams": profiles/r04_graph_fork.txt,
+    r04_graph_stages.txt), and a tree of three message levels with two message fields each does exactly
+    that; one stream costs a captured walk nothing (a graph's launches are queued by the device)."""
+    return _NO_BRANCH if _capturing(stream) else _BRANCH_MIN
 
 
 def _rows(cols: list, schema: FlatSchema) -> int:
@@ -199,8 +220,14 @@ def _encode(codec: Codec, ctx, schema: FlatSchema, cols: list, service_id: int, 
     runs += [(ctx, stream)] * (len(msg) - len(runs))  # small levels: every subtree on this stream
     for (r_ctx, r_st), k in zip(runs, msg):
         c = cols[k]
-        # a fieldless inner schema needs its record count: the one host read of a level
-        m_in = (int(c.rec[-1].item() - c.rec[0].item()) if c.rec.numel() > 1 else 0) if not c.cols else None
+        # a fieldless inner schema needs its record count: the one host read of a level, which a
+        # graph capture cannot hold
+        m_in = None
+        if not c.cols:
+            if c.rec.numel() > 1 and _capturing(r_st):
+                raise ValueError(f"{schema.fields[k].name}: a nested message without fields needs a host read "
+                                 "of its item count, which a graph capture cannot hold; encode it eagerly")
+            m_in = int(c.rec[-1].item() - c.rec[0].item()) if c.rec.numel() > 1 else 0
         ib, io = _encode(codec, r_ctx, schema.fields[k].message, c.cols, 0, 0, r_st, m_in, None, True, keep, fork)
         inner[k] = ListColumn(ib, io, c.rec)
         keep.append(inner[k])
@@ -287,11 +314,15 @@ def decode(codec: Codec, schema: FlatSchema, data: torch.Tensor, rec_off: torch.
         if rec_len.numel() and (extent is None or span is None):
             raise ValueError("records in place need extent and span")
     n = rec_off.numel() - 1 if rec_len is None else rec_len.numel()
+    cur = stream if stream is not None else torch.cuda.current_stream(codec.device)
+    if _capturing(cur):
+        raise ValueError("decode cuts its columns to sizes read back from the device, which a graph capture "
+                         "cannot hold: capture it with DecodeGraph")
     if span is None:
         span = int(rec_off[-1].item() - rec_off[0].item()) if n else 0
     pend: list = []  # every level's device list sizes, read back together
-    cur = stream if stream is not None else torch.cuda.current_stream(codec.device)
-    lvl = _decode_level(codec, codec._ctx, schema, data, rec_off, rec_len, n, None, span, extent, cur, pend, [0, _BRANCH_MIN])
+    lvl = _decode_level(codec, codec._ctx, schema, data, rec_off, rec_len, n, None, span, extent, cur, pend,
+                        [0, _fork_min(cur)])
     sizes = torch.cat(pend).tolist() if pend else []  # the tree's one host read
     out, st, fail = _finish_level(lvl, n, sizes)
     return (out, st, fail) if with_fail else (out, st)

@@ -317,6 +317,13 @@ class BatchingSerializer:
                         "decode_batches": v[2].value, "decode_records": v[3].value}
         return out
 
+    def quiesce(self) -> None:
+        """Stop the device's ring worker now (sym_batcher_quiesce; the next call restarts it): before a
+        device-wide synchronisation that should not wait for its idle timeout."""
+        for b in list(self._batchers.values()):
+            _native.check(_native.lib().sym_batcher_quiesce(b), "sym_batcher_quiesce")
+            break  # one ring per device
+
     def close(self) -> None:
         with self._lock:
             for b in self._batchers.values():

@@ -7,6 +7,7 @@ buffer sets rotate so the 256 MiB Infinity Cache cannot serve a step from a prev
 one: step s encodes set s%4 and decodes the stream encoded two steps earlier.
 
   python bench.py [--gpus N --steps K --warmup W] [--config 2|3|4] [--records R]
+      (N > 1 without torchrun's env: bench.py starts the N rank processes itself, spawn_ranks)
   torchrun --nproc-per-node N bench.py --gpus N ...   (weak scaling, no data-path collective)
 
 Prints ONE JSON line on rank 0.  `value` = algorithmic GB/s over all ranks (SURVEY.md
@@ -49,23 +50,91 @@ def alg_bytes(n: int, nvar: int, var_total: int, stream_total: int) -> tuple[int
     return enc, dec
 
 
-def dist_setup():
-    """One process per GPU (torch.distributed.run env).  RCCL ("nccl") carries only the barrier and
-    the max-over-ranks of the elapsed time: the shards exchange no data.  SYMHIP_BENCH_ONE_GPU=1
-    (rehearsal on a 1-GPU box) puts every rank on device 0 and uses gloo for that control traffic."""
+def spawn_ranks(n: int, argv: list[str]) -> int:
+    """`python bench.py --gpus N` with no torch.distributed env: start N rank processes of this same
+    script (one per GPU, LOCAL_RANK = GPU index) with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR
+    127.0.0.1 / MASTER_PORT set, and wait for them.  The parent makes no HIP call (it only imports
+    torch, which does not initialise the GPU), so the children start on an untouched runtime; they are
+    child processes, not an exec.  Rank 0 prints the JSON line to the inherited stdout.  When a rank
+    fails the others are stopped (they would wait in the barrier forever) and its exit code returned."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), *argv], env=env,
+                                      start_new_session=True))
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            time.sleep(0.2)
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    for q in live:
+                        os.killpg(q.pid, signal.SIGTERM)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.wait()
+    return rc
+
+
+def dist_setup(launch_check: bool = False):
+    """One process per GPU (torch.distributed.run env, or spawn_ranks).  RCCL ("nccl") carries only the
+    barrier and the max-over-ranks of the elapsed time: the shards exchange no data.
+    SYMHIP_BENCH_ONE_GPU=1 (rehearsal on a 1-GPU box) puts every rank on device 0 and uses gloo for
+    that control traffic; so does --launch-check, which touches no GPU at all."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if os.environ.get("SYMHIP_BENCH_ONE_GPU") == "1":
+    one_gpu = os.environ.get("SYMHIP_BENCH_ONE_GPU") == "1"
+    if one_gpu:
         local = 0
     if world > 1:
         import torch.distributed as dist
+        if launch_check:
+            dist.init_process_group(backend="gloo")
+            return world, rank, local
         torch.cuda.set_device(local)
-        if os.environ.get("SYMHIP_BENCH_ONE_GPU") == "1":
+        if one_gpu:
             dist.init_process_group(backend="gloo")
         else:
             dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
     return world, rank, local
+
+
+def launch_check(args) -> None:
+    """--launch-check: the N-rank launch alone (no GPU, gloo): every rank joins the group, meets the
+    barrier, contributes its elapsed time to the max, and rank 0 prints the world it saw."""
+    world, rank, local = dist_setup(launch_check=True)
+    barrier(world)
+    t0 = time.perf_counter()
+    barrier(world)
+    el = max_over_ranks(time.perf_counter() - t0, world, None)
+    ranks = [rank]
+    if world > 1:
+        import torch.distributed as dist
+        got = [None] * world
+        dist.all_gather_object(got, (rank, local, os.getpid()))
+        ranks = got
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "gpus_requested": args.gpus,
+                          "ranks": ranks, "elapsed_max_s": el}), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
 
 
 def barrier(world):
@@ -174,13 +243,13 @@ def cpu_baseline(kw: dict, seconds: float) -> dict:
     m_ns, u_ns = oracle.bench_echo(2_000_000)
     gb = lambda reps, el: round((enc_b + dec_b) * reps / el / 1e9, 4)
     return {"value": gb(reps1, el1), "unit": "GB/s", "cores": 1, "kind": "port",
-            "mrecords_per_s": round(2 * b.n * reps1 / el1 / 1e6, 4),
+            "mrecords_per_s": round(b.n * reps1 / el1 / 1e6, 4),
             "all_cores": {"value": gb(repsN, elN), "cores": threads,
-                          "mrecords_per_s": round(2 * b.n * repsN / elN / 1e6, 4),
+                          "mrecords_per_s": round(b.n * repsN / elN / 1e6, 4),
                           "share_from": "cgroup cpu quota" if info["cgroup_cpu_quota"] else
                                         ("OMP_NUM_THREADS" if omp else "affinity")},
             "nproc_threads": {"value": gb(repsP, elP), "threads": nproc,
-                              "mrecords_per_s": round(2 * b.n * repsP / elP / 1e6, 4),
+                              "mrecords_per_s": round(b.n * repsP / elP / 1e6, 4),
                               "oversubscribed": bool(info["cgroup_cpu_quota"] and nproc > info["cgroup_cpu_quota"]),
                               "note": "nproc threads on the CPUs this process may use: above its cgroup quota they "
                                       "time-slice, so this row shows the quota's cap, not a baseline"},
@@ -825,7 +894,7 @@ def mixed_leg(codec: Codec, dev, reps: int, cfg=None) -> dict:
             "round_trip_ok": ok, "encode_ms": round(enc_ms, 4), "encode_gbps": round(enc_alg / enc_ms / 1e6, 1),
             "decode_ms": round(dec_ms, 4), "decode_gbps": round(dec_alg / dec_ms / 1e6, 1),
             "gbps_algorithmic": round((enc_alg + dec_alg) / (enc_ms + dec_ms) / 1e6, 1),
-            "mrecords_per_s": round(2 * n / (enc_ms + dec_ms) / 1e3, 1),
+            "mrecords_per_s": round(n / (enc_ms + dec_ms) / 1e3, 1),
             "note": "Get/Set mix at the trace_large.req ratio (9,267 SET / 25,125); encode = one launch (sizer "
                     "groups, scanner, encode tiles); client IDs: service 1, Get 1, Set 2"}
 
@@ -911,9 +980,17 @@ def main():
                     help="per-record Serializer path: records per timing run of tests/batcher_driver (0 = skip)")
     ap.add_argument("--ref-reps", type=int, default=-1,
                     help="decode reference timings (three-kernel, look-back only); -1 = max(5, steps/2), 0 = skip")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="exercise the N-rank launch only (gloo, no GPU) and print the world rank 0 saw")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    if args.launch_check:
+        return launch_check(args)
     world, rank, local = dist_setup()
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}; measuring {world} rank(s)", file=sys.stderr)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     kw = workload(args, world, rank)
@@ -1098,7 +1175,9 @@ def main():
                    + ", device-resident encode+decode",
                    "records_per_gpu": n, "global_records": n * world, "parallelism": f"shard{world}", "streams": 2 if args.overlap else 1,
                    "bytes_per_record_algorithmic": round((enc_b + dec_b) / n, 3)},
-        "mrecords_per_s": round(world * 2 * n * args.steps / elapsed / 1e6, 2),
+        "mrecords_per_s": round(world * n * args.steps / elapsed / 1e6, 2),
+        "mrecords_per_s_note": "records per second, each record encoded once and decoded once (record "
+                               "operations per second = 2x)",
         "wire_gbps": round(world * 2 * total * args.steps / elapsed / 1e9, 2),
         "kernels": {"encode": {"avg_ms": round(enc_ms, 4), "alg_bytes": enc_b,
                                "gbps": round(enc_b / enc_ms / 1e6, 1)},

@@ -214,21 +214,28 @@ int sym_decode_host(sym_ctx* ctx, int schema, uint64_t n, const uint8_t* h_in, c
  *   Unmarshal server receive loop      pkg/rpc/server.go:152, client response  client.go:205
  *   adapter                            pkg/serializer/symphony.go:10-16
  * A batcher serves those concurrent one-record calls without a launch per call.  Records of up to
- * 4000 bytes (encode: the fields' bytes; decode: the record) go through a ring of 256 slots in
- * coherent pinned host memory per direction: the caller writes its record into a slot and
- * publishes it, a persistent one-workgroup kernel of the batcher (started at creation, leaving
- * after 20 ms without records and restarted by the next call) serves whatever is published in
- * place and sets the slot's done flag, and the caller copies its result out -- a few microseconds
- * per call, many calls per pass under load.  Larger records join the open batch of their
+ * 4000 bytes (encode: the fields' bytes; decode: the record) go through a ring of 512 slots in
+ * coherent pinned host memory, one ring per DEVICE shared by all its batchers and both directions:
+ * the caller writes its record into a slot and publishes it, a persistent one-workgroup kernel
+ * (started with the device's first batcher; leaving after 20 ms without records and restarted by
+ * the next call) serves whatever is published in place and sets the slot's done flag, and the
+ * caller copies its result out -- a few microseconds per call, many calls per pass under load.
+ * Queue budget: that kernel holds one hardware queue of the process (GPU_MAX_HW_QUEUES, 4 by
+ * default) while it runs, and a launch of another stream that maps to the same queue waits behind
+ * it; so a busy worker hands over to a fresh launch every 2 ms, and such a launch (the caller's own
+ * kernels, hipDeviceSynchronize / torch.cuda.synchronize, a batch of large records) waits at most
+ * about that long.  sym_batcher_quiesce stops the worker at once (it returns when the worker has
+ * left; the next call restarts it), e.g. before a device-wide synchronisation.  Larger records join the open batch of their
  * direction and block; when no batch of that direction is on the GPU, one caller of the open batch
  * runs it (no extra thread): at once with max_wait_us = 0 -- under load a batch is whatever
  * arrived while the previous one ran -- else once it holds max_records records or max_bytes bytes
  * of records or its first record has waited max_wait_us; every caller then copies its own result
  * out.  All entry points are thread-safe.  The batcher owns two contexts on `device` (one per
- * direction), the two rings and their workers, and pinned staging that the batch kernels read and
+ * direction), a reference to the device's ring, and pinned staging that the batch kernels read and
  * write in place (mapped host memory), so one batch is one kernel launch and one stream
  * synchronisation.  Results are bit-identical to sym_encode / sym_decode of the same records.
- * sym_batcher_stats counts the ring workers' passes as batches.
+ * sym_batcher_stats counts the ring worker's passes that served this batcher's records as batches
+ * (in completion order: an upper bound).
  *   sym_batcher_encode_one  MarshalSymphony of one record + the client's ID patch of bytes [5:13]
  *                           (service_id / method_id; 0 / 0 = MarshalSymphony's own bytes):
  *                           fixed[nfixed] int32 values, fields[nvar] pointers with lens[nvar]; out
@@ -244,7 +251,9 @@ int sym_decode_host(sym_ctx* ctx, int schema, uint64_t n, const uint8_t* h_in, c
 typedef struct sym_batcher sym_batcher;
 int sym_batcher_create(int device, int schema, uint32_t max_records, uint64_t max_bytes, uint32_t max_wait_us,
                        sym_batcher** out);
-int sym_batcher_destroy(sym_batcher* b); /* no call may be in progress; stops the ring workers */
+int sym_batcher_destroy(sym_batcher* b); /* no call on b may be in progress; the device's last batcher stops
+                                          * the ring worker */
+int sym_batcher_quiesce(sym_batcher* b); /* stop the device's ring worker now; the next call restarts it */
 int sym_batcher_encode_one(sym_batcher* b, const int32_t* fixed, const uint8_t* const* fields, const uint64_t* lens,
                            uint32_t service_id, uint32_t method_id, uint8_t* out, uint64_t out_cap,
                            uint64_t* out_len);

@@ -236,3 +236,80 @@ def test_ring_path_limits_and_worker_relaunch(gpu):
     st = ser.stats()
     assert sum(v["decode_records"] for v in st.values()) >= 9
     ser.close()
+
+
+@pytest.mark.gpu
+def test_shared_worker_two_batchers_large_records_bounded_latency(gpu):
+    """two batchers (SetRequest and GetRequest) driven from many threads at once share
+    the device's one ring worker; meanwhile records over the ring limit take the batched path (their
+    own stream's launches) and torch launches and synchronises the device.  Neither may wait for the
+    worker's 20 ms idle timeout, which steady traffic never reaches: the worker hands over every 2 ms
+    (kLifeTicks).  Every result is checked against the oracle, and the slow paths' worst latency is
+    bounded well below what waiting for an idle worker under this traffic would cost (forever)."""
+    import time
+    from arpc_amd.serializer import BatchingSerializer, GetRequest, SetRequest
+    ser = BatchingSerializer(gpu, service_id=1, method_id=2, max_bytes=1 << 16)
+    stop = threading.Event()
+    errors, worst = [], {"large": 0.0, "sync": 0.0}
+    counts = [0] * 24
+
+    def small(t):
+        try:
+            rng = np.random.default_rng(100 + t)
+            while not stop.is_set():
+                if t % 2:
+                    m = GetRequest(rng.integers(0, 256, int(rng.integers(0, 64)), dtype=np.uint8).tobytes())
+                    want = bytearray(oracle.marshal([], [m.Key]))
+                else:
+                    m = SetRequest(rng.integers(0, 256, 32, dtype=np.uint8).tobytes(),
+                                   rng.integers(0, 256, int(rng.integers(0, 500)), dtype=np.uint8).tobytes())
+                    want = bytearray(oracle.marshal([], [m.Key, m.Value]))
+                want[5:13] = struct.pack("<II", 1, 2)
+                data = ser.marshal(m)
+                assert data == bytes(want)
+                out = type(m)()
+                ser.unmarshal(data, out)
+                assert out == m
+                counts[t] += 1
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+            stop.set()
+
+    def large():
+        try:
+            for k in range(20):
+                m = SetRequest(b"K" * 16, bytes((k + j) & 255 for j in range(6000 + 37 * k)))
+                t0 = time.perf_counter()
+                data = ser.marshal(m)
+                out = SetRequest()
+                ser.unmarshal(data, out)
+                worst["large"] = max(worst["large"], time.perf_counter() - t0)
+                assert out == m
+                x = torch.ones(1 << 16, device="cuda") * k  # torch's own launch + a device-wide sync
+                t0 = time.perf_counter()
+                torch.cuda.synchronize()
+                worst["sync"] = max(worst["sync"], time.perf_counter() - t0)
+                assert float(x[0].item()) == k
+                time.sleep(0.01)
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+        finally:
+            stop.set()
+
+    th = [threading.Thread(target=small, args=(t,)) for t in range(len(counts))] + [threading.Thread(target=large)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=150)
+    assert not any(x.is_alive() for x in th), "a caller hung"
+    assert not errors, errors[:3]
+    assert min(counts) > 0, counts  # the small-record traffic really ran throughout
+    assert worst["large"] < 0.5 and worst["sync"] < 0.5, worst
+    ser.quiesce()  # the worker leaves at once; the next call restarts it
+    t0 = time.perf_counter()
+    torch.cuda.synchronize()
+    assert time.perf_counter() - t0 < 0.1
+    out = GetRequest()
+    ser.unmarshal(ser.marshal(GetRequest(b"after")), out)
+    assert out.Key == b"after"
+    ser.close()

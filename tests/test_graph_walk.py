@@ -127,3 +127,46 @@ def test_graphs_flat_schema(codec, dev):
     assert bool((st == 0).all().item())
     for a, b in zip(dcols, cols):
         assert torch.equal(a, b)
+
+
+def test_user_capture_of_branching_encode(codec, dev):
+    """A caller's own torch.cuda.graph around the eager flat.encode of a tree whose levels are large
+    enough to fork branch streams (2^17 orders: OrderResult has three message fields, OrderItem two,
+    so the eager walk forks from a fork -- the topology this ROCm's hipStreamEndCapture segfaults on,
+    DESIGN.md section 4).  Under capture the walk takes no branches (flat._fork_min), the capture ends,
+    and the replay equals the eager (branching) encode byte for byte and the restatement per record."""
+    from arpc_amd import datagen, flat
+    from tests.test_nested import tree_records
+    sch = flat.OB_PLACE_ORDER_RESPONSE
+    n = 1 << 17
+    tree = datagen.ob_place_order(n, seed=17)
+    cols = flat.columns_from_tree(sch, tree[1], dev)
+    want, woff = flat.encode(codec, sch, cols)
+    torch.cuda.synchronize()
+    codec.check()
+    assert len(codec.__dict__.get("_branches", [])) >= 2  # the eager walk did fork, twice deep
+    buf = torch.empty(want.numel() + 64, dtype=torch.uint8, device=dev)
+    off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):  # warm-up on a side stream, as torch's graph docs prescribe
+        flat.encode(codec, sch, cols, out=(buf, off))
+    torch.cuda.current_stream(dev).wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        flat.encode(codec, sch, cols, out=(buf, off))
+    buf.zero_()
+    off.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    codec.check()
+    assert torch.equal(off, woff) and torch.equal(buf[:want.numel()], want)
+    recs = tree_records(sch, tree[1], n)
+    idx = np.random.default_rng(3).choice(n, 500, replace=False)
+    got = _records(buf, off, n)
+    assert [got[i] for i in idx] == [ref.marshal(sch, recs[i]) for i in idx]
+    with pytest.raises(ValueError):  # the walks that need a host read say so instead of breaking a capture
+        g2 = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g2):
+            flat.decode(codec, sch, want, woff)
