@@ -12,7 +12,7 @@
 //            that it is quitting, see that the next one runs (batcher.cpp); spin until done == t + 1;
 //            copy the result out; turn = t + kRingSlots
 //   worker   poll `posted` (one 8-byte PCIe read) while cold; when it passed the records served -- or
-//            at once while hot (a record within the last 50 us) -- every lane of the first kRingSlots
+//            at once while hot (a record within the last 50 us) -- every lane of the first kRingSlots (256)
 //            looks at one slot of the window [e, e + kRingSlots) (req and in_len|kind in one round trip)
 //            and the ready ones are served, one wave per record, 16 at once: the record is read into
 //            LDS with system-scope 8-byte loads and encoded or parsed there exactly as MarshalSymphony /
@@ -38,6 +38,7 @@ namespace rw {
 __device__ __forceinline__ u64 ld_sys(const u64* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); }
 __device__ __forceinline__ void st_sys(u64* p, u64 v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); }
 __device__ __forceinline__ void fence_sys() { __atomic_thread_fence(__ATOMIC_SEQ_CST); }
+typedef u64 u64x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kThreads = 1024;  // 16 waves: up to 16 records served at once (each latency-bound)
 constexpr int kWaves = kThreads / 64;
@@ -250,7 +251,9 @@ __global__ __launch_bounds__(kThreads) void worker_kernel(RingCtl* ctl, uint8_t*
         if (tid < kRingSlots) {
             const u64 t = e + (u64)tid;
             const SlotCtl* sc = (const SlotCtl*)(slots + (size_t)(t % kRingSlots) * kSlotBytes);
-            const u64 rq = ld_sys(&sc->req), il = ld_sys(&sc->in_len);
+            // req and in_len in one system-coherent 16-byte load (volatile: sc0 sc1, as ld_sys)
+            const u64x2 ri = *(const volatile u64x2*)&sc->req;
+            const u64 rq = ri.x, il = ri.y;
             if (S.served[t % kRingSlots] != t + 1 && rq == t + 1) {
                 const int k = atomicAdd(&S.nlist, 1);
                 S.list[k] = tid;

@@ -6,13 +6,14 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
 #include <cstdint>
 
 #include "codec.hpp"
 
 namespace symhip {
 
-constexpr int kRingSlots = 512;            // tickets in flight per device ring (= the worker's window)
+constexpr int kRingSlots = 256;            // tickets in flight per device ring (= the worker's window)
 constexpr size_t kSlotBytes = 16384;       // one slot: control words, in area, out area
 constexpr size_t kSlotInAt = 64;
 constexpr size_t kSlotIn = 4096 - 64;      // in area bytes
@@ -47,12 +48,13 @@ constexpr uint64_t slot_kind(int dir, Layout lay, int bid) {
 
 struct SlotCtl {          // the first 64 bytes of a slot
     uint64_t req;         // caller: ticket + 1 once the in area is written
+    uint64_t in_len;      // caller: low half encode: field bytes after EncIn, decode: record bytes; high
+                          // half slot_kind() (next to req: the worker reads both with one 16-byte load)
     uint64_t done;        // worker: ticket + 1 once the out area is written
     uint64_t turn;        // caller: the ticket that may use the slot next
-    uint64_t in_len;      // caller: low half encode: field bytes after EncIn, decode: record bytes; high
-                          // half slot_kind()
     uint64_t pad[4];
 };
+static_assert(offsetof(SlotCtl, in_len) == 8, "req and in_len in one 16-byte load");
 
 struct EncIn {            // encode in area: the record's scalars, then its var fields' bytes back to back
     int32_t fixed[kMaxFixed];

@@ -789,13 +789,38 @@ def host_inclusive(codec: Codec, kw: dict, dev, steps: int, warm_s: float = 2.0)
         return json.loads(r.stdout.strip().splitlines()[-1])
 
     return {"pinned": c_caller(), "pinned_in_torch_process": run(True), "pageable": run(False),
-            "serial_one_stream": serial(),
+            "serial_one_stream": serial(), "e2e_loopback": e2e_leg(),
             "note": "sym_encode_host + sym_decode_host (chunked, one stream per direction, H2D/kernel/D2H "
                     "overlapped), host clock after a 2 s warm-up of the same calls; pinned: from a plain-C "
                     "process (tests/host_bench.c), the caller a cgo adapter is; pinned_in_torch_process: the same "
                     "calls on torch's bundled HIP runtime, which runs D2H copies as blit kernels "
                     "(profiles/r04_host_timeline.txt); "
                     "algorithmic bytes as the headline; serial_one_stream: the same work unchunked on one stream"}
+
+
+def e2e_leg(rpcs: int = 1 << 18, window: int = 4096, inflight: int = 2) -> dict:
+    """BASELINE config 5's stand-in: tests/e2e_loopback.c, a plain-C client and server process over UDP
+    127.0.0.1 exchanging kv Set RPCs (K=64, V=256) with the HIP codec, packetizer and reassembler on
+    both sides (C stand-in for the aRPC pair: no Go toolchain).  Host clock around the whole exchange:
+    H2D + kernels + D2H + sendmmsg / recvmmsg.  One untimed short run first (process and HIP start-up,
+    PCIe warm-up)."""
+    import subprocess
+    drv = os.path.join(ROOT, "tests", "bin", "e2e_loopback")
+    if not os.path.exists(drv):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests")], check=True, capture_output=True)
+    env = dict(os.environ, E2E_NOVERIFY="1")
+    subprocess.run([drv, str(4 * window), str(window), "64", "256", str(inflight)], capture_output=True, text=True,
+                   timeout=120, env=env)
+    r = subprocess.run([drv, str(rpcs), str(window), "64", "256", str(inflight)], capture_output=True, text=True,
+                       timeout=300, env=env)
+    if r.returncode != 0:
+        raise RuntimeError(r.stdout + r.stderr)
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    out["note"] = ("C stand-in for the aRPC client/server pair (tests/e2e_loopback.c; no Go toolchain): Set RPCs "
+                   "over UDP loopback, request and response each encoded, packetized, reassembled and decoded "
+                   "on the GPU through the C ABI; gbps_algorithmic counts the four codec calls' bytes "
+                   "(SURVEY 8d definition) per RPC; host clock around the whole exchange")
+    return out
 
 
 def per_record_leg(records: int, threads: int) -> dict:

@@ -214,7 +214,7 @@ int sym_decode_host(sym_ctx* ctx, int schema, uint64_t n, const uint8_t* h_in, c
  *   Unmarshal server receive loop      pkg/rpc/server.go:152, client response  client.go:205
  *   adapter                            pkg/serializer/symphony.go:10-16
  * A batcher serves those concurrent one-record calls without a launch per call.  Records of up to
- * 4000 bytes (encode: the fields' bytes; decode: the record) go through a ring of 512 slots in
+ * 4000 bytes (encode: the fields' bytes; decode: the record) go through a ring of 256 slots in
  * coherent pinned host memory, one ring per DEVICE shared by all its batchers and both directions:
  * the caller writes its record into a slot and publishes it, a persistent one-workgroup kernel
  * (started with the device's first batcher; leaving after 20 ms without records and restarted by
