@@ -30,11 +30,12 @@
 // worker per device -- shared by every batcher on the device and both directions, each slot carrying
 // its record's direction and layout -- serving tickets in place in coherent pinned slots; a record is
 // published with one store, served within a few microseconds, and read back as soon as its own flag
-// is set.  One worker per device, not per batcher and direction: a persistent kernel holds the
-// hardware queue its stream maps to (GPU_MAX_HW_QUEUES, 4 by default), and a launch of another stream
-// on that queue waits behind it; the worker also hands over to a fresh launch every kLifeTicks (2 ms)
-// while busy, so such a launch (a batch of large records, a caller's own kernels) waits at most that
-// long.  Larger records keep the batched path above.  Both give the same bytes and statuses.
+// is set.  ONE worker per device, however many batchers: a persistent kernel holds the hardware queue
+// its stream maps to (GPU_MAX_HW_QUEUES, 4 by default), and a launch of another stream on that queue
+// waits behind it -- two persistent workers whose streams share a queue serve in turns of their idle
+// timeout (measured: 40 ms per record, DESIGN.md section 4, per-record path).  The worker also hands
+// over to a fresh launch every kLifeTicks (2 ms), busy or idle, so such a launch (a batch of large
+// records, a caller's own kernels) waits at most that long.  Larger records keep the batched path above.  Both give the same bytes and statuses.
 #include <hip/hip_runtime.h>
 
 #include <immintrin.h>
@@ -83,13 +84,11 @@ struct BSlot {
     std::condition_variable cv;  // the slot's callers: DONE, or "lead me"
 };
 
-// The ring of one device (record_worker.hpp): coherent mapped pinned memory (the callers' ticket
-// counter in it), the worker's generation (relaunched under `mu` when one has exited), and the
-// batchers using it.
+// The ring of one device and direction (record_worker.hpp): coherent mapped pinned memory (the
+// callers' ticket counter in it) and the worker's generation (relaunched under `mu` when one has
+// exited).
 struct Ring {
     int device = 0;
-    int refs = 0;  // batchers on the device (under g_rings_mu)
-    bool id_used[symhip::kMaxBatchers] = {};  // batcher ids on the ring (under g_rings_mu)
     symhip::RingCtl* ctl = nullptr;
     uint8_t* slots = nullptr;
     std::atomic<uint64_t> gen{0};
@@ -97,9 +96,16 @@ struct Ring {
     hipStream_t stream = nullptr;
 };
 
+// A device's ring, the batchers using it and their ids.
+struct DevRings {
+    int refs = 0;
+    bool id_used[symhip::kMaxBatchers] = {};
+    Ring* ring = nullptr;
+};
+
 constexpr int kMaxDevices = 64;
-std::mutex g_rings_mu;
-Ring* g_rings[kMaxDevices] = {};
+std::mutex g_rings_mu;  // g_rings and every DevRings' refs / id_used
+DevRings g_rings[kMaxDevices];
 
 struct Queue {
     sym_ctx* ctx = nullptr;
@@ -123,7 +129,7 @@ struct sym_batcher {
     uint64_t B = 0;  // record bytes per batch
     uint32_t wait_us = 0;
     Queue q[2];      // 0 encode, 1 decode
-    Ring* ring = nullptr;  // the device's ring: records up to kRingRecordMax bytes
+    Ring* ring[2] = {};    // per direction, the device's ring (the same one): records up to kRingRecordMax bytes
     int bid = -1;          // this batcher's id on the ring (its records' kind; its pass counters)
     uint64_t pass_base[2] = {};  // the ring's pass counters of this id when the batcher took it
     std::atomic<uint64_t> ring_recs[2] = {};  // this batcher's ring records per direction
@@ -349,30 +355,33 @@ int ring_create(int device, Ring** out) {
 int ring_acquire(sym_batcher* b, int device) {
     if (device < 0 || device >= kMaxDevices) return fail(SYM_ERR_INVALID, "sym_batcher_create: device %d", device);
     std::lock_guard<std::mutex> lk(g_rings_mu);
-    if (!g_rings[device]) {
-        const int rc = ring_create(device, &g_rings[device]);
+    DevRings& d = g_rings[device];
+    if (!d.ring) {
+        const int rc = ring_create(device, &d.ring);
         if (rc != SYM_OK) return rc;
     }
-    Ring* r = g_rings[device];
     int id = 0;
-    while (id < symhip::kMaxBatchers && r->id_used[id]) ++id;
+    while (id < symhip::kMaxBatchers && d.id_used[id]) ++id;
     if (id == symhip::kMaxBatchers)
         return fail(SYM_ERR_INVALID, "sym_batcher_create: %d batchers on device %d already", symhip::kMaxBatchers, device);
-    r->id_used[id] = true;
-    ++r->refs;
-    b->ring = r;
+    d.id_used[id] = true;
+    ++d.refs;
     b->bid = id;
-    for (int d = 0; d < 2; ++d) b->pass_base[d] = __atomic_load_n(&r->ctl->bpasses[id][d], __ATOMIC_ACQUIRE);
+    for (int dir = 0; dir < 2; ++dir) {
+        b->ring[dir] = d.ring;
+        b->pass_base[dir] = __atomic_load_n(&d.ring->ctl->bpasses[id][dir], __ATOMIC_ACQUIRE);
+    }
     return SYM_OK;
 }
 
 // The device's last batcher stops the worker and frees the ring.
-void ring_release(Ring* r, int bid) {
+void ring_release(int device, int bid) {
     std::lock_guard<std::mutex> lk(g_rings_mu);
-    if (bid >= 0) r->id_used[bid] = false;
-    if (--r->refs > 0) return;
-    g_rings[r->device] = nullptr;
-    ring_destroy(r);
+    DevRings& d = g_rings[device];
+    d.id_used[bid] = false;
+    if (--d.refs > 0) return;
+    if (d.ring) ring_destroy(d.ring);
+    d.ring = nullptr;
 }
 
 // After a record is published: a worker that announced its exit (ctl->quit == its generation) is
@@ -422,7 +431,7 @@ int ring_wait(Ring& r, const uint64_t* p, uint64_t want) {
 // worker, `drain` the out area, free the slot.
 template <typename Fill, typename Drain>
 int ring_call(sym_batcher* b, int dir, uint64_t in_len, Fill&& fill, Drain&& drain) {
-    Ring& r = *b->ring;
+    Ring& r = *b->ring[dir];
     const uint64_t t = __atomic_fetch_add(&r.ctl->ticket, 1, __ATOMIC_SEQ_CST);
     uint8_t* slot = r.slots + (size_t)(t % symhip::kRingSlots) * symhip::kSlotBytes;
     symhip::SlotCtl* sc = (symhip::SlotCtl*)slot;
@@ -501,7 +510,7 @@ int sym_batcher_create(int device, int schema, uint32_t max_records, uint64_t ma
 
 int sym_batcher_destroy(sym_batcher* b) {
     if (!b) return SYM_OK;
-    if (b->ring) ring_release(b->ring, b->bid);
+    if (b->bid >= 0) ring_release(b->device, b->bid);
     for (Queue& q : b->q) destroy_queue(q);
     delete b;
     return SYM_OK;
@@ -635,8 +644,9 @@ int sym_batcher_stats(sym_batcher* b, uint64_t* enc_batches, uint64_t* enc_recor
     uint64_t v[4];
     for (int dir = 0; dir < 2; ++dir) {  // batches: the batched path's launches + the ring worker's passes
         std::lock_guard<std::mutex> lk(b->q[dir].mu);
-        const uint64_t passes = b->ring ? __atomic_load_n(&b->ring->ctl->bpasses[b->bid][dir], __ATOMIC_ACQUIRE) : 0;
-        v[2 * dir] = b->q[dir].batches + (b->ring ? passes - b->pass_base[dir] : 0);
+        const Ring* r = b->ring[dir];
+        const uint64_t passes = r ? __atomic_load_n(&r->ctl->bpasses[b->bid][dir], __ATOMIC_ACQUIRE) : 0;
+        v[2 * dir] = b->q[dir].batches + (r ? passes - b->pass_base[dir] : 0);
         v[2 * dir + 1] = b->q[dir].records + b->ring_recs[dir].load(std::memory_order_relaxed);
     }
     if (enc_batches) *enc_batches = v[0];
@@ -647,10 +657,9 @@ int sym_batcher_stats(sym_batcher* b, uint64_t* enc_batches, uint64_t* enc_recor
 }
 
 int sym_batcher_quiesce(sym_batcher* b) {
-    if (!b || !b->ring) return fail(SYM_ERR_INVALID, "sym_batcher_quiesce: NULL batcher");
-    Ring& r = *b->ring;
-    std::lock_guard<std::mutex> lk(r.mu);  // no relaunch meanwhile
-    ring_stop(r);
+    if (!b || !b->ring[0]) return fail(SYM_ERR_INVALID, "sym_batcher_quiesce: NULL batcher");
+    std::lock_guard<std::mutex> lk(b->ring[0]->mu);  // no relaunch meanwhile
+    ring_stop(*b->ring[0]);
     return SYM_OK;
 }
 

@@ -8,7 +8,7 @@
 // space and coherent both ways:
 //
 //   caller   t = ticket++; wait until slot[t % kRingSlots].turn == t; write the record and its kind
-//            (direction, layout) into the slot; store req = t + 1; posted += 1; if the worker announced
+//            (direction, layout, batcher id) into the slot; store req = t + 1; posted += 1; if the worker announced
 //            that it is quitting, see that the next one runs (batcher.cpp); spin until done == t + 1;
 //            copy the result out; turn = t + kRingSlots
 //   worker   poll `posted` (one 8-byte PCIe read) while cold; when it passed the records served -- or
@@ -20,9 +20,9 @@
 //            built from LDS and written with a system-scope store, waited for, then done = t + 1
 //
 // The worker exits when told to (the device's last sym_batcher_destroy, sym_batcher_quiesce), after
-// kIdleTicks without a record, or after kLifeTicks of life (a persistent kernel holds its hardware
-// queue: with more streams than queues, a launch that shares the queue waits behind it, so a busy
-// worker hands over to a fresh launch that queues behind that launch).  The exit is announced and
+// kIdleTicks without a record, or after kLifeTicks of life, busy or idle (a persistent kernel holds
+// its hardware queue: with more streams than queues, a launch that shares the queue waits behind it,
+// so the worker hands over to a fresh launch, which queues behind that launch).  The exit is announced and
 // the records owed are served first (worker_kernel), so no caller is left waiting.  No wave waits on
 // another workgroup, and every wave reaches the exit.
 #include <hip/hip_runtime.h>
@@ -237,7 +237,8 @@ __global__ __launch_bounds__(kThreads) void worker_kernel(RingCtl* ctl, uint8_t*
             S.owed = 0;
             while (!S.drain && !S.hot) {
                 const u64 posted = ld_sys(&ctl->posted);
-                if (ld_sys(&ctl->stop) || __builtin_amdgcn_s_memrealtime() - progress > kIdleTicks) announce();
+                const u64 now = __builtin_amdgcn_s_memrealtime();
+                if (ld_sys(&ctl->stop) || now - progress > kIdleTicks || now - born > kLifeTicks) announce();
                 else if (posted != nproc) break;  // published records not served yet
                 else __builtin_amdgcn_s_sleep(10);
             }

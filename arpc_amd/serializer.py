@@ -318,11 +318,11 @@ class BatchingSerializer:
         return out
 
     def quiesce(self) -> None:
-        """Stop the device's ring worker now (sym_batcher_quiesce; the next call restarts it): before a
-        device-wide synchronisation that should not wait for its idle timeout."""
+        """Stop the device's ring workers now (sym_batcher_quiesce; the next call restarts them): before
+        a device-wide synchronisation that should not wait for their idle timeout."""
         for b in list(self._batchers.values()):
             _native.check(_native.lib().sym_batcher_quiesce(b), "sym_batcher_quiesce")
-            break  # one ring per device
+            break  # the rings are the device's, shared by every batcher
 
     def close(self) -> None:
         with self._lock:

@@ -215,17 +215,18 @@ int sym_decode_host(sym_ctx* ctx, int schema, uint64_t n, const uint8_t* h_in, c
  *   adapter                            pkg/serializer/symphony.go:10-16
  * A batcher serves those concurrent one-record calls without a launch per call.  Records of up to
  * 4000 bytes (encode: the fields' bytes; decode: the record) go through a ring of 256 slots in
- * coherent pinned host memory, one ring per DEVICE shared by all its batchers and both directions:
- * the caller writes its record into a slot and publishes it, a persistent one-workgroup kernel
- * (started with the device's first batcher; leaving after 20 ms without records and restarted by
- * the next call) serves whatever is published in place and sets the slot's done flag, and the
- * caller copies its result out -- a few microseconds per call, many calls per pass under load.
- * Queue budget: that kernel holds one hardware queue of the process (GPU_MAX_HW_QUEUES, 4 by
- * default) while it runs, and a launch of another stream that maps to the same queue waits behind
- * it; so a busy worker hands over to a fresh launch every 2 ms, and such a launch (the caller's own
- * kernels, hipDeviceSynchronize / torch.cuda.synchronize, a batch of large records) waits at most
- * about that long.  sym_batcher_quiesce stops the worker at once (it returns when the worker has
- * left; the next call restarts it), e.g. before a device-wide synchronisation.  Larger records join the open batch of their
+ * coherent pinned host memory, one ring per DEVICE shared by all its batchers and both
+ * directions: the caller writes its record into a slot and publishes it, a persistent one-workgroup
+ * kernel (started with the device's first batcher, restarted by the next call after it leaves)
+ * serves whatever is published in place and sets the slot's done flag, and the caller copies its
+ * result out -- a few microseconds per call, many calls per pass under load.  Queue budget: that
+ * kernel holds one hardware queue of the process (GPU_MAX_HW_QUEUES, 4 by default) while it runs,
+ * and a launch of another stream that maps to the same queue waits behind it; so the worker hands
+ * over to a fresh launch every 2 ms (busy or idle, and leaves for good after 20 ms without records),
+ * and such a launch (the caller's own kernels, hipDeviceSynchronize / torch.cuda.synchronize, a
+ * batch of large records) waits at most about that long.  sym_batcher_quiesce stops the worker at
+ * once (it returns when the worker has left; the next call restarts it), e.g. before a device-wide
+ * synchronisation.  Larger records join the open batch of their
  * direction and block; when no batch of that direction is on the GPU, one caller of the open batch
  * runs it (no extra thread): at once with max_wait_us = 0 -- under load a batch is whatever
  * arrived while the previous one ran -- else once it holds max_records records or max_bytes bytes
