@@ -199,60 +199,78 @@ def host_cpu_info() -> dict:
 
 
 def cpu_baseline(kw: dict, seconds: float) -> dict:
-    """The C restatement of the Go codec (oracle/symphony_oracle.c; no Go toolchain exists here or
-    on the GPU box) on a bounded sample of the same workload: encode+decode at 1 thread, then
-    record-sharded over the CPUs this process may actually use (its cgroup CPU quota, else its
-    affinity, else OMP_NUM_THREADS) and over nproc threads (above the quota the threads
-    time-slice, so that row shows what the quota caps); ctypes releases the GIL, so the shards run in
-    parallel.  Plus config 1's echo record (ns per MarshalSymphony / UnmarshalSymphony, one record
-    per call)."""
-    from concurrent.futures import ThreadPoolExecutor
+    """The C restatement of the Go codec (oracle/symphony_oracle.c; no Go toolchain exists here or on
+    the GPU box) on the headline's own batch: the same 2^20 records, encoded into a stream allocated
+    once and decoded into columns allocated once (oracle.BatchBench), as the GPU is timed -- a working
+    set of ~1 GB, far beyond the host's caches.  One thread pinned to one CPU: a warm-up round, then
+    rounds for about seconds/2 (at least 5); `value` is the median round's GB/s, with the spread.  Then
+    the batch record-sharded over the CPUs this process may use (its cgroup CPU quota, else its
+    affinity, else OMP_NUM_THREADS), one pinned thread per shard (ctypes releases the GIL), rounds in
+    lockstep for about seconds/2: the aggregate.  Plus config 1's echo record (ns per MarshalSymphony /
+    UnmarshalSymphony, one record per call with Go's allocations)."""
+    import statistics
+    import threading
 
     from oracle import oracle
     info = host_cpu_info()
-    sample = dict(kw, n=min(kw["n"], 1 << 16))
-    b = datagen.make_batch(**sample)
+    b = datagen.make_batch(**kw)
     s = b.schema
-    stream, off = oracle.encode_batch(b.fixed, b.var)  # warm
     var_total = sum(int(o[-1] - o[0]) for _, o in b.var)
-    enc_b, dec_b = alg_bytes(b.n, s.nvar, var_total, int(off[-1]))
+    enc_b, dec_b = alg_bytes(b.n, s.nvar, var_total, b.encoded_size())
+    cpus = sorted(os.sched_getaffinity(0))
+    mine = os.sched_getaffinity(0)
 
-    def run(budget: float) -> tuple[int, float]:
-        reps, t0 = 0, time.perf_counter()
-        while True:
-            oracle.encode_batch(b.fixed, b.var)
-            oracle.decode_batch(s.nfixed, s.nvar, stream, off)
-            reps += 1
-            el = time.perf_counter() - t0
-            if el >= budget:
-                return reps, el
+    bb = oracle.BatchBench(b.fixed, b.var)
+    os.sched_setaffinity(0, {cpus[0]})  # this thread only (Linux: pid 0 = the calling thread)
+    try:
+        e, d = bb.run(1)
+        reps = max(5, int(seconds / 2 / (e[0] + d[0])))
+        e, d = bb.run(reps)
+    finally:
+        os.sched_setaffinity(0, mine)
+    del bb
+    rates = sorted((enc_b + dec_b) / (x + y) / 1e9 for x, y in zip(e, d))
+    med = statistics.median(rates)
 
-    def sharded(threads: int, budget: float) -> tuple[int, float]:
-        t0 = time.perf_counter()
-        with ThreadPoolExecutor(threads) as ex:
-            res = list(ex.map(run, [budget] * threads))
-        return sum(r for r, _ in res), time.perf_counter() - t0
-
-    reps1, el1 = run(seconds / 3)
     omp = int(info["omp_num_threads"]) if (info["omp_num_threads"] or "").isdigit() else None
     share = info["cgroup_cpu_quota"] or omp or info["affinity"]
-    threads = max(1, min(int(share), info["affinity"]))
-    repsN, elN = sharded(threads, seconds / 3)
-    nproc = max(1, min(info["nproc"] or 1, 512))
-    repsP, elP = sharded(nproc, seconds / 3) if nproc != threads else (repsN, elN)
+    threads = max(1, min(int(share), len(cpus)))
+    from arpc_amd import shard
+    benches = []
+    for t in range(threads):
+        lo, hi = shard.shard_range(b.n, threads, t)
+        benches.append(oracle.BatchBench([c[lo:hi] for c in b.fixed], shard.shard_columns(b.var, lo, hi)))
+    e1, d1 = benches[0].run(1)
+    rounds = max(3, int(seconds / 2 / (e1[0] + d1[0]) / max(1, threads // 2)))
+    go = threading.Barrier(threads + 1)
+
+    def work(t):
+        os.sched_setaffinity(0, {cpus[t % len(cpus)]})
+        go.wait()
+        benches[t].run(rounds)
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(threads)]
+    for x in th:
+        x.start()
+    go.wait()
+    t0 = time.perf_counter()
+    for x in th:
+        x.join()
+    el = time.perf_counter() - t0
+    del benches
+    agg = (enc_b + dec_b) * rounds / el / 1e9
     m_ns, u_ns = oracle.bench_echo(2_000_000)
-    gb = lambda reps, el: round((enc_b + dec_b) * reps / el / 1e9, 4)
-    return {"value": gb(reps1, el1), "unit": "GB/s", "cores": 1, "kind": "port",
-            "mrecords_per_s": round(b.n * reps1 / el1 / 1e6, 4),
-            "all_cores": {"value": gb(repsN, elN), "cores": threads,
-                          "mrecords_per_s": round(b.n * repsN / elN / 1e6, 4),
+    ws = (var_total + 16 * (b.n + 1)) * 2 + b.encoded_size() + 8 * (b.n + 1) + b.n
+    return {"value": round(med, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+            "mrecords_per_s": round(med * 1e9 / ((enc_b + dec_b) / b.n) / 1e6, 3),
+            "rounds": len(rates), "spread_gbps": [round(rates[0], 3), round(rates[-1], 3)],
+            "encode_ms_median": round(1e3 * statistics.median(e), 2),
+            "decode_ms_median": round(1e3 * statistics.median(d), 2),
+            "working_set_bytes": ws,
+            "all_cores": {"value": round(agg, 3), "cores": threads, "rounds": rounds,
+                          "mrecords_per_s": round(b.n * rounds / el / 1e6, 3),
                           "share_from": "cgroup cpu quota" if info["cgroup_cpu_quota"] else
                                         ("OMP_NUM_THREADS" if omp else "affinity")},
-            "nproc_threads": {"value": gb(repsP, elP), "threads": nproc,
-                              "mrecords_per_s": round(b.n * repsP / elP / 1e6, 4),
-                              "oversubscribed": bool(info["cgroup_cpu_quota"] and nproc > info["cgroup_cpu_quota"]),
-                              "note": "nproc threads on the CPUs this process may use: above its cgroup quota they "
-                                      "time-slice, so this row shows the quota's cap, not a baseline"},
             "host": info,
             "config1_echo": {"marshal_ns": round(m_ns, 2), "unmarshal_ns": round(u_ns, 2),
                              "records_per_s": round(1e9 / (m_ns + u_ns), 1),
@@ -260,10 +278,11 @@ def cpu_baseline(kw: dict, seconds: float) -> dict:
                              "note": "EchoRequest{42, 300, alice, hello world} (54 B), marshal then unmarshal, "
                                      "one record per call with Go's allocations (oracle/bench_oracle.c, "
                                      "testcases/simple/main.go:248-420 methodology), 1 thread"},
-            "sample": f"{b.n} {s.go_type} records of the same workload (seed {sample['seed']:#x}), "
-                      f"encode+decode x{reps1} in {el1:.1f} s on 1 thread, x{repsN} in {elN:.1f} s on "
-                      f"{threads} threads (the CPU share) and x{repsP} in {elP:.1f} s on {nproc} threads (nproc) "
-                      "by oracle/symphony_oracle.c (-O2): C restatement of the Go codec, not Go (no Go toolchain)"}
+            "sample": f"the headline batch itself: {b.n} {s.go_type} records (seed {kw['seed']:#x}), encode into a "
+                      f"preallocated stream + decode into preallocated columns, {len(rates)} rounds on 1 thread "
+                      f"pinned to CPU {cpus[0]} (median, spread min..max), {rounds} rounds on {threads} pinned "
+                      "threads over record shards (aggregate); oracle/symphony_oracle.c (-O2): the C "
+                      "restatement of the Go codec, not Go (no Go toolchain)"}
 
 
 def decode_kernel_name(s, mixed: bool = False) -> str:

@@ -61,3 +61,31 @@ uint64_t sym_oracle_bench_echo(uint64_t iters, double* marshal_ns, double* unmar
     *unmarshal_ns = (t2 - t1) / (double)iters;
     return sum;
 }
+
+uint64_t sym_oracle_encode_batch(int nfixed, int nvar, uint64_t n, const int32_t* const* fixed_cols,
+                                 const uint8_t* const* bytes, const uint64_t* const* offs, uint32_t sid,
+                                 uint32_t mid, uint8_t* out, uint64_t* out_off);
+void sym_oracle_decode_batch(int nfixed, int nvar, uint64_t n, const uint8_t* in, const uint64_t* rec_off,
+                             int32_t* const* fixed_out, uint8_t* const* bytes_out, uint64_t* const* offs_out,
+                             uint8_t* status);
+
+/* The batch restatement timed as the headline measures the GPU: `reps` rounds of encode into a
+ * preallocated stream, then decode of it into preallocated columns, over the caller's whole batch
+ * (bench.py passes the headline's 2^20 records: a working set of ~1 GB, far beyond the host's caches).
+ * Writes each round's encode and decode seconds.  Returns the last stream's size. */
+uint64_t sym_oracle_bench_batch(int nfixed, int nvar, uint64_t n, const int32_t* const* fixed, const uint8_t* const* bytes,
+                                const uint64_t* const* offs, uint8_t* out, uint64_t* out_off, int32_t* const* dfixed,
+                                uint8_t* const* dbytes, uint64_t* const* doffs, uint8_t* status, int reps,
+                                double* enc_s, double* dec_s) {
+    uint64_t size = 0;
+    for (int r = 0; r < reps; ++r) {
+        const double t0 = now_ns();
+        size = sym_oracle_encode_batch(nfixed, nvar, n, fixed, bytes, offs, 0, 0, out, out_off);
+        const double t1 = now_ns();
+        sym_oracle_decode_batch(nfixed, nvar, n, out, out_off, dfixed, dbytes, doffs, status);
+        const double t2 = now_ns();
+        enc_s[r] = (t1 - t0) * 1e-9;
+        dec_s[r] = (t2 - t1) * 1e-9;
+    }
+    return size;
+}

@@ -143,6 +143,45 @@ def bench_echo(iters: int) -> tuple[float, float]:
     return m.value, u.value
 
 
+class BatchBench:
+    """A batch's encode + decode on one CPU thread into buffers allocated once (oracle/bench_oracle.c
+    sym_oracle_bench_batch): run(reps) -> (encode seconds, decode seconds) per round."""
+
+    def __init__(self, fixed_cols, var_cols):
+        self.nf, self.nv = len(fixed_cols), len(var_cols)
+        self.n = n = len(var_cols[0][1]) - 1 if self.nv else len(fixed_cols[0])
+        self.fixed = [np.ascontiguousarray(c, dtype=np.int32) for c in fixed_cols]
+        self.vb = [np.ascontiguousarray(b, dtype=np.uint8) for b, _ in var_cols]
+        self.vo = [np.ascontiguousarray(o, dtype=np.uint64) for _, o in var_cols]
+        var = sum(int(o[-1] - o[0]) for o in self.vo)
+        self.total = n * (14 + 4 * (self.nf + self.nv) + 4 * self.nv) + var
+        self.out = np.zeros(max(1, self.total), dtype=np.uint8)
+        self.out_off = np.zeros(n + 1, dtype=np.uint64)
+        self.dfixed = [np.zeros(max(1, n), dtype=np.int32) for _ in range(self.nf)]
+        self.dbytes = [np.zeros(max(1, self.total), dtype=np.uint8) for _ in range(self.nv)]
+        self.doffs = [np.zeros(n + 1, dtype=np.uint64) for _ in range(self.nv)]
+        self.status = np.zeros(max(1, n), dtype=np.uint8)
+        for a in [self.out, self.out_off, self.status] + self.dbytes + self.doffs:
+            a.fill(0)  # first touch here, not in the timed rounds
+        L = lib()
+        if not getattr(L, "_bench_batch_ready", False):
+            vp, pa = ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)
+            dp = ctypes.POINTER(ctypes.c_double)
+            L.sym_oracle_bench_batch.restype = ctypes.c_uint64
+            L.sym_oracle_bench_batch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint64, pa, pa, pa, vp, vp, pa,
+                                                 pa, pa, vp, ctypes.c_int, dp, dp]
+            L._bench_batch_ready = True
+
+    def run(self, reps: int):
+        enc, dec = (ctypes.c_double * reps)(), (ctypes.c_double * reps)()
+        size = lib().sym_oracle_bench_batch(
+            self.nf, self.nv, self.n, _ptr_array(self.fixed), _ptr_array(self.vb), _ptr_array(self.vo),
+            _ptr(self.out), _ptr(self.out_off), _ptr_array(self.dfixed), _ptr_array(self.dbytes),
+            _ptr_array(self.doffs), _ptr(self.status), reps, enc, dec)
+        assert size == self.total and not self.status[:self.n].any()
+        return list(enc), list(dec)
+
+
 # ---------------------------------------------------------------- mixed Get/Set batches
 def encode_kv_mixed(rtype, key, val, service_id: int = 0, get_method_id: int = 0, set_method_id: int = 0):
     """rtype: u8 [n] (0 GetRequest, else SetRequest); key / val: (u8 bytes, u64 offs [n+1]).
