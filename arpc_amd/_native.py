@@ -72,17 +72,11 @@ SIGNATURES = {
     "sym_flat_encode": (_int, [_ctx, _vp, _int, _u64, _vp, _vp, _u32, _u32, _u8p, _u64p, _vp]),
     "sym_flat_decode": (_int, [_ctx, _vp, _int, _u64, _u8p, _u64p, _vp, _vp, _vp, _u8p, _vp]),
     "sym_flat_encoded_size_ex": (_u64, [_vp, _int, _u64, _vp, _vp]),
-    "sym_flat_encode_ex": (_int, [_ctx, _vp, _int, _u64, _vp, _vp, _vp, _u32, _u32, _u8p, _u64p, _vp]),
-    "sym_flat_encode_ex2": (_int, [_ctx, _vp, _int, _u64, _vp, _vp, _vp, _u32, _u32, _int, _u64, _u8p, _u64p, _vp]),
-    "sym_flat_decode_ex": (_int, [_ctx, _vp, _int, _u64, _u8p, _u64p, _vp, _vp, _vp, _vp, _vp, _u8p, _u8p, _vp]),
-    "sym_flat_decode_ex2": (_int, [_ctx, _vp, _int, _u64, _u8p, _u64p, _u64p, _u64p, _u64p, _vp, _vp, _vp, _vp, _vp,
-                                   _vp, _u8p, _u8p, _vp]),
-    "sym_flat_nested_status": (_int, [_ctx, _vp, _int, _int, _u64, _u64p, _u8p, _u8p, _u8p, _vp]),
-    "sym_flat_list_sizes": (_int, [_ctx, _int, _u64, _vp, _vp, _vp, _u64p, _vp]),
-    "sym_flat_decode_ex3": (_int, [_ctx, _vp, _int, _u64, _u64p, _u8p, _u64p, _u64p, _u64p, _u64p, _vp, _vp, _vp, _vp,
-                                   _vp, _vp, _u8p, _u8p, _vp]),
-    "sym_flat_nested_status2": (_int, [_ctx, _vp, _int, _int, _vp, _u64, _u64p, _vp, _vp, _u8p, _u8p, _vp]),
-    "sym_flat_list_sizes2": (_int, [_ctx, _int, _u64, _u64p, _vp, _vp, _vp, _u64p, _vp]),
+    "sym_flat_encode_ex": (_int, [_ctx, _vp, _int, _u64, _vp, _vp, _vp, _vp, _u8p, _u64p, _vp]),
+    "sym_flat_decode_ex": (_int, [_ctx, _vp, _int, _u64, _u64p, _u8p, _u64p, _u64p, _u64p, _u64p, _vp, _vp, _vp, _vp,
+                                  _vp, _vp, _u8p, _u8p, _vp]),
+    "sym_flat_nested_status": (_int, [_ctx, _vp, _int, _int, _vp, _u64, _u64p, _vp, _vp, _u8p, _u8p, _vp]),
+    "sym_flat_list_sizes": (_int, [_ctx, _int, _u64, _u64p, _vp, _vp, _vp, _u64p, _vp]),
     "sym_raw_set": (_int, [_ctx, _vp, _int, _int, _u8p, _u64p, _u64, _vp, _u64p, _u8p, _u64, _u64p, _u8p, _vp]),
     "sym_batcher_create": (_int, [_int, _int, _u32, _u64, _u32, ctypes.POINTER(ctypes.c_void_p)]),
     "sym_batcher_destroy": (_int, [_vp]),
@@ -152,6 +146,17 @@ class SymField(ctypes.Structure):
     _fields_ = [("segment", ctypes.c_uint8), ("width", ctypes.c_uint8)]
 
 
+SYM_FRAME_PREFIX_MAX = 24
+
+
+class FlatEncodeOpts(ctypes.Structure):
+    """struct sym_flat_encode_opts (include/symphony_hip.h)."""
+    _fields_ = [("service_id", ctypes.c_uint32), ("method_id", ctypes.c_uint32), ("framed", ctypes.c_uint32),
+                ("frame_prefix_len", ctypes.c_uint32), ("frame_prefix", ctypes.c_uint8 * SYM_FRAME_PREFIX_MAX),
+                ("string_bytes", ctypes.c_uint64), ("d_gate_rec", ctypes.c_void_p), ("gate_n", ctypes.c_uint64),
+                ("gate_when_all", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+
 class Endpoints(ctypes.Structure):
     """struct sym_endpoints (include/symphony_hip.h)."""
     _fields_ = [("dst_ip", ctypes.c_uint8 * 4), ("dst_port", ctypes.c_uint16),
@@ -179,7 +184,7 @@ def lib() -> ctypes.CDLL:
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.sym_abi_version() != 1:
+        if L.sym_abi_version() != 2:
             raise ImportError(f"unexpected ABI version {L.sym_abi_version()} in {LIB_PATH}")
         _lib = L
     return _lib

@@ -671,19 +671,15 @@ uint64_t sym_flat_encoded_size_ex(const sym_field* fields, int nfields, uint64_t
 }
 
 int sym_flat_encode_ex(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const void* const* d_cols,
-                       const uint64_t* const* d_offs, const uint64_t* const* d_items, uint32_t service_id,
-                       uint32_t method_id, uint8_t* d_out, uint64_t* d_out_off, void* stream) {
-    return sym_flat_encode_ex2(ctx, fields, nfields, n, d_cols, d_offs, d_items, service_id, method_id, 0, 0, d_out,
-                               d_out_off, stream);
-}
-
-int sym_flat_encode_ex2(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const void* const* d_cols,
-                        const uint64_t* const* d_offs, const uint64_t* const* d_items, uint32_t service_id,
-                        uint32_t method_id, int framed, uint64_t string_bytes, uint8_t* d_out, uint64_t* d_out_off,
-                        void* stream) {
+                       const uint64_t* const* d_offs, const uint64_t* const* d_items, const sym_flat_encode_opts* opts,
+                       uint8_t* d_out, uint64_t* d_out_off, void* stream) {
     if (!ctx) return fail(SYM_ERR_INVALID, "sym_flat_encode: ctx is NULL");
     int rc = flat_check("sym_flat_encode", fields, nfields, d_items != nullptr);
     if (rc != SYM_OK) return rc;
+    const sym_flat_encode_opts o = opts ? *opts : sym_flat_encode_opts{};
+    if (o.frame_prefix_len > SYM_FRAME_PREFIX_MAX || (o.frame_prefix_len && !o.framed))
+        return fail(SYM_ERR_INVALID, "sym_flat_encode: frame_prefix_len %u (framed output only, <= %d)",
+                    o.frame_prefix_len, SYM_FRAME_PREFIX_MAX);
     if (!d_out_off || (n && (!d_out || (nfields && (!d_cols || !d_offs)))))
         return fail(SYM_ERR_INVALID, "sym_flat_encode: NULL argument");
     for (int k = 0; k < nfields && n; ++k) {
@@ -695,11 +691,11 @@ int sym_flat_encode_ex2(sym_ctx* ctx, const sym_field* fields, int nfields, uint
     DeviceGuard g(ctx->device);
     if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
     if (n == 0) {
+        if (o.d_gate_rec) return fail(SYM_ERR_INVALID, "sym_flat_encode: a gated launch needs records");
         hipError_t e = hipMemsetAsync(d_out_off, 0, sizeof(uint64_t), (hipStream_t)stream);
         return e == hipSuccess ? SYM_OK : hip_fail(e, "hipMemsetAsync");
     }
-    hipError_t e = symhip::launch_flat_encode(fields, nfields, n, d_cols, d_offs, d_items, service_id, method_id,
-                                              framed != 0, string_bytes, d_out, d_out_off, ctx->err,
+    hipError_t e = symhip::launch_flat_encode(fields, nfields, n, d_cols, d_offs, d_items, o, d_out, d_out_off, ctx->err,
                                               (hipStream_t)stream);
     return e == hipSuccess ? SYM_OK : hip_fail(e, "flat encode launch");
 }
@@ -707,15 +703,17 @@ int sym_flat_encode_ex2(sym_ctx* ctx, const sym_field* fields, int nfields, uint
 int sym_flat_encode(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const void* const* d_cols,
                     const uint64_t* const* d_offs, uint32_t service_id, uint32_t method_id, uint8_t* d_out,
                     uint64_t* d_out_off, void* stream) {
-    return sym_flat_encode_ex(ctx, fields, nfields, n, d_cols, d_offs, nullptr, service_id, method_id, d_out,
-                              d_out_off, stream);
+    sym_flat_encode_opts o{};
+    o.service_id = service_id;
+    o.method_id = method_id;
+    return sym_flat_encode_ex(ctx, fields, nfields, n, d_cols, d_offs, nullptr, &o, d_out, d_out_off, stream);
 }
 
-int sym_flat_decode_ex3(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const uint64_t* d_n,
-                        const uint8_t* d_in, const uint64_t* d_rec_src, const uint64_t* d_rec_len,
-                        const uint64_t* d_lo, const uint64_t* d_hi, void* const* d_cols, const uint64_t* caps,
-                        uint64_t* const* d_offs, uint64_t* const* d_items, uint64_t* const* d_item_len,
-                        const uint64_t* item_caps, uint8_t* d_status, uint8_t* d_fail, void* stream) {
+int sym_flat_decode_ex(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const uint64_t* d_n,
+                       const uint8_t* d_in, const uint64_t* d_rec_src, const uint64_t* d_rec_len, const uint64_t* d_lo,
+                       const uint64_t* d_hi, void* const* d_cols, const uint64_t* caps, uint64_t* const* d_offs,
+                       uint64_t* const* d_items, uint64_t* const* d_item_len, const uint64_t* item_caps,
+                       uint8_t* d_status, uint8_t* d_fail, void* stream) {
     if (!ctx) return fail(SYM_ERR_INVALID, "sym_flat_decode: ctx is NULL");
     const bool lists = d_items != nullptr;
     int rc = flat_check("sym_flat_decode", fields, nfields, lists);
@@ -753,40 +751,16 @@ int sym_flat_decode_ex3(sym_ctx* ctx, const sym_field* fields, int nfields, uint
     return e == hipSuccess ? SYM_OK : hip_fail(e, "flat decode launch");
 }
 
-int sym_flat_decode_ex2(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const uint8_t* d_in,
-                        const uint64_t* d_rec_src, const uint64_t* d_rec_len, const uint64_t* d_lo,
-                        const uint64_t* d_hi, void* const* d_cols, const uint64_t* caps, uint64_t* const* d_offs,
-                        uint64_t* const* d_items, uint64_t* const* d_item_len, const uint64_t* item_caps,
-                        uint8_t* d_status, uint8_t* d_fail, void* stream) {
-    return sym_flat_decode_ex3(ctx, fields, nfields, n, nullptr, d_in, d_rec_src, d_rec_len, d_lo, d_hi, d_cols, caps,
-                               d_offs, d_items, d_item_len, item_caps, d_status, d_fail, stream);
-}
-
-int sym_flat_decode_ex(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const uint8_t* d_in,
-                       const uint64_t* d_rec_off, void* const* d_cols, const uint64_t* caps, uint64_t* const* d_offs,
-                       uint64_t* const* d_items, const uint64_t* item_caps, uint8_t* d_status, uint8_t* d_fail,
-                       void* stream) {
-    return sym_flat_decode_ex2(ctx, fields, nfields, n, d_in, d_rec_off, nullptr, nullptr, nullptr, d_cols, caps, d_offs,
-                               d_items, nullptr, item_caps, d_status, d_fail, stream);
-}
-
 int sym_flat_decode(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const uint8_t* d_in,
                     const uint64_t* d_rec_off, void* const* d_cols, const uint64_t* caps, uint64_t* const* d_offs,
                     uint8_t* d_status, void* stream) {
-    return sym_flat_decode_ex(ctx, fields, nfields, n, d_in, d_rec_off, d_cols, caps, d_offs, nullptr, nullptr,
-                              d_status, nullptr, stream);
+    return sym_flat_decode_ex(ctx, fields, nfields, n, nullptr, d_in, d_rec_off, nullptr, nullptr, nullptr, d_cols, caps,
+                              d_offs, nullptr, nullptr, nullptr, d_status, nullptr, stream);
 }
 
-int sym_flat_nested_status(sym_ctx* ctx, const sym_field* fields, int nfields, int field, uint64_t n,
-                           const uint64_t* d_rec_items, const uint8_t* d_item_status, uint8_t* d_status,
-                           uint8_t* d_fail, void* stream) {
-    return sym_flat_nested_status2(ctx, fields, nfields, 1, &field, n, nullptr, &d_rec_items, &d_item_status, d_status,
-                                   d_fail, stream);
-}
-
-int sym_flat_nested_status2(sym_ctx* ctx, const sym_field* fields, int nfields, int nk, const int* ks, uint64_t n,
-                            const uint64_t* d_n, const uint64_t* const* d_rec_items,
-                            const uint8_t* const* d_item_status, uint8_t* d_status, uint8_t* d_fail, void* stream) {
+int sym_flat_nested_status(sym_ctx* ctx, const sym_field* fields, int nfields, int nk, const int* ks, uint64_t n,
+                           const uint64_t* d_n, const uint64_t* const* d_rec_items,
+                           const uint8_t* const* d_item_status, uint8_t* d_status, uint8_t* d_fail, void* stream) {
     if (!ctx) return fail(SYM_ERR_INVALID, "sym_flat_nested_status: ctx is NULL");
     int rc = flat_check("sym_flat_nested_status", fields, nfields, true);
     if (rc != SYM_OK) return rc;
@@ -811,13 +785,8 @@ int sym_flat_nested_status2(sym_ctx* ctx, const sym_field* fields, int nfields, 
     return e == hipSuccess ? SYM_OK : hip_fail(e, "nested status launch");
 }
 
-int sym_flat_list_sizes(sym_ctx* ctx, int nl, uint64_t n, const uint64_t* const* d_recs,
+int sym_flat_list_sizes(sym_ctx* ctx, int nl, uint64_t n, const uint64_t* d_n, const uint64_t* const* d_recs,
                         const uint64_t* const* d_items, const uint64_t* item_caps, uint64_t* d_out, void* stream) {
-    return sym_flat_list_sizes2(ctx, nl, n, nullptr, d_recs, d_items, item_caps, d_out, stream);
-}
-
-int sym_flat_list_sizes2(sym_ctx* ctx, int nl, uint64_t n, const uint64_t* d_n, const uint64_t* const* d_recs,
-                         const uint64_t* const* d_items, const uint64_t* item_caps, uint64_t* d_out, void* stream) {
     if (!ctx) return fail(SYM_ERR_INVALID, "sym_flat_list_sizes: ctx is NULL");
     if (nl < 0 || nl > SYM_MAX_FLAT_FIELDS) return fail(SYM_ERR_INVALID, "sym_flat_list_sizes: %d lists", nl);
     if (nl == 0) return SYM_OK;

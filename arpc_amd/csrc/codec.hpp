@@ -188,12 +188,12 @@ hipError_t launch_segment_gather(const raw::GatherArgs& a, hipStream_t stream);
 // ---- any flat schema (flat.hip); sym_field is defined in include/symphony_hip.h
 }  // namespace symhip
 struct sym_field;
+struct sym_flat_encode_opts;
 namespace symhip {
 size_t flat_ws_bytes(const sym_field* f, int nf, uint64_t n, const uint64_t* item_caps);
 hipError_t launch_flat_encode(const sym_field* f, int nf, uint64_t n, const void* const* cols,
-                              const uint64_t* const* offs, const uint64_t* const* items, uint32_t sid, uint32_t mid,
-                              bool framed, uint64_t string_bytes, uint8_t* out, uint64_t* out_off, unsigned* err,
-                              hipStream_t stream);
+                              const uint64_t* const* offs, const uint64_t* const* items, const sym_flat_encode_opts& o,
+                              uint8_t* out, uint64_t* out_off, unsigned* err, hipStream_t stream);
 // rec_len non-null: record i is in[rec_off[i], + rec_len[i]) (records in place); lo / hi: device
 // values bounding in's readable extent (null: rec_off[0], rec_off[n]); item_len[k] non-null for a
 // message field k: items[k] / item_len[k] receive each item's (offset into in, length), no bytes

@@ -187,12 +187,32 @@ def _rows(cols: list, schema: FlatSchema) -> int:
     return 0
 
 
+def _wrapper(schema: FlatSchema) -> bool:
+    """A wrapper: one field, a private non-repeated message of a schema with fields (online-boutique's
+    PlaceOrderResponse{Order}, GetQuoteResponse{CostUsd}).  Its record is 18 constant bytes before
+    the item's frame when the item is present (generator main.go:196-330, :565-590): header
+    (version, offset_to_private 13, service, method), the private marker, the table entry 5."""
+    return len(schema.fields) == 1 and schema.fields[0].kind == "message" and not schema.fields[0].repeated \
+        and not schema.fields[0].public and bool(schema.fields[0].message.fields)
+
+
+def _wrapper_prefix(service_id: int, method_id: int) -> bytes:
+    le = lambda v: int(v).to_bytes(4, "little")  # noqa: E731
+    return b"\x01" + le(13) + le(service_id) + le(method_id) + b"\x01" + le(5)
+
+
 def _encode(codec: Codec, ctx, schema: FlatSchema, cols: list, service_id: int, method_id: int, stream, n, out,
-            framed: bool, keep: list, fork: list):
+            framed: bool, keep: list, fork: list, wrap: dict | None = None):
     """encode() without the final read-back: the output buffer is sized from the columns' tensor
     sizes (an upper bound of the encoded size: sym_flat_encoded_size_ex of every byte / item column
     taken whole), so no level needs a device value on the host.  Inner levels are encoded framed
-    (sym_flat_encode_ex2: [u32 size] before each record), so an outer body is one window of them.
+    (sym_flat_encode_opts.framed: [u32 size] before each record), so an outer body is one window of
+    them.  A wrapper level that is not itself framed (_wrapper; the tree's root) is written by its
+    inner level's kernel when every record has its item -- the 18 wrapper bytes as that kernel's
+    frame prefix, straight into the wrapper's output (`wrap`) -- and by its own kernel otherwise;
+    both alternatives are queued, gated on the device by the item ranges (d_gate_rec), so the walk
+    still reads nothing back.  The wrapper's own kernel would copy every inner byte again (the
+    boutique root level: ~90 us for 150 MB).
     Subtrees on other branches free nothing before the whole tree is queued (`keep`): a block freed
     while a kernel of another branch may still read it could be handed to a concurrent branch;
     after the walk, later work on any branch is ordered after this tree (branches start by waiting
@@ -217,6 +237,7 @@ def _encode(codec: Codec, ctx, schema: FlatSchema, cols: list, service_id: int, 
         b_st.wait_stream(stream)
         runs.append((b_ctx, b_st))
     inner = {}
+    gate = None  # a wrapper level written by its inner level's kernel: the item ranges its own launch is gated on
     runs += [(ctx, stream)] * (len(msg) - len(runs))  # small levels: every subtree on this stream
     for (r_ctx, r_st), k in zip(runs, msg):
         c = cols[k]
@@ -228,7 +249,12 @@ def _encode(codec: Codec, ctx, schema: FlatSchema, cols: list, service_id: int, 
                 raise ValueError(f"{schema.fields[k].name}: a nested message without fields needs a host read "
                                  "of its item count, which a graph capture cannot hold; encode it eagerly")
             m_in = int(c.rec[-1].item() - c.rec[0].item()) if c.rec.numel() > 1 else 0
-        ib, io = _encode(codec, r_ctx, schema.fields[k].message, c.cols, 0, 0, r_st, m_in, None, True, keep, fork)
+        w = None
+        if not framed and _wrapper(schema) and c.rec.numel() > 1:
+            w = {"prefix": _wrapper_prefix(service_id, method_id), "out": out, "n": c.rec.numel() - 1, "rec": c.rec}
+        ib, io = _encode(codec, r_ctx, schema.fields[k].message, c.cols, 0, 0, r_st, m_in, None, True, keep, fork, w)
+        if w is not None and w.get("fused"):
+            out, gate = w["out"], w["rec"]  # this level's output: the buffers the fused launch wrote
         inner[k] = ListColumn(ib, io, c.rec)
         keep.append(inner[k])
     for _, r_st in runs[1:]:
@@ -285,10 +311,35 @@ def _encode(codec: Codec, ctx, schema: FlatSchema, cols: list, service_id: int, 
         if off.numel() != n + 1:
             raise ValueError("out offsets: n + 1 entries expected")
     lists = schema.has_lists
-    _native.check(codec._lib.sym_flat_encode_ex2(ctx, cf, len(schema.fields), n, _native.ptr_array(ptrs),
-                                                _native.ptr_array(offs), _native.ptr_array(items) if lists else None,
-                                                service_id, method_id, 1 if framed else 0, string_bytes, _dptr(out),
-                                                _dptr(off), stream.cuda_stream), "sym_flat_encode_ex2")
+
+    def launch(o, buf, boff):
+        _native.check(codec._lib.sym_flat_encode_ex(ctx, cf, len(schema.fields), n, _native.ptr_array(ptrs),
+                                                    _native.ptr_array(offs), _native.ptr_array(items) if lists else None,
+                                                    ctypes.byref(o), _dptr(buf), _dptr(boff), stream.cuda_stream),
+                      "sym_flat_encode_ex")
+
+    opts = _native.FlatEncodeOpts(service_id=service_id, method_id=method_id, framed=1 if framed else 0,
+                                  string_bytes=string_bytes)
+    if wrap is not None and n and n == wrap["n"]:  # the wrapper above, written here when every record has its item
+        wn = wrap["n"]
+        if wrap["out"] is None:  # its output, sized as its own launch would size it (and for the prefixes)
+            wsize = 18 * max(wn, n) + out.numel() + 16
+            wrap["out"] = (torch.empty(wsize, dtype=torch.uint8, device=codec.device),
+                           torch.empty(wn + 1, dtype=torch.int64, device=codec.device))
+        wbuf, woff = wrap["out"]
+        _check_col(wbuf, torch.uint8, "out", codec.device)
+        _check_col(woff, torch.int64, "out offsets", codec.device)
+        if woff.numel() != wn + 1:
+            raise ValueError("out offsets: n + 1 entries expected")
+        fused = _native.FlatEncodeOpts(framed=1, frame_prefix_len=len(wrap["prefix"]), string_bytes=string_bytes,
+                                       d_gate_rec=_dptr(wrap["rec"]), gate_n=wn, gate_when_all=1)
+        fused.frame_prefix[:len(wrap["prefix"])] = list(wrap["prefix"])
+        launch(fused, wbuf, woff)
+        wrap["fused"] = True
+        opts.d_gate_rec, opts.gate_n, opts.gate_when_all = _dptr(wrap["rec"]), wn, 0
+    if gate is not None and n:  # this (wrapper) level's own launch: only when an item is missing
+        opts.d_gate_rec, opts.gate_n, opts.gate_when_all = _dptr(gate), n, 0
+    launch(opts, out, off)
     return out, off
 
 
@@ -298,12 +349,12 @@ def decode(codec: Codec, schema: FlatSchema, data: torch.Tensor, rec_off: torch.
     """UnmarshalSymphony into fresh structs -> (cols, status) (with_fail: (cols, status, fail)); cols
     per the module docstring, message fields decoded recursively with their items' statuses folded
     into `status` (SYM_STATUS_NESTED).  span = rec_off[n] - rec_off[0] when the caller knows it
-    (skips a device sync).  Inner levels are decoded in place (sym_flat_decode_ex3): a message
+    (skips a device sync).  Inner levels are decoded in place (sym_flat_decode_ex): a message
     field's items stay where they are in `data` -- rec_off holds their offsets, rec_len their
     lengths, extent the device pointers bounding data's readable bytes, span an upper bound of their
     bytes -- so no level copies its inner messages out.  The whole tree is queued without a host
     sync: an inner level's record count stays on the device (the outer level's item count, from
-    sym_flat_list_sizes2) and its columns are sized for a capacity; every level's list sizes are
+    sym_flat_list_sizes) and its columns are sized for a capacity; every level's list sizes are
     read back once, at the end, and the columns cut to them.  A level's message fields are
     independent subtrees: with two or more, each runs on a branch of the codec (Codec.branch: its
     own stream and context, the decode workspace being per context)."""
@@ -391,13 +442,13 @@ def _decode_level(codec: Codec, ctx, schema: FlatSchema, data, rec_src, rec_len,
     cf = schema.c_fields()
     lists = schema.has_lists
     lo, hi = extent if in_place else (0, 0)
-    _native.check(codec._lib.sym_flat_decode_ex3(ctx, cf, len(schema.fields), ncap, n_dev, _dptr(data) or 1,
+    _native.check(codec._lib.sym_flat_decode_ex(ctx, cf, len(schema.fields), ncap, n_dev, _dptr(data) or 1,
                                                 _dptr(rec_src) or 1, _dptr(rec_len) if in_place else 0, lo, hi,
                                                 _native.ptr_array(ptrs), _native.u64_array(caps),
                                                 _native.ptr_array(offs), _native.ptr_array(items) if lists else None,
                                                 _native.ptr_array(ilens) if lists else None,
                                                 _native.u64_array(icaps) if lists else None, _dptr(st), _dptr(fail),
-                                                hs), "sym_flat_decode_ex3")
+                                                hs), "sym_flat_decode_ex")
     lk = [k for k, f in enumerate(schema.fields) if f.list_like]
     lvl = _Level(schema, cols, st, fail, lk, sum(t.numel() for t in pend), {})
     if not ncap:  # no records: empty inner levels
@@ -411,11 +462,11 @@ def _decode_level(codec: Codec, ctx, schema: FlatSchema, data, rec_src, rec_len,
         return lvl
     # every list field's item count and item bytes, on the device (read back with the whole tree's)
     sz = torch.empty(2 * len(lk), dtype=torch.int64, device=codec.device)
-    _native.check(codec._lib.sym_flat_list_sizes2(ctx, len(lk), ncap, n_dev,
+    _native.check(codec._lib.sym_flat_list_sizes(ctx, len(lk), ncap, n_dev,
                                                   _native.ptr_array([_dptr(cols[k].rec) for k in lk]),
                                                   _native.ptr_array([_dptr(cols[k].item_off) for k in lk]),
                                                   _native.u64_array([icaps[k] for k in lk]), _dptr(sz), hs),
-                  "sym_flat_list_sizes2")
+                  "sym_flat_list_sizes")
     pend.append(sz)
     msg = [(i, k) for i, k in enumerate(lk) if schema.fields[k].kind == "message"]
     runs = [(ctx, stream)]
@@ -434,11 +485,11 @@ def _decode_level(codec: Codec, ctx, schema: FlatSchema, data, rec_src, rec_len,
         stream.wait_stream(r_st)
     if lvl.inner:  # the inner statuses folded into this level's, every message field in one launch
         ks = sorted(lvl.inner)
-        _native.check(codec._lib.sym_flat_nested_status2(
+        _native.check(codec._lib.sym_flat_nested_status(
             ctx, cf, len(schema.fields), len(ks), (ctypes.c_int * len(ks))(*ks), ncap, n_dev,
             _native.ptr_array([_dptr(cols[k].rec) for k in ks]),
             _native.ptr_array([_dptr(lvl.inner[k].st) or 1 for k in ks]), _dptr(st), _dptr(fail), hs),
-            "sym_flat_nested_status2")
+            "sym_flat_nested_status")
     return lvl
 
 

@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define SYMPHONY_HIP_ABI_VERSION 1
+#define SYMPHONY_HIP_ABI_VERSION 2
 
 /* Return codes (0 = ok, negative = error); text via sym_last_error(). */
 #define SYM_OK 0
@@ -444,7 +444,7 @@ int sym_decrypt(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_off, ui
 #define SYM_FIELD_REPEATED 0x80 /* or'ed into sym_field.width: repeated fixed-width field */
 #define SYM_FIELD_MESSAGE 0x40  /* nested message; | SYM_FIELD_REPEATED: repeated message (sym_flat_*_ex) */
 #define SYM_FIELD_FRAMED 0x20   /* | SYM_FIELD_MESSAGE, encode: the items already carry their [u32 len] (the
-                                   inner level was encoded with framed output, sym_flat_encode_ex2) */
+                                   inner level was encoded with framed output, sym_flat_encode_opts) */
 
 typedef struct sym_field {
     uint8_t segment; /* SYM_SEGMENT_PUBLIC / SYM_SEGMENT_PRIVATE */
@@ -471,79 +471,85 @@ uint64_t sym_flat_encoded_size(const sym_field* fields, int nfields, uint64_t n,
  *                    list-like field (nested: records where it is set).
  *   sym_flat_encode_ex  as sym_flat_encode; list bodies ([count], then [u32 len][item] per item)
  *                    are written by the same output-stationary kernel.  More than one item for a
- *                    nested field is SYM_ERR_INVALID from sym_ctx_check.
+ *                    nested field is SYM_ERR_INVALID from sym_ctx_check.  `opts` (nullable: IDs 0,
+ *                    nothing else) -- see sym_flat_encode_opts.
  *   sym_flat_decode_ex  as sym_flat_decode; list-like field k: item bytes into d_cols[k] (caps[k]),
  *                    item offsets into d_items[k] (item_caps[k] + 1 entries) and record item ranges
  *                    into d_offs[k] (n + 1).  A list keeps the items that fit in the record, in order
  *                    (Go's loop stops making progress at the first that does not).  d_fail (n bytes,
  *                    nullable): the unmarshal position (public fields in order, then private) of
  *                    the field where decoding stopped, nfields when it did not.
- *   sym_flat_nested_status  after decoding field `field`'s items with the inner schema (their
- *                    statuses d_item_status), marks the records that reached the field and have a
- *                    failed item SYM_STATUS_NESTED (Go returns "failed to unmarshal nested message"
- *                    there); d_fail is updated, so fields can be folded in in any order.  Field
- *                    values of a record with a non-OK status are unspecified beyond the fields
- *                    before the failing one (Go callers discard the struct on error).
- *   sym_flat_decode_ex2  sym_flat_decode_ex over records in place and with message fields left in
- *                    place, so a tree decodes without copying inner messages out: record i is
- *                    d_in[d_rec_src[i], d_rec_src[i] + d_rec_len[i]) (d_rec_len NULL: contiguous, d_rec_src
- *                    is d_rec_off), and d_in's readable extent is [*d_lo, *d_hi) (device values; both NULL:
- *                    d_rec_src[0], d_rec_src[n]; required with d_rec_len).  For a message field k with
- *                    d_item_len[k] non-NULL no item bytes are written: d_items[k][j] receives item j's
- *                    offset into d_in and d_item_len[k][j] its length, and the inner level is decoded
- *                    from there (d_rec_src = d_items[k], d_rec_len = d_item_len[k], the same d_in).
+ *                    Records in place: record i is d_in[d_rec_src[i], d_rec_src[i] + d_rec_len[i])
+ *                    (d_rec_len NULL: contiguous, d_rec_src is d_rec_off), and d_in's readable extent
+ *                    is [*d_lo, *d_hi) (device values; both NULL: d_rec_src[0], d_rec_src[n]; required
+ *                    with d_rec_len).  For a message field k with d_item_len[k] non-NULL no item bytes
+ *                    are written: d_items[k][j] receives item j's offset into d_in and d_item_len[k][j]
+ *                    its length, and the inner level is decoded from there (d_rec_src = d_items[k],
+ *                    d_rec_len = d_item_len[k], the same d_in), so a tree decodes without copying
+ *                    inner messages out.  Record count on the device: d_n (nullable) holds it and n is
+ *                    its capacity (an inner level of a tree walk, whose count is the outer level's
+ *                    item count from sym_flat_list_sizes); columns are sized for the capacity and
+ *                    every launch strides over the tiles of the count, so a tree decodes with no host
+ *                    read until its end.
+ *   sym_flat_nested_status  after decoding message fields ks[q] (q < nk; their items' statuses
+ *                    d_item_status[q], item ranges d_rec_items[q]) with the inner schemas, marks the
+ *                    records that reached the field and have a failed item SYM_STATUS_NESTED (Go
+ *                    returns "failed to unmarshal nested message" there), all nk fields in one launch;
+ *                    d_fail is updated, so fields can be folded in in any order.  Field values of a
+ *                    record with a non-OK status are unspecified beyond the fields before the failing
+ *                    one (Go callers discard the struct on error).  d_n as in sym_flat_decode_ex.
  *   sym_flat_list_sizes  after sym_flat_decode_ex, for `nl` list-like fields (record item ranges
  *                    d_recs[i], n + 1 entries; item offsets d_items[i], item_caps[i] + 1): item count
  *                    m_i = d_recs[i][n] - d_recs[i][0] (clamped to item_caps[i]) and item bytes
  *                    d_items[i][m_i] into d_out[2i], d_out[2i + 1] (device memory), in one launch,
- *                    so a host walking a message tree reads back one small array per level.
- *   sym_flat_decode_ex3 / sym_flat_nested_status2 / sym_flat_list_sizes2  the same three with the
- *                    record count on the device: d_n (nullable) holds it, n is its capacity (an inner
- *                    level of a tree walk, whose count is the outer level's item count from
- *                    sym_flat_list_sizes2, d_out[2i]).  Columns are sized for the capacity; every
- *                    launch strides over the tiles of the count, so a tree decodes with no host read
- *                    until its end (arpc_amd/flat.py reads all levels' sizes back at once).
- *                    sym_flat_nested_status2 folds nk message fields ks[q] (item ranges
- *                    d_rec_items[q], statuses d_item_status[q]) in one launch. */
+ *                    so a host walking a message tree reads back one small array at the end.  d_n as
+ *                    in sym_flat_decode_ex. */
+#define SYM_FRAME_PREFIX_MAX 24
+/* Options of sym_flat_encode_ex (all zero: MarshalSymphony with service / method IDs 0).
+ *   framed         nonzero: each record is written as [frame_prefix][u32 size][record] (an inner level
+ *                  of a tree walk: [u32 size][record] is what the outer level's body holds for one item,
+ *                  so an outer message field takes the items with SYM_FIELD_FRAMED and its bodies become
+ *                  one window each); d_out_off are the frames' offsets
+ *   frame_prefix   framed only: frame_prefix_len (<= SYM_FRAME_PREFIX_MAX) constant bytes before each
+ *                  frame.  A message whose one field is a private nested message (a wrapper such as
+ *                  online-boutique's PlaceOrderResponse{Order}) is, when every record has its item,
+ *                  exactly 18 constant bytes (header, marker, table entry 5) before the item's frame:
+ *                  with them as the prefix the inner level's kernel writes the wrapper level itself
+ *                  and the wrapper's own launch copies nothing (arpc_amd/flat.py)
+ *   string_bytes   the caller's estimate of the string / bytes fields' payload bytes (0: unknown); a
+ *                  level of short strings is then written with more payload windows per 16-byte chunk
+ *   d_gate_rec     nullable, device memory: the launch does its work only when
+ *                  (d_gate_rec[gate_n] - d_gate_rec[0] == gate_n) equals (gate_when_all != 0), and
+ *                  otherwise leaves every output untouched -- a condition on device data (a nested
+ *                  field's item ranges: is every record's item present?) that lets a tree walk queue
+ *                  both alternatives without a host read */
+typedef struct sym_flat_encode_opts {
+    uint32_t service_id, method_id;
+    uint32_t framed;
+    uint32_t frame_prefix_len;
+    uint8_t frame_prefix[SYM_FRAME_PREFIX_MAX];
+    uint64_t string_bytes;
+    const uint64_t* d_gate_rec;
+    uint64_t gate_n;
+    uint32_t gate_when_all;
+    uint32_t reserved;
+} sym_flat_encode_opts;
+
 uint64_t sym_flat_encoded_size_ex(const sym_field* fields, int nfields, uint64_t n, const uint64_t* bytes,
                                   const uint64_t* items);
 int sym_flat_encode_ex(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const void* const* d_cols,
-                       const uint64_t* const* d_offs, const uint64_t* const* d_items, uint32_t service_id,
-                       uint32_t method_id, uint8_t* d_out, uint64_t* d_out_off, void* stream);
-/* sym_flat_encode_ex2: as sym_flat_encode_ex; framed != 0 writes each record as [u32 size][record] (what
- * the outer level's body holds for one item: d_out_off are the frames' offsets, 4n more bytes), so an
- * outer message field takes the items with SYM_FIELD_FRAMED and its bodies become one window each
- * ([u32 count] and the items' frames for a repeated field; the frame for a nested one).
- * string_bytes: the caller's estimate of the string / bytes fields' payload bytes (0: unknown); a
- * level of short strings is then written with more payload windows per 16-byte chunk. */
-int sym_flat_encode_ex2(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const void* const* d_cols,
-                        const uint64_t* const* d_offs, const uint64_t* const* d_items, uint32_t service_id,
-                        uint32_t method_id, int framed, uint64_t string_bytes, uint8_t* d_out, uint64_t* d_out_off,
-                        void* stream);
-int sym_flat_decode_ex(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const uint8_t* d_in,
-                       const uint64_t* d_rec_off, void* const* d_cols, const uint64_t* caps, uint64_t* const* d_offs,
-                       uint64_t* const* d_items, const uint64_t* item_caps, uint8_t* d_status, uint8_t* d_fail,
-                       void* stream);
-int sym_flat_decode_ex2(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const uint8_t* d_in,
-                        const uint64_t* d_rec_src, const uint64_t* d_rec_len, const uint64_t* d_lo,
-                        const uint64_t* d_hi, void* const* d_cols, const uint64_t* caps, uint64_t* const* d_offs,
-                        uint64_t* const* d_items, uint64_t* const* d_item_len, const uint64_t* item_caps,
-                        uint8_t* d_status, uint8_t* d_fail, void* stream);
-int sym_flat_nested_status(sym_ctx* ctx, const sym_field* fields, int nfields, int field, uint64_t n,
-                           const uint64_t* d_rec_items, const uint8_t* d_item_status, uint8_t* d_status,
-                           uint8_t* d_fail, void* stream);
-int sym_flat_list_sizes(sym_ctx* ctx, int nl, uint64_t n, const uint64_t* const* d_recs,
+                       const uint64_t* const* d_offs, const uint64_t* const* d_items, const sym_flat_encode_opts* opts,
+                       uint8_t* d_out, uint64_t* d_out_off, void* stream);
+int sym_flat_decode_ex(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const uint64_t* d_n,
+                       const uint8_t* d_in, const uint64_t* d_rec_src, const uint64_t* d_rec_len, const uint64_t* d_lo,
+                       const uint64_t* d_hi, void* const* d_cols, const uint64_t* caps, uint64_t* const* d_offs,
+                       uint64_t* const* d_items, uint64_t* const* d_item_len, const uint64_t* item_caps,
+                       uint8_t* d_status, uint8_t* d_fail, void* stream);
+int sym_flat_nested_status(sym_ctx* ctx, const sym_field* fields, int nfields, int nk, const int* ks, uint64_t n,
+                           const uint64_t* d_n, const uint64_t* const* d_rec_items,
+                           const uint8_t* const* d_item_status, uint8_t* d_status, uint8_t* d_fail, void* stream);
+int sym_flat_list_sizes(sym_ctx* ctx, int nl, uint64_t n, const uint64_t* d_n, const uint64_t* const* d_recs,
                         const uint64_t* const* d_items, const uint64_t* item_caps, uint64_t* d_out, void* stream);
-int sym_flat_decode_ex3(sym_ctx* ctx, const sym_field* fields, int nfields, uint64_t n, const uint64_t* d_n,
-                        const uint8_t* d_in, const uint64_t* d_rec_src, const uint64_t* d_rec_len,
-                        const uint64_t* d_lo, const uint64_t* d_hi, void* const* d_cols, const uint64_t* caps,
-                        uint64_t* const* d_offs, uint64_t* const* d_items, uint64_t* const* d_item_len,
-                        const uint64_t* item_caps, uint8_t* d_status, uint8_t* d_fail, void* stream);
-int sym_flat_nested_status2(sym_ctx* ctx, const sym_field* fields, int nfields, int nk, const int* ks, uint64_t n,
-                            const uint64_t* d_n, const uint64_t* const* d_rec_items,
-                            const uint8_t* const* d_item_status, uint8_t* d_status, uint8_t* d_fail, void* stream);
-int sym_flat_list_sizes2(sym_ctx* ctx, int nl, uint64_t n, const uint64_t* d_n, const uint64_t* const* d_recs,
-                         const uint64_t* const* d_items, const uint64_t* item_caps, uint64_t* d_out, void* stream);
 
 /* ---- Batched Raw setters ----------------------------------------------------
  * XxxRaw.SetF(v_i) on buffer i of a flat schema (generator main.go:1038-1093 assertions,

@@ -40,7 +40,7 @@ def test_symbols_are_extern_c():
 
 def test_schema_metadata_matches_python():
     L = _native.lib()
-    assert L.sym_abi_version() == 1
+    assert L.sym_abi_version() == 2
     for s in schemas.ALL:
         nf, nv = ctypes.c_int(), ctypes.c_int()
         assert L.sym_schema_info(s.schema_id, ctypes.byref(nf), ctypes.byref(nv)) == 0

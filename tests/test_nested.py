@@ -287,6 +287,79 @@ def test_gpu_nested_item_count_checked(codec, dev):
         codec.check()
 
 
+WRAP = S("Wrap", (F("Inner", "message", message=LEVEL1),))  # one private nested message: a wrapper
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nil_every", [0, 1, 7])
+@pytest.mark.parametrize("ids", [(0, 0), (3, 4)])
+def test_gpu_wrapper_level(codec, dev, nil_every, ids):
+    """A wrapper message (one private nested field: flat._wrapper) is written by its inner level's
+    kernel -- the 18 wrapper bytes as that kernel's frame prefix -- when every record has its item,
+    and by its own kernel when one is nil (both queued, gated on the device).  Bytes == the
+    generator's either way (with the client's ID patch in [5:13]), offsets included, and the round
+    trip returns the input."""
+    from arpc_amd import flat
+    rng = random.Random(31 + nil_every)
+    n = 700
+    recs = [{"Inner": None if nil_every and i % nil_every == 3 else rand_rec(rng, LEVEL1)} for i in range(n)]
+    if nil_every == 1:  # every record nil
+        recs = [{"Inner": None} for _ in range(n)]
+    data, off = flat.encode(codec, WRAP, to_columns(WRAP, recs, dev), service_id=ids[0], method_id=ids[1])
+    codec.check()
+    got = data.cpu().numpy().tobytes()
+    o = off.cpu().numpy()
+    want = []
+    for r in recs:
+        b = bytearray(ref.marshal(WRAP, r))
+        b[5:13] = struct.pack("<II", *ids)
+        want.append(bytes(b))
+    assert o[0] == 0 and [got[o[i]:o[i + 1]] for i in range(n)] == want
+    assert len(got) == sum(len(w) for w in want)
+    cols, st = flat.decode(codec, WRAP, data, off)
+    codec.check()
+    assert (st.cpu().numpy() == 0).all()
+    assert from_columns(WRAP, cols, n) == [full(WRAP, r) for r in recs]
+
+
+@pytest.mark.gpu
+def test_gpu_wrapper_level_bad_item_ranges(codec, dev):
+    """Item ranges that sum to n but give one record two items (and another none): the fused path's
+    gate passes, and its per-record check reports what the wrapper's own kernel would
+    (SYM_ERR_INVALID, "more than one item for a nested field")."""
+    from arpc_amd import flat
+    recs = [{"Inner": {"L1Data": b"x"}}, {"Inner": {"L1Data": b"y"}}]
+    cols = to_columns(WRAP, recs, dev)
+    cols[0].rec = torch.tensor([0, 2, 2], dtype=torch.int64, device=dev)
+    flat.encode(codec, WRAP, cols)
+    with pytest.raises(Exception):
+        codec.check()
+
+
+@pytest.mark.gpu
+def test_gpu_wrapper_under_graph_capture(dev):
+    """The two gated alternatives replay from one captured graph, which follows the data: item ranges
+    refilled in place switch a replay from the fused path to the wrapper's own kernel."""
+    from arpc_amd import flat
+    rng = random.Random(5)
+    n = 300
+    recs = [{"Inner": rand_rec(rng, LEVEL1)} for _ in range(n)]
+    cols = to_columns(WRAP, recs, dev)
+    g = flat.EncodeGraph(dev, WRAP, cols)
+    for rep in range(2):
+        data, off = g.replay()
+        torch.cuda.synchronize()
+        g.codec.check()
+        o = off.cpu().numpy()
+        got = data.cpu().numpy().tobytes()
+        assert [got[o[i]:o[i + 1]] for i in range(n)] == [ref.marshal(WRAP, r) for r in recs], rep
+        # refill the item ranges in place: record 5 loses its item, records after it take the next one
+        rec = np.arange(n + 1, dtype=np.int64)
+        rec[6:] -= 1
+        cols[0].rec.copy_(torch.from_numpy(rec))
+        recs = recs[:5] + [{"Inner": None}] + recs[5:-1]
+
+
 def tree_records(schema, nodes, n):
     """arpc_amd.datagen column trees -> Python records (the restatement's input form)."""
     recs = [dict() for _ in range(n)]
@@ -335,8 +408,8 @@ def test_gpu_online_boutique(codec, dev):
 
 @pytest.mark.gpu
 def test_gpu_in_place_level_matches_packed_items(codec, dev):
-    """sym_flat_decode_ex2 leaves a message field's items in place ((offset, length) into the input);
-    sym_flat_decode_ex's packed form gathers them into an item column.  The inner level decoded from
+    """sym_flat_decode_ex with d_item_len leaves a message field's items in place ((offset, length)
+    into the input); without it the items are gathered into an item column.  The inner level decoded from
     either is the same (boutique OrderResults -> their repeated OrderItems)."""
     from arpc_amd import _native, datagen, flat
     from arpc_amd.codec import _dptr
@@ -374,10 +447,10 @@ def test_gpu_in_place_level_matches_packed_items(codec, dev):
                 ilens.append(0)
                 icaps.append(0)
         st = torch.empty(n, dtype=torch.uint8, device=dev)
-        _native.check(codec._lib.sym_flat_decode_ex2(
-            codec._ctx, outer.c_fields(), len(outer.fields), n, _dptr(ob), _dptr(oo), 0, 0, 0,
+        _native.check(codec._lib.sym_flat_decode_ex(
+            codec._ctx, outer.c_fields(), len(outer.fields), n, None, _dptr(ob), _dptr(oo), 0, 0, 0,
             _native.ptr_array(cols), _native.u64_array(caps), _native.ptr_array(offs), _native.ptr_array(items),
-            _native.ptr_array(ilens), _native.u64_array(icaps), _dptr(st), 0, 0), "sym_flat_decode_ex2")
+            _native.ptr_array(ilens), _native.u64_array(icaps), _dptr(st), 0, 0), "sym_flat_decode_ex")
         codec.check()
         assert (st.cpu().numpy() == 0).all()
         it = t[k]
@@ -399,7 +472,7 @@ def test_gpu_in_place_level_matches_packed_items(codec, dev):
 
 
 @pytest.mark.gpu
-def test_gpu_decode_ex2_argument_checks(codec, dev):
+def test_gpu_decode_ex_in_place_argument_checks(codec, dev):
     from arpc_amd import _native, flat
     from arpc_amd.codec import _dptr
     sch = flat.OB_MONEY  # no message field
@@ -414,13 +487,13 @@ def test_gpu_decode_ex2_argument_checks(codec, dev):
     args = dict(cols=_native.ptr_array([_dptr(b), _dptr(v), _dptr(v)]), caps=_native.u64_array([64, 0, 0]),
                 offs=_native.ptr_array([_dptr(o), 0, 0]))
     # records in place need the input's extent
-    rc = codec._lib.sym_flat_decode_ex2(codec._ctx, cf, 3, 1, _dptr(data), _dptr(off), _dptr(ln), 0, 0, args["cols"],
+    rc = codec._lib.sym_flat_decode_ex(codec._ctx, cf, 3, 1, None, _dptr(data), _dptr(off), _dptr(ln), 0, 0, args["cols"],
                                         args["caps"], args["offs"], None, None, None, _dptr(st), 0, 0)
     assert rc == _native.SYM_ERR_INVALID
     # an in-place item column only for a message field
     io = torch.empty(2, dtype=torch.int64, device=dev)
     sch2 = flat.FlatSchema("L", (flat.FlatField("S", "string", repeated=True),))
-    rc = codec._lib.sym_flat_decode_ex2(codec._ctx, sch2.c_fields(), 1, 1, _dptr(data), _dptr(off), 0, 0, 0,
+    rc = codec._lib.sym_flat_decode_ex(codec._ctx, sch2.c_fields(), 1, 1, None, _dptr(data), _dptr(off), 0, 0, 0,
                                         _native.ptr_array([_dptr(b)]), _native.u64_array([64]),
                                         _native.ptr_array([_dptr(o)]), _native.ptr_array([_dptr(io)]),
                                         _native.ptr_array([_dptr(io)]), _native.u64_array([1]), _dptr(st), 0, 0)
