@@ -54,6 +54,39 @@ __global__ __launch_bounds__(256) void k0_4(const uint8_t* __restrict__ in, uint
     if (k == 0x12345u) sink[threadIdx.x] = k;
 }
 
+// the same 4-byte loads with other cache policies (gfx950 sc0 / sc1 / nt bits), aligned to 4 here
+__global__ __launch_bounds__(256) void k0_nt(const uint8_t* __restrict__ in, uint64_t n, uint32_t* sink) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t k = __builtin_nontemporal_load((const uint32_t*)(in + 352 * i + 24));
+    if (k == 0x12345u) sink[threadIdx.x] = k;
+}
+__global__ __launch_bounds__(256) void k0_sc1(const uint8_t* __restrict__ in, uint64_t n, uint32_t* sink) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t k = __hip_atomic_load((const uint32_t*)(in + 352 * i + 24), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (k == 0x12345u) sink[threadIdx.x] = k;
+}
+__global__ __launch_bounds__(256) void k0_sys(const uint8_t* __restrict__ in, uint64_t n, uint32_t* sink) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t k = __hip_atomic_load((const uint32_t*)(in + 352 * i + 24), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (k == 0x12345u) sink[threadIdx.x] = k;
+}
+__global__ __launch_bounds__(256) void k0_ntsc(const uint8_t* __restrict__ in, uint64_t n, uint32_t* sink) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    uint32_t k;
+    asm volatile("global_load_dword %0, %1, off sc0 sc1 nt\n s_waitcnt vmcnt(0)" : "=v"(k) : "v"(in + 352 * i + 24) : "memory");
+    if (k == 0x12345u) sink[threadIdx.x] = k;
+}
+__global__ __launch_bounds__(256) void k0_a4(const uint8_t* __restrict__ in, uint64_t n, uint32_t* sink) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t k = *(const uint32_t*)(in + 352 * i + 24);
+    if (k == 0x12345u) sink[threadIdx.x] = k;
+}
+
 __global__ __launch_bounds__(256) void parser(const uint8_t* __restrict__ in, const uint64_t* __restrict__ off,
                                                uint64_t n, uint32_t* sink) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
@@ -85,11 +118,11 @@ int main(int argc, char** argv) {
     uint64_t* off;
     uint32_t* sink;
     CK(hipMalloc(&a, big));
-    CK(hipMalloc(&s, rec * n + 64));
+    CK(hipMalloc(&s, 352 * n + 64));
     CK(hipMalloc(&off, 8 * (n + 1)));
     CK(hipMalloc(&sink, 4096));
     CK(hipMemset(a, 1, big));
-    CK(hipMemset(s, 2, rec * n + 64));
+    CK(hipMemset(s, 2, 352 * n + 64));
     store8<<<(n + 1 + 255) / 256, 256>>>(off, n + 1);
     CK(hipDeviceSynchronize());
     hipEvent_t e0, e1;
@@ -102,7 +135,8 @@ int main(int argc, char** argv) {
         int which;
     } ks[] = {{"stream16", (double)big, 0}, {"off8", 8.0 * (n + 1), 1}, {"k0_4", 4.0 * n, 2},
               {"parser", 8.0 * (n + 1) + 4.0 * n, 3}, {"store16", (double)(256ull << 20), 4},
-              {"store8", 8.0 * (n + 1), 5}, {"store1", (double)n, 6}};
+              {"store8", 8.0 * (n + 1), 5}, {"store1", (double)n, 6}, {"k0_a4", 4.0 * n, 7}, {"k0_nt", 4.0 * n, 8},
+              {"k0_sc1", 4.0 * n, 9}, {"k0_sys", 4.0 * n, 10}, {"k0_ntsc", 4.0 * n, 11}};
     for (const K& k : ks) {
         float best = 1e30f;
         for (int r = 0; r < reps; ++r) {
@@ -117,6 +151,11 @@ int main(int argc, char** argv) {
                 case 4: store16<<<4096, 256>>>((uint4*)a, (256ull << 20) / 16); break;
                 case 5: store8<<<(n + 1 + 255) / 256, 256>>>(off, n + 1); break;
                 case 6: store1<<<g, 256>>>(s, n); break;
+                case 7: k0_a4<<<g, 256>>>(s, n, sink); break;
+                case 8: k0_nt<<<g, 256>>>(s, n, sink); break;
+                case 9: k0_sc1<<<g, 256>>>(s, n, sink); break;
+                case 10: k0_sys<<<g, 256>>>(s, n, sink); break;
+                case 11: k0_ntsc<<<g, 256>>>(s, n, sink); break;
             }
             CK(hipEventRecord(e1));
             CK(hipEventSynchronize(e1));
