@@ -14,7 +14,7 @@
 //   worker   poll `posted` (one 8-byte PCIe read) while cold; when it passed the records served -- or
 //            at once while hot (a record within the last 50 us) -- every lane of the first kRingSlots (256)
 //            looks at one slot of the window [e, e + kRingSlots) (req and in_len|kind in one round trip)
-//            and the ready ones are served, one wave per record, 16 at once: the record is read into
+//            and the ready ones are served, one half-wave per record, 32 at once: the record is read into
 //            LDS with system-scope 8-byte loads and encoded or parsed there exactly as MarshalSymphony /
 //            UnmarshalSymphony (kv.syn.go:611-745, echo.syn.go:111-263), each 8-byte word of the result
 //            built from LDS and written with a system-scope store, waited for, then done = t + 1
@@ -40,12 +40,14 @@ __device__ __forceinline__ void st_sys(u64* p, u64 v) { __hip_atomic_store(p, v,
 __device__ __forceinline__ void fence_sys() { __atomic_thread_fence(__ATOMIC_SEQ_CST); }
 typedef u64 u64x2 __attribute__((ext_vector_type(2)));
 
-constexpr int kThreads = 1024;  // 16 waves: up to 16 records served at once (each latency-bound)
+constexpr int kThreads = 1024;  // 16 waves
 constexpr int kWaves = kThreads / 64;
+constexpr int kServers = 2 * kWaves;  // a record per half-wave: 32 records served at once (each latency-bound)
+constexpr int kSub = 32;              // lanes per server
 constexpr u64 kHotTicks = 5000;  // 50 us after the last record the worker polls the slots directly
 
 struct alignas(16) Lds {
-    uint8_t in[kWaves][kSlotIn + 16];  // a wave's record (results are built from it word by word)
+    uint8_t in[kServers][kSlotIn + 16];  // a server's record (results are built from it word by word)
     u64 served[kRingSlots];  // served[t % kRingSlots] == t + 1: ticket t was served by a worker
     int list[kRingSlots];    // ready tickets of this pass (offsets from e)
     u32 len[kRingSlots];     // and their in_len
@@ -69,17 +71,18 @@ __device__ __forceinline__ u64 rd64(const uint8_t* b) {  // 8 bytes from any LDS
     return v;
 }
 
-// One wave copies `bytes` (rounded up to 8) from host memory at src (8-byte aligned) into LDS with
-// system-scope 8-byte loads: they read the caller's bytes from host memory, never a cached copy.
-__device__ __forceinline__ void load_in(uint8_t* dst, const uint8_t* src, u64 bytes, int lane) {
-    for (u64 c = 8 * (u64)lane; c < bytes; c += 8 * 64) *(u64*)(dst + c) = ld_sys((const u64*)(src + c));
+// One server (kSub lanes, sl = its lane) copies `bytes` (rounded up to 8) from host memory at src
+// (8-byte aligned) into LDS with system-scope 8-byte loads: they read the caller's bytes from host
+// memory, never a cached copy.
+__device__ __forceinline__ void load_in(uint8_t* dst, const uint8_t* src, u64 bytes, int sl) {
+    for (u64 c = 8 * (u64)sl; c < bytes; c += 8 * kSub) *(u64*)(dst + c) = ld_sys((const u64*)(src + c));
 }
-// One wave writes words [0, words) of a result, word(w) computed from LDS, to host memory at dst
+// One server writes words [0, words) of a result, word(w) computed from LDS, to host memory at dst
 // with system-scope 8-byte stores, then waits until they are performed: the done flag that follows
 // cannot overtake them.
 template <class W>
-__device__ __forceinline__ void store_words(uint8_t* dst, u64 words, int lane, W&& word) {
-    for (u64 w = (u64)lane; w < words; w += 64) st_sys((u64*)dst + w, word(w));
+__device__ __forceinline__ void store_words(uint8_t* dst, u64 words, int sl, W&& word) {
+    for (u64 w = (u64)sl; w < words; w += kSub) st_sys((u64*)dst + w, word(w));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -269,25 +272,28 @@ __global__ __launch_bounds__(kThreads) void worker_kernel(RingCtl* ctl, uint8_t*
         if (drain && S.owed == 0) break;  // every record this generation owes is served
         const int nl = S.nlist;
         ++passes;
-        for (int i = wave; i < nl; i += kWaves) {  // one wave per record
+        // one half-wave per record: the two halves of a wave serve two records at once (their
+        // instructions interleave under the exec mask; an encode beside a decode runs both paths)
+        const int server = 2 * wave + (lane >> 5), sl = lane & (kSub - 1);
+        for (int i = server; i < nl; i += kServers) {
             const u64 t = e + (u64)S.list[i];
             uint8_t* slot = slots + (size_t)(t % kRingSlots) * kSlotBytes;
             SlotCtl* sc = (SlotCtl*)slot;
-            uint8_t* in = S.in[wave];
+            uint8_t* in = S.in[server];
             const u64 in_len = S.len[i];
             const u32 kind = S.kind[i];
             const Layout lay{(int)((kind >> 8) & 0xff), (int)((kind >> 16) & 0xff)};
             if ((kind & 0xff) == 0) {
-                load_in(in, slot + kSlotInAt, sizeof(EncIn) + in_len, lane);
+                load_in(in, slot + kSlotInAt, sizeof(EncIn) + in_len, sl);
                 wave_sync();
-                encode_one(lay, in, slot + kSlotOutAt, lane);
+                encode_one(lay, in, slot + kSlotOutAt, sl);
             } else {
-                load_in(in, slot + kSlotInAt, in_len, lane);
+                load_in(in, slot + kSlotInAt, in_len, sl);
                 wave_sync();
-                decode_one(lay, in, in_len, slot + kSlotOutAt, lane);
+                decode_one(lay, in, in_len, slot + kSlotOutAt, sl);
             }
-            if (lane == 0) st_sys(&sc->done, t + 1);  // after the wave's stores were performed
-            wave_sync();  // the wave's in buffer is read before its next record overwrites it
+            if (sl == 0) st_sys(&sc->done, t + 1);  // after the server's stores were performed
+            wave_sync();  // the server's in buffer is read before its next record overwrites it
         }
         // the pass counters of the batchers served in this pass (issued after the records' done flags,
         // not waited for: a caller may see its record done a few microseconds before its pass counts)
