@@ -26,8 +26,8 @@
 // sym_ctx (only the current leader uses it) and a non-blocking stream.
 //
 // Records up to kRingRecordMax bytes (every kv / echo request an RPC carries in practice) take the
-// ring instead (record_worker.hip): no launch per record or batch, one persistent single-workgroup
-// worker per device -- shared by every batcher on the device and both directions, each slot carrying
+// ring instead (record_worker.hip): no launch per record or batch, one persistent launch (four
+// workgroups) per device -- shared by every batcher on the device and both directions, each slot carrying
 // its record's direction and layout -- serving tickets in place in coherent pinned slots; a record is
 // published with one store, served within a few microseconds, and read back as soon as its own flag
 // is set.  ONE worker per device, however many batchers: a persistent kernel holds the hardware queue
@@ -91,6 +91,7 @@ struct Ring {
     int device = 0;
     symhip::RingCtl* ctl = nullptr;
     uint8_t* slots = nullptr;
+    unsigned* exits = nullptr;  // device word: the worker's groups count their exits on it
     std::atomic<uint64_t> gen{0};
     std::mutex mu;
     hipStream_t stream = nullptr;
@@ -289,7 +290,7 @@ void release(Queue& q, std::unique_lock<std::mutex>& lk, BSlot& s) {
 int ring_launch(Ring& r, uint64_t gen) {
     DeviceGuard g(r.device);
     if (g.err != hipSuccess) return hip_fail(g.err, "sym_batcher: hipSetDevice");
-    hipError_t e = symhip::launch_record_worker(r.ctl, r.slots, gen, r.stream);
+    hipError_t e = symhip::launch_record_worker(r.ctl, r.slots, r.exits, gen, r.stream);
     return e == hipSuccess ? SYM_OK : hip_fail(e, "sym_batcher: record worker launch");
 }
 
@@ -311,6 +312,7 @@ void ring_destroy(Ring* r) {
     if (r->stream) (void)hipStreamDestroy(r->stream);
     if (r->slots) (void)hipHostFree(r->slots);
     if (r->ctl) (void)hipHostFree(r->ctl);
+    if (r->exits) (void)hipFree(r->exits);
     delete r;
 }
 
@@ -330,7 +332,14 @@ int ring_create(int device, Ring** out) {
         ring_destroy(r);
         return fail(SYM_ERR_NOMEM, "sym_batcher_create: ring of %d slots: %s", symhip::kRingSlots, hipGetErrorString(e));
     }
+    if (e == hipSuccess && (e = hipMalloc((void**)&r->exits, sizeof(unsigned))) == hipSuccess)
+        e = hipMemset(r->exits, 0, sizeof(unsigned));
+    if (e != hipSuccess) {
+        ring_destroy(r);
+        return hip_fail(e, "sym_batcher_create: worker exit counter");
+    }
     memset(r->ctl, 0, sizeof(symhip::RingCtl));
+    for (int w = 0; w < symhip::kGroups; ++w) r->ctl->e[w] = (uint64_t)w;  // group w's first ticket
     memset(r->slots, 0, (size_t)symhip::kRingSlots * symhip::kSlotBytes);
     for (int k = 0; k < symhip::kRingSlots; ++k)
         ((symhip::SlotCtl*)(r->slots + (size_t)k * symhip::kSlotBytes))->turn = (uint64_t)k;
@@ -346,6 +355,13 @@ int ring_create(int device, Ring** out) {
     }
     *out = r;
     return SYM_OK;
+}
+
+// Worker passes that served records of batcher id `bid` in direction `dir` (both groups).
+uint64_t ring_passes(const Ring& r, int bid, int dir) {
+    uint64_t v = 0;
+    for (int w = 0; w < symhip::kGroups; ++w) v += __atomic_load_n(&r.ctl->bpasses[w][bid][dir], __ATOMIC_ACQUIRE);
+    return v;
 }
 
 // The device's ring, created with its first batcher, and an id on it for batcher b.  The id's pass
@@ -369,7 +385,7 @@ int ring_acquire(sym_batcher* b, int device) {
     b->bid = id;
     for (int dir = 0; dir < 2; ++dir) {
         b->ring[dir] = d.ring;
-        b->pass_base[dir] = __atomic_load_n(&d.ring->ctl->bpasses[id][dir], __ATOMIC_ACQUIRE);
+        b->pass_base[dir] = ring_passes(*d.ring, id, dir);
     }
     return SYM_OK;
 }
@@ -440,7 +456,7 @@ int ring_call(sym_batcher* b, int dir, uint64_t in_len, Fill&& fill, Drain&& dra
     fill(slot + symhip::kSlotInAt);
     sc->in_len = in_len | symhip::slot_kind(dir, b->lay, b->bid);
     __atomic_store_n(&sc->req, t + 1, __ATOMIC_RELEASE);
-    __atomic_fetch_add(&r.ctl->posted, 1, __ATOMIC_SEQ_CST);  // then look at quit (the worker's hand-shake)
+    __atomic_fetch_add(&r.ctl->posted[t % symhip::kGroups], 1, __ATOMIC_SEQ_CST);  // then look at quit (hand-shake)
     rc = ring_ensure_worker(r, false);
     if (rc == SYM_OK) rc = ring_wait(r, &sc->done, t + 1);
     if (rc != SYM_OK) return rc;  // (the slot stays taken: the device failed)
@@ -645,7 +661,7 @@ int sym_batcher_stats(sym_batcher* b, uint64_t* enc_batches, uint64_t* enc_recor
     for (int dir = 0; dir < 2; ++dir) {  // batches: the batched path's launches + the ring worker's passes
         std::lock_guard<std::mutex> lk(b->q[dir].mu);
         const Ring* r = b->ring[dir];
-        const uint64_t passes = r ? __atomic_load_n(&r->ctl->bpasses[b->bid][dir], __ATOMIC_ACQUIRE) : 0;
+        const uint64_t passes = r ? ring_passes(*r, b->bid, dir) : 0;
         v[2 * dir] = b->q[dir].batches + (r ? passes - b->pass_base[dir] : 0);
         v[2 * dir + 1] = b->q[dir].records + b->ring_recs[dir].load(std::memory_order_relaxed);
     }

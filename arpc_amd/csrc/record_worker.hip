@@ -3,7 +3,7 @@
 // The reference calls Marshal / Unmarshal once per record from many goroutines at once
 // (pkg/rpc/client.go:233-310, :252; pkg/rpc/server.go:152 / :173; pkg/serializer/symphony.go:10-16).
 // A kernel launch plus a synchronisation per call costs ~10 us or more; here one small persistent
-// kernel per device (one workgroup, shared by every batcher on the device and both directions) serves
+// kernel per device (kGroups workgroups, shared by every batcher on the device and both directions) serves
 // the records in place in a ring of slots in pinned host memory that is mapped into the GPU's address
 // space and coherent both ways:
 //
@@ -12,9 +12,9 @@
 //            that it is quitting, see that the next one runs (batcher.cpp); spin until done == t + 1;
 //            copy the result out; turn = t + kRingSlots
 //   worker   poll `posted` (one 8-byte PCIe read) while cold; when it passed the records served -- or
-//            at once while hot (a record within the last 50 us) -- every lane of the first kRingSlots (256)
-//            looks at one slot of the window [e, e + kRingSlots) (req and in_len|kind in one round trip)
-//            and the ready ones are served, one half-wave per record, 32 at once: the record is read into
+//            at once while hot (a record within the last 50 us) -- each of the first kWin (128) threads
+//            looks at one slot of the group's window (req and in_len|kind in one round trip)
+//            and the ready ones are served, one wave per record, 16 at once: the record is read into
 //            LDS with system-scope 8-byte loads and encoded or parsed there exactly as MarshalSymphony /
 //            UnmarshalSymphony (kv.syn.go:611-745, echo.syn.go:111-263), each 8-byte word of the result
 //            built from LDS and written with a system-scope store, waited for, then done = t + 1
@@ -40,18 +40,18 @@ __device__ __forceinline__ void st_sys(u64* p, u64 v) { __hip_atomic_store(p, v,
 __device__ __forceinline__ void fence_sys() { __atomic_thread_fence(__ATOMIC_SEQ_CST); }
 typedef u64 u64x2 __attribute__((ext_vector_type(2)));
 
-constexpr int kThreads = 1024;  // 16 waves
+constexpr int kThreads = 1024;  // 16 waves: up to 16 records served at once (each latency-bound)
 constexpr int kWaves = kThreads / 64;
-constexpr int kServers = 2 * kWaves;  // a record per half-wave: 32 records served at once (each latency-bound)
-constexpr int kSub = 32;              // lanes per server
 constexpr u64 kHotTicks = 5000;  // 50 us after the last record the worker polls the slots directly
+constexpr int kWin = kRingSlots / kGroups;  // a group's window: tickets e, e + kGroups, ... (one slot each)
+static_assert(kRingSlots % kGroups == 0 && kWin <= kThreads, "window");
 
 struct alignas(16) Lds {
-    uint8_t in[kServers][kSlotIn + 16];  // a server's record (results are built from it word by word)
-    u64 served[kRingSlots];  // served[t % kRingSlots] == t + 1: ticket t was served by a worker
-    int list[kRingSlots];    // ready tickets of this pass (offsets from e)
-    u32 len[kRingSlots];     // and their in_len
-    u32 kind[kRingSlots];    // and kind (slot_kind >> 32)
+    uint8_t in[kWaves][kSlotIn + 16];  // a wave's record (results are built from it word by word)
+    u64 served[kWin];        // served[widx(t)] == t + 1: this group's ticket t was served
+    int list[kWin];          // ready tickets of this pass (window positions: ticket e + kGroups * k)
+    u32 len[kWin];           // and their in_len
+    u32 kind[kWin];          // and kind (slot_kind >> 32)
     int nlist;
     int owed;                // draining: ready tickets below t0 in this pass
     int drain;               // 1: the exit is announced (serve what is owed, then leave)
@@ -71,18 +71,17 @@ __device__ __forceinline__ u64 rd64(const uint8_t* b) {  // 8 bytes from any LDS
     return v;
 }
 
-// One server (kSub lanes, sl = its lane) copies `bytes` (rounded up to 8) from host memory at src
-// (8-byte aligned) into LDS with system-scope 8-byte loads: they read the caller's bytes from host
-// memory, never a cached copy.
-__device__ __forceinline__ void load_in(uint8_t* dst, const uint8_t* src, u64 bytes, int sl) {
-    for (u64 c = 8 * (u64)sl; c < bytes; c += 8 * kSub) *(u64*)(dst + c) = ld_sys((const u64*)(src + c));
+// One wave copies `bytes` (rounded up to 8) from host memory at src (8-byte aligned) into LDS with
+// system-scope 8-byte loads: they read the caller's bytes from host memory, never a cached copy.
+__device__ __forceinline__ void load_in(uint8_t* dst, const uint8_t* src, u64 bytes, int lane) {
+    for (u64 c = 8 * (u64)lane; c < bytes; c += 8 * 64) *(u64*)(dst + c) = ld_sys((const u64*)(src + c));
 }
-// One server writes words [0, words) of a result, word(w) computed from LDS, to host memory at dst
+// One wave writes words [0, words) of a result, word(w) computed from LDS, to host memory at dst
 // with system-scope 8-byte stores, then waits until they are performed: the done flag that follows
 // cannot overtake them.
 template <class W>
-__device__ __forceinline__ void store_words(uint8_t* dst, u64 words, int sl, W&& word) {
-    for (u64 w = (u64)sl; w < words; w += kSub) st_sys((u64*)dst + w, word(w));
+__device__ __forceinline__ void store_words(uint8_t* dst, u64 words, int lane, W&& word) {
+    for (u64 w = (u64)lane; w < words; w += 64) st_sys((u64*)dst + w, word(w));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -205,18 +204,27 @@ __device__ void decode_one(const Layout lay, const uint8_t* in, u64 L, uint8_t* 
 // worker keeps scanning until a pass finds no ready ticket below T0 in its window; a ready ticket
 // below T0 outside the window waits behind a lower one whose caller published after the
 // announcement, and the next generation serves both.
-__global__ __launch_bounds__(kThreads) void worker_kernel(RingCtl* ctl, uint8_t* slots, u64 gen) {
+// kGroups (4) workgroups run as one launch, so the worker still holds one hardware queue: group w
+// serves the tickets t with t % kGroups == w -- its own window, `posted` word, counters and exit --
+// so kGroups passes are in flight at once (a pass is a few PCIe round trips whatever its size: one
+// group served both directions at ~0.65 M records/s from 64 threads, four at ~0.86 M).  Each group
+// announces and drains as above for its own tickets (all reach kLifeTicks together); the last group
+// to leave publishes `gone`.
+__device__ __forceinline__ int widx(u64 t) { return (int)((t % kRingSlots) / kGroups); }
+
+__global__ __launch_bounds__(kThreads) void worker_kernel(RingCtl* ctl, uint8_t* slots, unsigned* exits, u64 gen) {
     __shared__ Lds S;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    u64 e = ld_sys(&ctl->e), nproc = ld_sys(&ctl->nproc);  // where the previous worker stopped
+    const int grp = blockIdx.x;
+    u64 e = ld_sys(&ctl->e[grp]), nproc = ld_sys(&ctl->nproc[grp]);  // where the group's previous run stopped
     // tickets of the window the previous worker served out of order
-    for (int k = tid; k < kRingSlots; k += kThreads) {
-        const u64 t = e + (u64)k;
+    for (int k = tid; k < kWin; k += kThreads) {
+        const u64 t = e + (u64)kGroups * k;
         const SlotCtl* sc = (const SlotCtl*)(slots + (size_t)(t % kRingSlots) * kSlotBytes);
         const u64 d = ld_sys(&sc->done);
-        S.served[t % kRingSlots] = d == t + 1 ? t + 1 : 0;
+        S.served[widx(t)] = d == t + 1 ? t + 1 : 0;
     }
-    for (int k = tid; k < 2 * kMaxBatchers; k += kThreads) S.bp[k] = ld_sys(&ctl->bpasses[k >> 1][k & 1]);
+    for (int k = tid; k < 2 * kMaxBatchers; k += kThreads) S.bp[k] = ld_sys(&ctl->bpasses[grp][k >> 1][k & 1]);
     if (tid == 0) {
         S.drain = 0;
         S.t0 = 0;
@@ -225,7 +233,7 @@ __global__ __launch_bounds__(kThreads) void worker_kernel(RingCtl* ctl, uint8_t*
     __syncthreads();
     const u64 born = __builtin_amdgcn_s_memrealtime();
     u64 progress = born;  // when a record was last served (every thread)
-    u64 served = tid == 0 ? ld_sys(&ctl->served) : 0, passes = tid == 0 ? ld_sys(&ctl->passes) : 0;
+    u64 served = tid == 0 ? ld_sys(&ctl->served[grp]) : 0, passes = tid == 0 ? ld_sys(&ctl->passes[grp]) : 0;
     auto announce = [&]() {  // (thread 0)
         st_sys(&ctl->quit, gen);
         fence_sys();
@@ -239,7 +247,7 @@ __global__ __launch_bounds__(kThreads) void worker_kernel(RingCtl* ctl, uint8_t*
             S.nlist = 0;
             S.owed = 0;
             while (!S.drain && !S.hot) {
-                const u64 posted = ld_sys(&ctl->posted);
+                const u64 posted = ld_sys(&ctl->posted[grp]);
                 const u64 now = __builtin_amdgcn_s_memrealtime();
                 if (ld_sys(&ctl->stop) || now - progress > kIdleTicks || now - born > kLifeTicks) announce();
                 else if (posted != nproc) break;  // published records not served yet
@@ -252,13 +260,13 @@ __global__ __launch_bounds__(kThreads) void worker_kernel(RingCtl* ctl, uint8_t*
         // ---- the window: which tickets are ready and not served yet (req and in_len in one round trip) ----
         const u64 t0 = S.t0;
         const bool drain = S.drain;
-        if (tid < kRingSlots) {
-            const u64 t = e + (u64)tid;
+        if (tid < kWin) {
+            const u64 t = e + (u64)kGroups * tid;
             const SlotCtl* sc = (const SlotCtl*)(slots + (size_t)(t % kRingSlots) * kSlotBytes);
             // req and in_len in one system-coherent 16-byte load (volatile: sc0 sc1, as ld_sys)
             const u64x2 ri = *(const volatile u64x2*)&sc->req;
             const u64 rq = ri.x, il = ri.y;
-            if (S.served[t % kRingSlots] != t + 1 && rq == t + 1) {
+            if (S.served[widx(t)] != t + 1 && rq == t + 1) {
                 const int k = atomicAdd(&S.nlist, 1);
                 S.list[k] = tid;
                 S.len[k] = (u32)min(il & 0xffffffffull, (u64)kRingRecordMax);  // (the caller checked it)
@@ -272,49 +280,46 @@ __global__ __launch_bounds__(kThreads) void worker_kernel(RingCtl* ctl, uint8_t*
         if (drain && S.owed == 0) break;  // every record this generation owes is served
         const int nl = S.nlist;
         ++passes;
-        // one half-wave per record: the two halves of a wave serve two records at once (their
-        // instructions interleave under the exec mask; an encode beside a decode runs both paths)
-        const int server = 2 * wave + (lane >> 5), sl = lane & (kSub - 1);
-        for (int i = server; i < nl; i += kServers) {
-            const u64 t = e + (u64)S.list[i];
+        for (int i = wave; i < nl; i += kWaves) {  // one wave per record
+            const u64 t = e + (u64)kGroups * S.list[i];
             uint8_t* slot = slots + (size_t)(t % kRingSlots) * kSlotBytes;
             SlotCtl* sc = (SlotCtl*)slot;
-            uint8_t* in = S.in[server];
+            uint8_t* in = S.in[wave];
             const u64 in_len = S.len[i];
             const u32 kind = S.kind[i];
             const Layout lay{(int)((kind >> 8) & 0xff), (int)((kind >> 16) & 0xff)};
             if ((kind & 0xff) == 0) {
-                load_in(in, slot + kSlotInAt, sizeof(EncIn) + in_len, sl);
+                load_in(in, slot + kSlotInAt, sizeof(EncIn) + in_len, lane);
                 wave_sync();
-                encode_one(lay, in, slot + kSlotOutAt, sl);
+                encode_one(lay, in, slot + kSlotOutAt, lane);
             } else {
-                load_in(in, slot + kSlotInAt, in_len, sl);
+                load_in(in, slot + kSlotInAt, in_len, lane);
                 wave_sync();
-                decode_one(lay, in, in_len, slot + kSlotOutAt, sl);
+                decode_one(lay, in, in_len, slot + kSlotOutAt, lane);
             }
-            if (sl == 0) st_sys(&sc->done, t + 1);  // after the server's stores were performed
-            wave_sync();  // the server's in buffer is read before its next record overwrites it
+            if (lane == 0) st_sys(&sc->done, t + 1);  // after the wave's stores were performed
+            wave_sync();  // the wave's in buffer is read before its next record overwrites it
         }
         // the pass counters of the batchers served in this pass (issued after the records' done flags,
         // not waited for: a caller may see its record done a few microseconds before its pass counts)
         if (tid < 2 * kMaxBatchers && (S.bseen[tid >> 5] >> (tid & 31) & 1u))
-            st_sys(&ctl->bpasses[tid >> 1][tid & 1], ++S.bp[tid]);
+            st_sys(&ctl->bpasses[grp][tid >> 1][tid & 1], ++S.bp[tid]);
         __syncthreads();
         // ---- served: advance the window over its served prefix ----
         for (int i = tid; i < nl; i += kThreads) {
-            const u64 t = e + (u64)S.list[i];
-            S.served[t % kRingSlots] = t + 1;
+            const u64 t = e + (u64)kGroups * S.list[i];
+            S.served[widx(t)] = t + 1;
         }
         __syncthreads();
         nproc += (u64)nl;
-        while (S.served[e % kRingSlots] == e + 1) ++e;  // (every thread, the same walk)
+        while (S.served[widx(e)] == e + 1) e += kGroups;  // (every thread, the same walk)
         const u64 now = __builtin_amdgcn_s_memrealtime();
         if (nl) {
             progress = now;
             if (tid == 0) {  // (stores only: the counters of earlier workers were read at the start)
                 served += (u64)nl;
-                st_sys(&ctl->served, served);
-                st_sys(&ctl->passes, passes);
+                st_sys(&ctl->served[grp], served);
+                st_sys(&ctl->passes[grp], passes);
                 S.hot = 1;
             }
         } else {
@@ -324,19 +329,23 @@ __global__ __launch_bounds__(kThreads) void worker_kernel(RingCtl* ctl, uint8_t*
         }
         __syncthreads();
     }
-    if (tid == 0) {  // where the next worker starts; then gone (the callers' hand-shake)
-        st_sys(&ctl->e, e);
-        st_sys(&ctl->nproc, nproc);
-        st_sys(&ctl->passes, passes);
+    if (tid == 0) {  // where the group's next run starts; the last group out publishes gone
+        st_sys(&ctl->e[grp], e);
+        st_sys(&ctl->nproc[grp], nproc);
+        st_sys(&ctl->passes[grp], passes);
         fence_sys();
-        st_sys(&ctl->gone, gen);
+        if (atomicAdd(exits, 1u) == kGroups - 1) {
+            __hip_atomic_store(exits, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next launch
+            fence_sys();
+            st_sys(&ctl->gone, gen);
+        }
     }
 }
 
 }  // namespace rw
 
-hipError_t launch_record_worker(RingCtl* ctl, uint8_t* slots, uint64_t gen, hipStream_t stream) {
-    hipLaunchKernelGGL(rw::worker_kernel, dim3(1), dim3(rw::kThreads), 0, stream, ctl, slots, (u64)gen);
+hipError_t launch_record_worker(RingCtl* ctl, uint8_t* slots, unsigned* exits, uint64_t gen, hipStream_t stream) {
+    hipLaunchKernelGGL(rw::worker_kernel, dim3(kGroups), dim3(rw::kThreads), 0, stream, ctl, slots, exits, (u64)gen);
     return hipGetLastError();
 }
 

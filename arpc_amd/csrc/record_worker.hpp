@@ -23,21 +23,23 @@ constexpr uint64_t kRingRecordMax = 4000;  // records (encode: field bytes; deco
                                            // this go through the ring; larger ones through batches
 constexpr uint64_t kIdleTicks = 2000000;   // 20 ms without a record (s_memrealtime, 100 MHz): the worker exits
 constexpr int kMaxBatchers = 256;         // batchers per device ring (their pass counters)
+constexpr int kGroups = 4;                 // worker workgroups of one launch: group w serves tickets t % kGroups == w
 constexpr uint64_t kLifeTicks = 200000;    // 2 ms: a busy worker hands over to a fresh launch, so work queued
                                            // behind it on a shared hardware queue waits at most this long
 
 struct RingCtl {          // one per device, written as commented
-    uint64_t posted;      // callers: records published so far (atomic add after the slot's req store)
+    uint64_t posted[kGroups];  // callers: records published so far per ticket class t % kGroups (atomic add
+                               // after the slot's req store)
     uint64_t stop;        // host: leave now (last sym_batcher_destroy of the device, sym_batcher_quiesce)
     uint64_t quit;        // worker: the generation that is about to exit (0: none)
-    uint64_t gone;        // worker: the generation that has exited
-    uint64_t e, nproc;    // worker, at exit: its window base and records served (the next one resumes)
-    uint64_t served;      // worker: records served so far, every pass
-    uint64_t passes;      // worker: passes that served records, every pass
+    uint64_t gone;        // worker: the generation that has exited (its last group)
+    uint64_t e[kGroups], nproc[kGroups];  // worker group, at exit: its window base and records served
+    uint64_t served[kGroups];  // worker group: records served so far, every pass
+    uint64_t passes[kGroups];  // worker group: passes that served records, every pass
     uint64_t ticket;      // callers: the next ticket (atomic fetch-add); the worker reads it when it
                           // announces its exit: every record it still owes has a smaller ticket
-    uint64_t bpasses[kMaxBatchers][2];  // worker: passes that served records of batcher id b, direction d
-                                        // (stored after those records' done flags; sym_batcher_stats)
+    uint64_t bpasses[kGroups][kMaxBatchers][2];  // worker group: passes that served records of batcher id b,
+                                                 // direction d (stored after those records' done flags)
 };
 
 // A record's kind, in the high half of SlotCtl::in_len: direction (0 encode, 1 decode), layout and
@@ -77,6 +79,7 @@ static_assert(sizeof(DecOut) <= kDecData, "DecOut layout");
 static_assert(kDecData + 2 * (kRingRecordMax + 16) <= kSlotOut, "decode out area");
 static_assert(sizeof(EncIn) + kRingRecordMax <= kSlotIn, "encode in area");
 
-hipError_t launch_record_worker(RingCtl* ctl, uint8_t* slots, uint64_t gen, hipStream_t stream);
+// exits: a device word the worker's groups count their exits on (zero between launches)
+hipError_t launch_record_worker(RingCtl* ctl, uint8_t* slots, unsigned* exits, uint64_t gen, hipStream_t stream);
 
 }  // namespace symhip

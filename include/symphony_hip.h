@@ -216,8 +216,8 @@ int sym_decode_host(sym_ctx* ctx, int schema, uint64_t n, const uint8_t* h_in, c
  * A batcher serves those concurrent one-record calls without a launch per call.  Records of up to
  * 4000 bytes (encode: the fields' bytes; decode: the record) go through a ring of 256 slots in
  * coherent pinned host memory, one ring per DEVICE shared by all its batchers and both
- * directions: the caller writes its record into a slot and publishes it, a persistent one-workgroup
- * kernel (started with the device's first batcher, restarted by the next call after it leaves)
+ * directions: the caller writes its record into a slot and publishes it, a persistent kernel (one
+ * launch of four workgroups; started with the device's first batcher, restarted by the next call after it leaves)
  * serves whatever is published in place and sets the slot's done flag, and the caller copies its
  * result out -- a few microseconds per call, many calls per pass under load.  Queue budget: that
  * kernel holds one hardware queue of the process (GPU_MAX_HW_QUEUES, 4 by default) while it runs,
