@@ -378,7 +378,8 @@ __device__ __forceinline__ void exact_parse(bool live, u64 L, int nvr, Rd8&& rd8
 // bytes and tags ctrl[kCtrlMismatch] on any difference (the gate then decodes the batch again), and
 // a capacity error is tagged in ctrl[kCtrlSpecErr] (it may come from a speculative prefix), merged
 // into p.err by the gate when the speculation held.
-template <int NF, int NV, bool MIX, int MODE, int DIAG, int STG, bool SPEC, int UK = kU, bool FAST = false>
+template <int NF, int NV, bool MIX, int MODE, int DIAG, int STG, bool SPEC, int UK = kU, bool FAST = false, bool LOC = false,
+          bool CANON = false>
 __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 epoch, u64 tile, bool forced, Lds<NV, STG>& S) {
     constexpr int kLoads = (STG / 16 + kThreads - 1) / kThreads;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -408,6 +409,7 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
     // FAST: the copy takes the speculative field positions (the generator's layout, spec_flen) right
     // after the stage, and wave 0 runs Go's exact parse as the check WHILE waves 1-3 copy
     const bool fast = FAST && SPEC && NF == 0 && !held;
+    const bool canon = CANON && SPEC && NF == 0 && !held && !fast;
     if (wave == 0) {
         start = p.rec_off[r0 + min(lane, cnt)];
         endv = p.rec_off[r0 + min(lane + 1, cnt)];
@@ -452,6 +454,47 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
             fpos[0] = nvr == 2 ? 26 : 22;
             if constexpr (NV == 2) fpos[1] = 30 + (u64)k0;
             if (live) p.status[r0 + lane] = 0;  // (no int32 columns: NF == 0)
+        } else if (canon) {
+            // CANON: a record whose header is the generator's image (version bytes, off2p = 13, the
+            // table pointing at back-to-back fields, the last length prefix = the bytes left) parses,
+            // by Go's rules, to exactly its speculative lengths with status 0: six independent LDS
+            // reads and one dependent one instead of Go's parse chain.  Any other record (wave-rare)
+            // takes Go's exact parse, and a length it gives that differs from the speculation tags
+            // the mismatch, as the check below does.
+            u32 k0 = 0;
+            bool ok = false;
+            if (live && L >= (nvr == 2 ? 30u : 22u)) {
+                const u32 b0 = rd8(0), o2 = rd32(1), b13 = rd8(13), t0 = rd32(14), t1 = rd32(18);
+                const bool hdr = b0 == 1 && o2 == 13 && b13 == 1;
+                if (nvr == 2) {
+                    k0 = rd32(22);
+                    ok = hdr && L - 30 >= (u64)k0 && t0 == 9 && t1 == 13 + k0 && rd32(26 + (u64)k0) == (u32)(L - 30 - k0);
+                } else {
+                    ok = hdr && t0 == 5 && t1 == (u32)(L - 22);
+                }
+            }
+            spec_flen<NV>(live ? L : 0, nvr, k0, flen);
+            fpos[0] = nvr == 2 ? 26 : 22;
+            if constexpr (NV == 2) fpos[1] = 30 + (u64)k0;
+            if (__ballot(live && !ok)) {
+                u64 elen[NV], epos[NV];
+                exact_parse<NF, NV>(live, L, nvr, rd8, rd32, st, fx, elen, epos);
+                bool mm = false;
+                if (!ok) {
+#pragma unroll
+                    for (int f = 0; f < NV; ++f) {
+                        mm |= elen[f] != flen[f];
+                        flen[f] = elen[f];
+                        fpos[f] = epos[f];
+                    }
+                } else {
+                    st = 0;
+                }
+                u64* const ctrl = ctrl_words(flags, NV, ntiles);
+                if (__ballot(mm) && lane == 0 && !tagged(load_word(&ctrl[kCtrlMismatch]), epoch))
+                    store_word(&ctrl[kCtrlMismatch], make_word(epoch, kStAgg, 1));
+            }
+            if (live) p.status[r0 + lane] = (uint8_t)st;
         } else {
             exact_parse<NF, NV>(live, L, nvr, rd8, rd32, st, fx, flen, fpos);
             if (live) {
@@ -461,7 +504,7 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
             }
         }
         u64* const ctrl = ctrl_words(flags, NV, ntiles);
-        if (SPEC && !held && !fast) {  // the parsers' speculative lengths of these records, from the same bytes
+        if (SPEC && !held && !fast && !canon) {  // the parsers' speculative lengths of these records, from the same bytes
             const u32 k0 = live && nvr == 2 && L >= 30 ? rd32(22) : 0u;
             u64 sf[NV];
             spec_flen<NV>(live ? L : 0, nvr, k0, sf);
@@ -571,17 +614,51 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
     const i64 pre0 = uniform_i64(S.pre[0]), pre1 = uniform_i64(S.pre[NV - 1]);
     const i64 lim0 = uniform_i64(S.lim[0]), lim1 = uniform_i64(S.lim[NV - 1]);
     const uintptr_t stage_end = base + (uintptr_t)nst;
+    // LOC: a chunk's record by ballots instead of a binary search over S.cs.  Lane k of every wave
+    // holds record k's first chunk (records with no chunks: never); in a wave's 64-chunk window the
+    // records starting inside it mark their start with their index, and a chunk's record is the
+    // nearest mark at or below it, else the last record starting at or before the window.
+    __shared__ uint8_t loc_flg[LOC ? kThreads / 64 : 1][LOC ? UK : 1][64];
+    int mk = 0x7fffffff;
+    if constexpr (LOC) {
+        if (lane < cnt && S.cs[lane + 1] > S.cs[lane]) mk = S.cs[lane];
+#pragma unroll
+        for (int u = 0; u < UK; ++u) loc_flg[wave][u][lane] = 0xff;
+        wave_sync();
+    }
     for (int c0 = 0; c0 < T; c0 += nct * UK) {  // uniform loop
         u32x4 v[UK];
         int P_[UK], code[UK];
         uintptr_t X[UK];
         bool glob[UK];
         bool anyg = false;
+        int kl[UK];
+        if constexpr (LOC) {
+#pragma unroll
+            for (int u = 0; u < UK; ++u) {
+                const int d = mk - (c0 + nct * u + ctid - lane);
+                if (d >= 1 && d <= 63) loc_flg[wave][u][d] = (uint8_t)lane;
+            }
+            wave_sync();
+#pragma unroll
+            for (int u = 0; u < UK; ++u) {
+                const int cw = c0 + nct * u + ctid - lane;
+                const u64 bm = __ballot(mk <= cw);
+                const int bo = bm ? 63 - __clzll((long long)bm) : 0;
+                const int fv = loc_flg[wave][u][lane];
+                const u64 m = __ballot(fv != 0xff);
+                if (fv != 0xff) loc_flg[wave][u][lane] = 0xff;
+                const u64 mm = m & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
+                const int pos = mm ? 63 - __clzll((long long)mm) : 0;
+                const int vo = __shfl(fv, pos, 64);
+                kl[u] = mm ? vo : bo;
+            }
+        }
 #pragma unroll
         for (int u = 0; u < UK; ++u) {
             const int c = c0 + nct * u + ctid;
             const bool has = c < T;
-            const int k = has ? lds_search_64(S.cs, cnt, c) : 0;
+            const int k = !has ? 0 : LOC ? kl[u] : lds_search_64(S.cs, cnt, c);
             int q = c - S.cs[k];
             const int n0 = S.nch0[k];
             const bool second = NV == 2 && q >= n0;
@@ -651,6 +728,9 @@ struct PipeCfg {
     int wpe = 6;        // waves per SIMD the kernel is built for (8 needs <= 64 VGPRs and ~20 KB LDS)
     int uk = kU;        // copy chunks per lane per step
     bool fast = false;  // the copy takes the speculative positions; wave 0 checks them meanwhile
+    bool loc = false;   // copy chunks find their record by ballots instead of a binary search
+    bool canon = false; // speculative kv decodes: the copier checks the generator's header image, Go's
+                        // exact parse only for records that differ from it
 };
 
 template <int NF, int NV, bool MIX, PipeCfg C>
@@ -676,8 +756,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(C.wpe,
     }
     const u64 tile = kRoles ? blockIdx.x - P - 1 : blockIdx.x;
     if (tile >= ntiles) return;
-    copier<NF, NV, MIX, C.mode, C.diag, C.stg, C.spec && C.mode == 0 && C.specx != 1, C.uk, C.fast>(p, flags, epoch, tile,
-                                                                                                    forced, S);
+    copier<NF, NV, MIX, C.mode, C.diag, C.stg, C.spec && C.mode == 0 && C.specx != 1, C.uk, C.fast, C.loc, C.canon>(p, flags, epoch,
+                                                                                                           tile, forced, S);
 }
 
 // ---------------------------------------------------------------- the gate
@@ -789,7 +869,10 @@ size_t decode_pipe_flag_bytes(int nvar, uint64_t n) {
 // stages 720-728, the persistent ring 500-512) were retired in round 4 with their numbers recorded
 // in DESIGN.md; their code is in the history before that commit.
 namespace pipe {
-constexpr PipeCfg kSpecCfg{.sk = 1, .spec = true};   // kv layouts
+// kv layouts: copy chunks located by ballots, the copier's check on the generator's header image
+// (round 5, tools/kbench.py: config 2 159 -> 155 us, config 3 393 -> 385 us; variant 730 is the
+// round-4 form)
+constexpr PipeCfg kSpecCfg{.sk = 1, .spec = true, .loc = true, .canon = true};
 constexpr PipeCfg kExactCfg{.spec = true};          // int32 layouts (exact parsers: spec needs NF == 0)
 // mixed Get/Set batches: 8 waves per SIMD (<= 64 VGPRs) with a 16 KiB stage, 8 copiers per CU
 // (tuning variant 740; r04b: 117.7 -> 102.4 us for the 2^20-record mix, trace mix 551 -> 554 us;
@@ -815,7 +898,7 @@ hipError_t launch_decode_pipe(const DecodeParams& p, void* flags, unsigned epoch
         case 712: return launch_layout<PipeCfg{.spec = true, .specx = 2}>(p, fl, epoch, stream);
         case 713: return launch_layout<PipeCfg{.spec = true, .specx = 3}>(p, fl, epoch, stream);
         // speculative parsers on half the CUs: scanner tiles per thread 1 / 4, parser tiles per wave step 4 / 1
-        case 730: return launch_layout<pipe::kSpecCfg>(p, fl, epoch, stream, 1, 2);
+        case 730: return launch_layout<PipeCfg{.sk = 1, .spec = true}>(p, fl, epoch, stream, 1, 2);
         case 731: return launch_layout<PipeCfg{.sk = 4, .spec = true}>(p, fl, epoch, stream, 1, 2);
         case 732: return launch_layout<PipeCfg{.sk = 2, .pr = 4, .spec = true}>(p, fl, epoch, stream, 1, 2);
         case 733: return launch_layout<PipeCfg{.sk = 2, .pr = 1, .spec = true}>(p, fl, epoch, stream, 1, 2);
@@ -837,6 +920,18 @@ hipError_t launch_decode_pipe(const DecodeParams& p, void* flags, unsigned epoch
         case 751: return launch_layout<PipeCfg{.sk = 1, .spec = true, .uk = 3, .fast = true}>(p, fl, epoch, stream, 1, 2);
         case 752: return launch_layout<PipeCfg{.sk = 1, .stg = 16384, .spec = true, .wpe = 8, .fast = true}>(p, fl, epoch, stream, 1, 2);
         case 753: return launch_layout<PipeCfg{.sk = 1, .stg = 16384, .spec = true, .wpe = 8, .uk = 3, .fast = true}>(p, fl, epoch, stream, 1, 2);
+        // round 5: timestamps of the default kv decode; copy chunks located by ballots (LOC), with
+        // timestamps, with 3 chunks per lane, and on the mixed batch's 8-wave 16 KiB stage
+        case 414: return launch_layout<PipeCfg{.diag = 1, .sk = 1, .spec = true}>(p, fl, epoch, stream, 1, 2);
+        case 760: return launch_layout<PipeCfg{.sk = 1, .spec = true, .loc = true}>(p, fl, epoch, stream, 1, 2);
+        case 761: return launch_layout<PipeCfg{.diag = 1, .sk = 1, .spec = true, .loc = true}>(p, fl, epoch, stream, 1, 2);
+        case 762: return launch_layout<PipeCfg{.sk = 1, .spec = true, .uk = 3, .loc = true}>(p, fl, epoch, stream, 1, 2);
+        case 764: return launch_layout<PipeCfg{.sk = 1, .spec = true, .loc = true, .canon = true}>(p, fl, epoch, stream, 1, 2);
+        case 765: return launch_layout<PipeCfg{.diag = 1, .sk = 1, .spec = true, .loc = true, .canon = true}>(p, fl, epoch, stream, 1, 2);
+        case 766: return launch_layout<PipeCfg{.sk = 1, .stg = 16384, .spec = true, .wpe = 8, .loc = true, .canon = true}>(p, fl, epoch, stream, 1, 2);
+        case 767: return launch_layout<PipeCfg{.sk = 1, .spec = true, .canon = true}>(p, fl, epoch, stream, 1, 2);
+        case 768: return launch_layout<PipeCfg{.sk = 1, .stg = 16384, .spec = true, .wpe = 8, .canon = true}>(p, fl, epoch, stream, 1, 2);
+        case 763: return launch_layout<PipeCfg{.sk = 1, .stg = 16384, .spec = true, .wpe = 8, .loc = true}>(p, fl, epoch, stream, 1, 2);
         default: break;
     }
 #endif

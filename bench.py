@@ -290,11 +290,12 @@ def decode_kernel_name(s, mixed: bool = False) -> str:
     kv layouts (no int32 fields) run the speculative parsers with 256-tile scanner steps
     (decode_pipe.hip kSpecCfg), followed by the small gate launch; int32 layouts the exact parsers
     (kExactCfg); the mixed batch 8 waves per SIMD with a 16 KiB stage (kMixCfg).
-    PipeCfg{mode, diag, sk, pr, stg, spec, specx, wpe, uk}."""
+    PipeCfg{mode, diag, sk, pr, stg, spec, specx, wpe, uk, fast, loc, canon} (trailing defaults are
+    not printed); kSpecCfg's copiers locate chunks by ballots and check the generator's header image."""
     if mixed:
         cfg = "0, 0, 1, 2, 16384, true, 0, 8, 2"
     else:
-        cfg = "0, 0, 1, 2, 22528, true, 0, 6, 2" if s.nfixed == 0 else "0, 0, 2, 2, 22528, false, 0, 6, 2"
+        cfg = "0, 0, 1, 2, 22528, true, 0, 6, 2, false, true, true" if s.nfixed == 0 else "0, 0, 2, 2, 22528, false, 0, 6, 2"
     return f"decode_pipe_kernel<{s.nfixed}, {s.nvar}, {'true' if mixed else 'false'}, symhip::pipe::PipeCfg{{{cfg}}}>"
 
 
@@ -838,7 +839,9 @@ def e2e_leg(rpcs: int = 1 << 18, window: int = 4096, inflight: int = 2) -> dict:
     out["note"] = ("C stand-in for the aRPC client/server pair (tests/e2e_loopback.c; no Go toolchain): Set RPCs "
                    "over UDP loopback, request and response each encoded, packetized, reassembled and decoded "
                    "on the GPU through the C ABI; gbps_algorithmic counts the four codec calls' bytes "
-                   "(SURVEY 8d definition) per RPC; host clock around the whole exchange")
+                   "(SURVEY 8d definition) per RPC; host clock around the whole exchange; every response's "
+                   "status and length checked (verified: false = the value bytes are not compared here, "
+                   "tests/test_e2e_loopback.py compares them)")
     return out
 
 
