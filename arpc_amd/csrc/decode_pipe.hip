@@ -410,9 +410,11 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
     // after the stage, and wave 0 runs Go's exact parse as the check WHILE waves 1-3 copy
     const bool fast = FAST && SPEC && NF == 0 && !held;
     const bool canon = CANON && SPEC && NF == 0 && !held && !fast;
+    u32 ty = 1;  // mixed batches: the record's type, loaded with its offsets (not after the stage)
     if (wave == 0) {
         start = p.rec_off[r0 + min(lane, cnt)];
         endv = p.rec_off[r0 + min(lane + 1, cnt)];
+        if constexpr (MIX) ty = p.type[lane < cnt ? r0 + lane : 0];
     }
     {
         u32x4 sv[kLoads];
@@ -443,7 +445,7 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
         const u64 a = (u64)(A - base) + q;
         return a + 4 <= (u64)nst ? *(const u32*)&S.stage[a] : *(gc_u32*)(A + q);  // unaligned OK
     };
-    const int nvr = rec_nvar<NV, MIX>(p, live ? r0 + lane : 0);
+    const int nvr = MIX ? (ty != 0 ? NV : 1) : NV;  // rec_nvar
     u64 flen[NV], fpos[NV];  // (wave 0; fast: the speculative ones, kept for the check)
     if (wave == 0) {
         u32 st = 0;

@@ -264,9 +264,10 @@ __device__ __forceinline__ void enc_phase1(const EncodeParams& p, EncWaveLds<NV,
     // loads, issued with the per-record ones.
     bool part_safe = true;
     i64 o = 0, size = 0;
-    u64 L[NV];
+    u64 L[NV], lo[NV];  // the record's field lengths and first payload offsets (kept: a re-read after
+                        // the out_off stores or the prefix-word polls is another trip to memory)
 #pragma unroll
-    for (int f = 0; f < NV; ++f) L[f] = 0;
+    for (int f = 0; f < NV; ++f) L[f] = lo[f] = 0;
     bool isset = true;  // mixed batches: SetRequest (else GetRequest)
     if (hdr_wave) {
 #pragma unroll
@@ -289,8 +290,13 @@ __device__ __forceinline__ void enc_phase1(const EncodeParams& p, EncWaveLds<NV,
             if (lane < hcnt) {
                 const u64 r = rb + lane;
                 isset = TYP(r) != 0;
-                L[0] = OFF(0, r + 1) - OFF(0, r);
-                if (isset) L[1] = OFF(1, r + 1) - OFF(1, r);
+                lo[0] = OFF(0, r);
+                L[0] = OFF(0, r + 1) - lo[0];
+                // the value offsets are loaded whatever the type (a select, not a branch): behind a
+                // test of the type byte they would wait for its load, a second round trip per tile
+                lo[1] = OFF(1, r);
+                const u64 l1 = OFF(1, r + 1) - lo[1];
+                L[1] = isset ? l1 : 0;
                 size = (i64)(22 + L[0] + (isset ? 8 + L[1] : 0));
             }
             const u64 part = rb / kWaveRecs;  // the size scan's 64-record tiles
@@ -316,9 +322,9 @@ __device__ __forceinline__ void enc_phase1(const EncodeParams& p, EncWaveLds<NV,
             size = OVH;
 #pragma unroll
             for (int f = 0; f < NV; ++f) {
-                const u64 lo = OFF(f, r);
-                L[f] = OFF(f, r + 1) - lo;
-                o += (i64)(lo - p.offs[f][0]);
+                lo[f] = OFF(f, r);
+                L[f] = OFF(f, r + 1) - lo[f];
+                o += (i64)(lo[f] - p.offs[f][0]);
                 size += (i64)L[f];
                 S.len[f][rec] = (u32)L[f];
             }
@@ -378,7 +384,7 @@ __device__ __forceinline__ void enc_phase1(const EncodeParams& p, EncWaveLds<NV,
             int ps = h0;
 #pragma unroll
             for (int f = 0; f < NV; ++f) {
-                S.delta[f][rec] = (u64)(uintptr_t)(p.bytes[f] + OFF(f, r)) - (u64)(i64)(orel + ps);
+                S.delta[f][rec] = (u64)(uintptr_t)(p.bytes[f] + lo[f]) - (u64)(i64)(orel + ps);
                 ps += (int)L[f] + 4;
             }
             // header image: [0]=1 | [1:5]=13 | [5:9]=sid | [9:13]=mid | [13]=1 | table | len(field 0)
