@@ -542,11 +542,12 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
                 store_word(&aw[(size_t)lane * ntiles + tile], make_word(epoch, kStAgg, lane == 0 ? agg[0] : agg[NV - 1]));
                 u64* a = &pw[(size_t)lane * ntiles + tile];
                 wv = load_word(a);
-                if (!forced) {
-                    for (const u64 t0 = now_ticks(); !tagged(wv, epoch) && now_ticks() - t0 <= kFallbackTicks;) {
+                if (!forced && !tagged(wv, epoch)) {  // (the clock only when the word is not there yet)
+                    const u64 t0 = now_ticks();
+                    do {
                         __builtin_amdgcn_s_sleep(2);
                         wv = load_word(a);
-                    }
+                    } while (!tagged(wv, epoch) && now_ticks() - t0 <= kFallbackTicks);
                 }
                 got = tagged(wv, epoch);
             }
@@ -753,7 +754,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(C.wpe,
         return;
     }
     if (kRoles && blockIdx.x == P) {
-        if (!forced) scanner<NV, C.sk>(aw, pw, ntiles, epoch, S);
+        if (!forced) scanner<NV, C.sk>(aw, pw, ntiles, epoch, S, C.diag ? p.dbg + 1 : nullptr);  // diag: publish times in slot 6
         return;
     }
     const u64 tile = kRoles ? blockIdx.x - P - 1 : blockIdx.x;
@@ -932,6 +933,15 @@ hipError_t launch_decode_pipe(const DecodeParams& p, void* flags, unsigned epoch
         case 765: return launch_layout<PipeCfg{.diag = 1, .sk = 1, .spec = true, .loc = true, .canon = true}>(p, fl, epoch, stream, 1, 2);
         case 766: return launch_layout<PipeCfg{.sk = 1, .stg = 16384, .spec = true, .wpe = 8, .loc = true, .canon = true}>(p, fl, epoch, stream, 1, 2);
         case 767: return launch_layout<PipeCfg{.sk = 1, .spec = true, .canon = true}>(p, fl, epoch, stream, 1, 2);
+        // round 5: parser and scanner geometry around the default (startup: the first prefixes)
+        case 770: return launch_layout<PipeCfg{.sk = 1, .pr = 4, .spec = true, .loc = true, .canon = true}>(p, fl, epoch, stream, 1, 2);
+        case 771: return launch_layout<PipeCfg{.sk = 2, .spec = true, .loc = true, .canon = true}>(p, fl, epoch, stream, 1, 2);
+        case 772: return launch_layout<PipeCfg{.sk = 2, .pr = 4, .spec = true, .loc = true, .canon = true}>(p, fl, epoch, stream, 1, 2);
+        case 773: return launch_layout<PipeCfg{.diag = 1, .sk = 1, .pr = 4, .spec = true, .loc = true, .canon = true}>(p, fl, epoch, stream, 1, 2);
+        case 774: return launch_layout<PipeCfg{.sk = 1, .pr = 4, .spec = true, .loc = true, .canon = true}>(p, fl, epoch, stream, 3, 8);
+        case 775: return launch_layout<PipeCfg{.sk = 1, .spec = true, .loc = true, .canon = true}>(p, fl, epoch, stream, 3, 8);
+        // (round 5, measured slower and removed: the prefix word loaded when the tile starts, 156 ->
+        // 160 us; loaded right after the stage, ahead of the parse's stores, 158 -> 162 us)
         case 768: return launch_layout<PipeCfg{.sk = 1, .stg = 16384, .spec = true, .wpe = 8, .canon = true}>(p, fl, epoch, stream, 1, 2);
         case 763: return launch_layout<PipeCfg{.sk = 1, .stg = 16384, .spec = true, .wpe = 8, .loc = true}>(p, fl, epoch, stream, 1, 2);
         default: break;

@@ -64,6 +64,12 @@ def main():
     ready = np.maximum(t[1:, 2], t[:-1, 3])
     print("look-back lag after predecessor's inclusive", q(t[1:, 3] - ready))
     print("predecessor inclusive minus my aggregate   ", q(t[:-1, 3] - t[1:, 2]))
+    pub = raw[:, 6]
+    if (pub > 0).all():  # round-5 diag variants: the scanner's publish time of each tile's prefix (slot 6)
+        tp = (pub - t0) * 10 / 1000.0
+        print("prefix published - tile start      ", q(tp - t[:, 0]))
+        print("prefix published - copier's parse  ", q(tp - t[:, 2]))
+        print("prefix known - prefix published    ", q(t[:, 3] - tp))
     first = t[:min(1400, ntiles)]
     print("first 1400 tiles: aggregate ready", q(first[:, 2]), "\n                  prefix known   ", q(first[:, 3]),
           "\n                  staged         ", q(first[:, 1]))
