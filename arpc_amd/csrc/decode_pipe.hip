@@ -479,6 +479,7 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
             fpos[0] = nvr == 2 ? 26 : 22;
             if constexpr (NV == 2) fpos[1] = 30 + (u64)k0;
             if (__ballot(live && !ok)) {
+                if (DIAG && lane == 0) atomicAdd((unsigned long long*)&p.dbg[ntiles * 8], 1ull);  // waves off the image
                 u64 elen[NV], epos[NV];
                 exact_parse<NF, NV>(live, L, nvr, rd8, rd32, st, fx, elen, epos);
                 bool mm = false;
@@ -942,6 +943,9 @@ hipError_t launch_decode_pipe(const DecodeParams& p, void* flags, unsigned epoch
         case 775: return launch_layout<PipeCfg{.sk = 1, .spec = true, .loc = true, .canon = true}>(p, fl, epoch, stream, 3, 8);
         // (round 5, measured slower and removed: the prefix word loaded when the tile starts, 156 ->
         // 160 us; loaded right after the stage, ahead of the parse's stores, 158 -> 162 us)
+        // (round 5, measured no faster and removed: the record heads' first 32 bytes loaded into
+        // registers beside the stage for the header-image check, 156 -> 158 us)
+        case 787: return launch_layout<PipeCfg{.diag = 1, .sk = 1, .stg = 16384, .spec = true, .wpe = 8, .canon = true}>(p, fl, epoch, stream, 1, 2);
         case 768: return launch_layout<PipeCfg{.sk = 1, .stg = 16384, .spec = true, .wpe = 8, .canon = true}>(p, fl, epoch, stream, 1, 2);
         case 763: return launch_layout<PipeCfg{.sk = 1, .stg = 16384, .spec = true, .wpe = 8, .loc = true}>(p, fl, epoch, stream, 1, 2);
         default: break;
