@@ -11,12 +11,13 @@ the Get/Set batch (tools/mixed_ab.py).
 import json
 import sys
 
-RECORDS = {"config2": 1 << 20, "config3": 1 << 20, "config4": 1 << 23, "mixed": 1 << 20, "trace": 1 << 20}
+RECORDS = {"config2": 1 << 20, "config3": 1 << 20, "config4": 1 << 23, "mixed": 1 << 20, "trace": 1 << 20, "crypto": 1 << 20}
 
 
 def main():
     out = {"note": "per workload: kernel -> avg_ns (kernel trace) and HBM bytes per launch = FETCH_SIZE x 2 "
-                   "(gfx950 wide-read correction) + WRITE_SIZE, both KiB-scaled (tools/summarize_profile.py)",
+                   "+ WRITE_SIZE, both KiB-scaled (tools/summarize_profile.py); x 2 is exact on gfx950 for every "
+                   "read width (profiles/r05_traffic_calibration.txt)",
            "workloads": {}}
     for arg in sys.argv[2:]:
         name, path = arg.split("=", 1)
