@@ -172,6 +172,7 @@ struct GatherArgs {
     uint64_t* nkept;       // FW
     unsigned* err;
     uint64_t seg_bytes_hint;  // VAR: the caller's estimate of the mean segment length (0: none)
+    int nt;                   // nontemporal stores for wave spans of at most kNtSpan bytes (st16; 4-chunk kernel)
 };
 }  // namespace raw
 hipError_t launch_tile_scan(const raw::Pair* agg, raw::Pair* pre, uint64_t ntiles, hipStream_t stream);

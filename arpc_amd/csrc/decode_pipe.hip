@@ -618,6 +618,7 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
     const i64 pre0 = uniform_i64(S.pre[0]), pre1 = uniform_i64(S.pre[NV - 1]);
     const i64 lim0 = uniform_i64(S.lim[0]), lim1 = uniform_i64(S.lim[NV - 1]);
     const uintptr_t stage_end = base + (uintptr_t)nst;
+    const bool nt = __builtin_amdgcn_readfirstlane((int)(s1 - s0 <= (u64)kNtSpan)) != 0;  // (st16)
     // LOC: a chunk's record by ballots instead of a binary search over S.cs.  Lane k of every wave
     // holds record k's first chunk (records with no chunks: never); in a wave's 64-chunk window the
     // records starting inside it mark their start with their index, and a chunk's record is the
@@ -703,11 +704,11 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
             const i64 hi = min((i64)(P_[u] + nb), second ? lim1 : lim0);
             uint8_t* colb = second ? p.bytes[NV - 1] + pre1 : p.bytes[0] + pre0;
             const bool full = P_[u] >= 0 && (i64)P_[u] + 16 <= hi;
-            if (full) *(g_u4*)(colb + P_[u]) = v[u];
+            if (full) st16(colb + P_[u], v[u], nt);
             const bool part = P_[u] >= 0 && !full && (i64)P_[u] < hi;
             if (__ballot(part)) {
                 const u32 rr[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-                if (part) store_chunk(colb, P_[u], 0, hi, rr);
+                if (part) store_chunk(colb, P_[u], 0, hi, rr, nt);
             }
         }
     }

@@ -159,12 +159,33 @@ __device__ __forceinline__ uint8_t chunk_byte(const u32 r[4], int t) {
     return (uint8_t)(w >> ((t & 3) * 8));
 }
 
+// A 16-byte output store of the streaming kernels, nontemporal where it pays: nothing in the launch
+// re-reads the written lines.  One-box A/B of libraries (round 5): with 22 KB or smaller tiles (config 2,
+// the Get/Set mix) nontemporal stores took config 2's encode 145 -> 141 us, its decode 152.5 -> 145.5 us
+// and the mix's pair 3.6 -> 3.8 TB/s; with tiles of tens to hundreds of KB (config 3, the trace replays)
+// they cost 1-8 % (config3_trace decode 1.40 -> 1.51 ms), so the kernels pass nt = their tile's span
+// <= kNtSpan.  `sc1` stores (the line leaves the XCD's L2) gained nothing.  Span-gated library against
+// plain stores, two runs each on one box: headline 4995 -> 5100 GB/s (decode 151 -> 146 us), N3
+// reassembly 2670 -> 2840 GB/s, config 3 / the trace replays / the N5 legs within +-2 %.
+constexpr i64 kNtSpan = 32768;
+__device__ __forceinline__ void st16(uint8_t* p, u32x4 v, bool nt = true) {
+    if (nt) {
+        // the empty asm statements keep the compiler from hoisting or sinking the two stores into
+        // one (merged, the store loses its nontemporal flag)
+        asm volatile("");
+        __builtin_nontemporal_store(v, (g_u4*)p);
+        asm volatile("");
+    } else {
+        *(g_u4*)p = v;
+    }
+}
+
 // Store a 16-byte chunk at dst (absolute, 16-byte aligned) keeping only the bytes
 // whose position P+t lies in [lo, hi).  Full chunks use one global_store_dwordx4;
 // the partial chunks at a workgroup's range edges fall back to byte stores.
-__device__ __forceinline__ void store_chunk(uint8_t* base, i64 P, i64 lo, i64 hi, const u32 r[4]) {
+__device__ __forceinline__ void store_chunk(uint8_t* base, i64 P, i64 lo, i64 hi, const u32 r[4], bool nt = true) {
     if (P >= lo && P + 16 <= hi) {
-        *(g_u4*)(base + P) = u32x4{r[0], r[1], r[2], r[3]};
+        st16(base + P, u32x4{r[0], r[1], r[2], r[3]}, nt);
     } else {
         for (int t = 0; t < 16; ++t) {
             const i64 q = P + t;

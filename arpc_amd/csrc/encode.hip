@@ -435,6 +435,7 @@ __device__ __forceinline__ void enc_phase2(const EncodeParams& p, EncWaveLds<NV,
     // ---------------- phase 2: natural-order output chunks ----------------
     const i64 T0 = uniform_i64(S.t0);
     const int span = __builtin_amdgcn_readfirstlane(S.span);
+    const bool nt = span <= kNtSpan;  // (st16)
     const i64 mis = (i64)((uintptr_t)p.out & 15);
     const int first = (int)(((T0 + mis) & ~(i64)15) - mis - T0);  // in (-16, 0]
     uint8_t* const out_t = p.out + T0;
@@ -525,7 +526,7 @@ __device__ __forceinline__ void enc_phase2(const EncodeParams& p, EncWaveLds<NV,
             if (nb > -16) r |= lds16u(S.hdr, (j + 2) * SLOT + nb);
         }
         const u32 rr[4] = {r.x, r.y, r.z, r.w};
-        store_chunk(out_t, P, 0, span, rr);
+        store_chunk(out_t, P, 0, span, rr, nt);
     };
     auto chunk = [&](int P, int j, bool careful) {
         u32x4 w[NV];
@@ -646,7 +647,7 @@ __device__ __forceinline__ void enc_phase2(const EncodeParams& p, EncWaveLds<NV,
                 if (nb > -16) r |= lds16u(S.hdr, (j + 2) * SLOT + nb);
             }
             const u32 rr[4] = {r.x, r.y, r.z, r.w};
-            store_chunk(out_t, P, 0, span, rr);
+            store_chunk(out_t, P, 0, span, rr, nt);
         }
     }
 }

@@ -1,6 +1,8 @@
 // gather_tile.hpp -- one 256-segment tile of the output-stationary segment gather (raw_fields.hip's
 // gather_kernel; flat.hip's fused decode emit kernel takes the same tiles of several fields).
 #pragma once
+#include <type_traits>
+
 #include "codec.hpp"
 #include "device_util.hpp"
 
@@ -23,7 +25,7 @@ __device__ __forceinline__ u64 readlane_u64(u64 v, int l) {
 // One 256-segment tile (a workgroup loop body of gather_kernel, or of flat.hip's dec_emit_kernel).
 // pre[ntiles] is the total: a scan over the capacity's tiles has it there too, at the exclusive
 // prefix of the first empty tile.
-template <bool FW, int KU = 4>
+template <bool FW, int KU = 4, bool NT = false>
 __device__ __forceinline__ void gather_tile(const GatherArgs& a, u64 tile, u64 n, u64 ntiles, WaveLds* lds_all,
                                             const MaskTable& masks, u64* wsum_b, u64* wsum_c) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -93,6 +95,7 @@ __device__ __forceinline__ void gather_tile(const GatherArgs& a, u64 tile, u64 n
     const int slot = __builtin_amdgcn_mbcnt_hi((u32)(lm >> 32), __builtin_amdgcn_mbcnt_lo((u32)lm, 0u));
     const int nl = __popcll(lm);
     const int span = (int)(D1 - D0);
+    const bool nt = NT && span <= kNtSpan;  // (st16)
     if (live) {
         S.addr[slot] = (u64)(uintptr_t)(a.in + src);
         S.o[slot] = (int)(d - D0);
@@ -102,52 +105,63 @@ __device__ __forceinline__ void gather_tile(const GatherArgs& a, u64 tile, u64 n
     const bool safe = __all(!live || (src >= in_lo + 16 && src + len + 16 <= in_hi));
     wave_sync();
     if (nl == 0) return;
-    const i64 mis = (i64)((uintptr_t)a.out & 15);
-    const int firstc = (int)((((i64)D0 + mis) & ~(i64)15) - mis - (i64)D0);  // in (-16, 0]
-    uint8_t* const out_t = a.out + D0;
-    if (safe) {
-        // kU chunks per lane per step: every load of the step is issued before its stores
-        constexpr int kU = KU;
-        for (int B = firstc; B < span; B += 16 * 64 * kU) {  // wave-uniform loop
-            u32x4 r[kU];
+    // the copy, instantiated per store kind (NT kernels only: with the nontemporal copy present in
+    // the kernel the general reassembly path's gather ran 406 -> 440 us with plain stores selected)
+    auto copy = [&](auto ntc) {
+        constexpr bool NTS = decltype(ntc)::value;
+        const i64 mis = (i64)((uintptr_t)a.out & 15);
+        const int firstc = (int)((((i64)D0 + mis) & ~(i64)15) - mis - (i64)D0);  // in (-16, 0]
+        uint8_t* const out_t = a.out + D0;
+        if (safe) {
+            // kU chunks per lane per step: every load of the step is issued before its stores
+            constexpr int kU = KU;
+            for (int B = firstc; B < span; B += 16 * 64 * kU) {  // wave-uniform loop
+                u32x4 r[kU];
 #pragma unroll
-            for (int u = 0; u < kU; ++u) {
-                const int P = B + 16 * 64 * u + 16 * lane;
-                r[u] = u32x4{0, 0, 0, 0};
-                if (P >= span) continue;
-                const int k0 = lds_search_64(S.o, nl, max(P, 0));
-                const int o0 = S.o[k0], o1 = S.o[k0 + 1];
-                const bool two = k0 + 1 < nl && o1 < P + 16;  // the next segment starts in this chunk
-                const int o2 = two ? S.o[k0 + 2] : o1;
-                const uintptr_t X0 = (uintptr_t)(S.addr[k0] + (u64)(i64)(P - o0));
-                r[u] = ld16u(X0) & range_mask(masks, o0 - P, o1 - P);
-                if (two)  // (a chunk inside one segment, the usual case, issues one load)
-                    r[u] |= ld16u((uintptr_t)(S.addr[k0 + 1] + (u64)(i64)(P - o1))) & range_mask(masks, o1 - P, o2 - P);
-                for (int k = k0 + 2; two && k < nl && S.o[k] < P + 16; ++k)  // segments < 16 bytes
-                    r[u] |= ld16u((uintptr_t)(S.addr[k] + (u64)(i64)(P - S.o[k]))) &
-                            range_mask(masks, S.o[k] - P, S.o[k + 1] - P);
-            }
+                for (int u = 0; u < kU; ++u) {
+                    const int P = B + 16 * 64 * u + 16 * lane;
+                    r[u] = u32x4{0, 0, 0, 0};
+                    if (P >= span) continue;
+                    const int k0 = lds_search_64(S.o, nl, max(P, 0));
+                    const int o0 = S.o[k0], o1 = S.o[k0 + 1];
+                    const bool two = k0 + 1 < nl && o1 < P + 16;  // the next segment starts in this chunk
+                    const int o2 = two ? S.o[k0 + 2] : o1;
+                    const uintptr_t X0 = (uintptr_t)(S.addr[k0] + (u64)(i64)(P - o0));
+                    r[u] = ld16u(X0) & range_mask(masks, o0 - P, o1 - P);
+                    if (two)  // (a chunk inside one segment, the usual case, issues one load)
+                        r[u] |= ld16u((uintptr_t)(S.addr[k0 + 1] + (u64)(i64)(P - o1))) & range_mask(masks, o1 - P, o2 - P);
+                    for (int k = k0 + 2; two && k < nl && S.o[k] < P + 16; ++k)  // segments < 16 bytes
+                        r[u] |= ld16u((uintptr_t)(S.addr[k] + (u64)(i64)(P - S.o[k]))) &
+                                range_mask(masks, S.o[k] - P, S.o[k + 1] - P);
+                }
 #pragma unroll
-            for (int u = 0; u < kU; ++u) {
-                const int P = B + 16 * 64 * u + 16 * lane;
-                if (P >= span) continue;
-                const u32 rr[4] = {r[u].x, r[u].y, r[u].z, r[u].w};
-                store_chunk(out_t, P, 0, span, rr);
+                for (int u = 0; u < kU; ++u) {
+                    const int P = B + 16 * 64 * u + 16 * lane;
+                    if (P >= span) continue;
+                    const u32 rr[4] = {r[u].x, r[u].y, r[u].z, r[u].w};
+                    store_chunk(out_t, P, 0, span, rr, NTS);
+                }
             }
+            return;
         }
-        return;
-    }
-    for (int B = firstc; B < span; B += 16 * 64) {  // batch-edge waves: aligned blocks only
-        const int P = B + 16 * lane;
-        if (P >= span) continue;
-        u32 t[4] = {0, 0, 0, 0};
-        for (int k = lds_search_64(S.o, nl, max(P, 0)); k < nl; ++k) {
-            const int lo = S.o[k] - P;
-            if (lo >= 16) break;
-            const int hi = min(S.o[k + 1] - P, 16);
-            or_window_global((uintptr_t)(S.addr[k] + (u64)(i64)(P - S.o[k])), max(lo, 0), hi, t);
+        for (int B = firstc; B < span; B += 16 * 64) {  // batch-edge waves: aligned blocks only
+            const int P = B + 16 * lane;
+            if (P >= span) continue;
+            u32 t[4] = {0, 0, 0, 0};
+            for (int k = lds_search_64(S.o, nl, max(P, 0)); k < nl; ++k) {
+                const int lo = S.o[k] - P;
+                if (lo >= 16) break;
+                const int hi = min(S.o[k + 1] - P, 16);
+                or_window_global((uintptr_t)(S.addr[k] + (u64)(i64)(P - S.o[k])), max(lo, 0), hi, t);
+            }
+            store_chunk(out_t, P, 0, span, t, NTS);
         }
-        store_chunk(out_t, P, 0, span, t);
+    };
+    if constexpr (NT) {
+        if (nt) copy(std::true_type{});
+        else copy(std::false_type{});
+    } else {
+        copy(std::false_type{});
     }
 }
 

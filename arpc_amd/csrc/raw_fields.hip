@@ -192,7 +192,7 @@ __global__ __launch_bounds__(1024) void tile_scan_kernel(const Pair* agg, Pair* 
 
 // Grid-stride over the tiles of the segment count (*n_ptr when given, else n): a launch sized for a
 // capacity far above the real count (nested item lists) does not dispatch a workgroup per empty tile.
-template <bool FW, int KU = 4>
+template <bool FW, int KU = 4, bool NT = false>
 __global__ __launch_bounds__(kWaves * 64) void gather_kernel(GatherArgs a) {
     __shared__ WaveLds lds_all[kWaves];
     __shared__ MaskTable masks;
@@ -202,7 +202,7 @@ __global__ __launch_bounds__(kWaves * 64) void gather_kernel(GatherArgs a) {
     if (n == 0) return;  // nothing to place (and the scan of an empty count may not have run)
     mask_table_init(masks, threadIdx.x);
     for (u64 t = blockIdx.x; t < ntiles; t += gridDim.x) {  // workgroup-uniform loop
-        gather_tile<FW, KU>(a, t, n, ntiles, lds_all, masks, wsum_b, wsum_c);
+        gather_tile<FW, KU, NT>(a, t, n, ntiles, lds_all, masks, wsum_b, wsum_c);
         __syncthreads();  // wsum_* and the wave slots are rewritten by the next tile
     }
 }
@@ -258,6 +258,7 @@ hipError_t launch_segment_gather(const raw::GatherArgs& a, hipStream_t stream) {
 #ifdef SYMHIP_TUNING
     else if (ku == 8) hipLaunchKernelGGL((raw::gather_kernel<false, 8>), grid, dim3(256), 0, stream, a);
 #endif
+    else if (a.nt) hipLaunchKernelGGL((raw::gather_kernel<false, 4, true>), grid, dim3(256), 0, stream, a);
     else hipLaunchKernelGGL(raw::gather_kernel<false>, grid, dim3(256), 0, stream, a);
     return hipGetLastError();
 }

@@ -748,6 +748,7 @@ hipError_t launch_reassemble(const uint8_t* wire, const u64* dg_off, u64 n, uint
         ga.cap = msg_cap;
         ga.err = err;
         ga.seg_bytes_hint = msg_cap / n;  // (the capacity is usually the wire size)
+        ga.nt = gate == nullptr;  // the simple path's gather (one A/B: +6 %; the general path's -5 %)
         return launch_segment_gather(ga, st);
     };
     // Simple batches (every DataPacket one whole message) complete here: parse (with the tile
