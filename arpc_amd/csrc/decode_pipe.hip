@@ -946,6 +946,9 @@ hipError_t launch_decode_pipe(const DecodeParams& p, void* flags, unsigned epoch
         // 160 us; loaded right after the stage, ahead of the parse's stores, 158 -> 162 us)
         // (round 5, measured no faster and removed: the record heads' first 32 bytes loaded into
         // registers beside the stage for the header-image check, 156 -> 158 us)
+        // round 5: the default with the gate on one workgroup per CU (152.1 vs 152.6 us: the gate's
+        // ~4.7 us is its launch behind the pipeline, not its 1024 workgroups)
+        case 788: return launch_layout<PipeCfg{.sk = 1, .spec = true, .specx = 3, .loc = true, .canon = true}>(p, fl, epoch, stream, 1, 2);
         case 787: return launch_layout<PipeCfg{.diag = 1, .sk = 1, .stg = 16384, .spec = true, .wpe = 8, .canon = true}>(p, fl, epoch, stream, 1, 2);
         case 768: return launch_layout<PipeCfg{.sk = 1, .stg = 16384, .spec = true, .wpe = 8, .canon = true}>(p, fl, epoch, stream, 1, 2);
         case 763: return launch_layout<PipeCfg{.sk = 1, .stg = 16384, .spec = true, .wpe = 8, .loc = true}>(p, fl, epoch, stream, 1, 2);
