@@ -1016,11 +1016,15 @@ hipError_t launch_encode_mixed(EncodeParams p, void* ws, hipStream_t stream) {
     const u64 nt = mixed_ntiles(p.n);
     const int ncu = device_cus();
     if (ncu <= 0) return hipErrorInvalidDevice;
-    u64 P = (u64)ncu / 2;  // sizers: one per 2 CUs (kPipeGroup tiles per workgroup step)
+    // sizers: two per CU (kPipeGroup tiles per workgroup step).  Round 5, tools/mixed_ab.py, 30
+    // rounds: one per 2 CUs (round 4, variant 32) 102.7 us, one per CU (31) 101.2, two per CU 100.6;
+    // the trace replay 563.0 / 561.4 / 560.4 us
+    u64 P = (u64)ncu * 2;
     p.pipe_lookback = impl == SYM_ENCODE_LOOKBACK;
 #ifdef SYMHIP_TUNING
     if (p.variant == 30) P = (u64)ncu / 4;
     if (p.variant == 31) P = (u64)ncu;
+    if (p.variant == 32) P = (u64)ncu / 2;
 #endif
     if (P > mixed_npgroups(p.n)) P = mixed_npgroups(p.n);
     p.pipe_sizers = (unsigned)P;
