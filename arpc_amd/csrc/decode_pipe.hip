@@ -949,6 +949,11 @@ hipError_t launch_decode_pipe(const DecodeParams& p, void* flags, unsigned epoch
         // round 5: the default with the gate on one workgroup per CU (152.1 vs 152.6 us: the gate's
         // ~4.7 us is its launch behind the pipeline, not its 1024 workgroups)
         case 788: return launch_layout<PipeCfg{.sk = 1, .spec = true, .specx = 3, .loc = true, .canon = true}>(p, fl, epoch, stream, 1, 2);
+        // round 5: parser workgroups at one and two per CU (the mixed batch's config; config 2's):
+        // mixed 100.6 -> 105.7 / 113.2 us, config 2 153.4 -> 156.3 us (kbench medians): half a CU's worth kept
+        case 789: return launch_layout<PipeCfg{.sk = 1, .stg = 16384, .spec = true, .wpe = 8}>(p, fl, epoch, stream, 1, 1);
+        case 790: return launch_layout<PipeCfg{.sk = 1, .stg = 16384, .spec = true, .wpe = 8}>(p, fl, epoch, stream, 2, 1);
+        case 791: return launch_layout<PipeCfg{.sk = 1, .spec = true, .loc = true, .canon = true}>(p, fl, epoch, stream, 1, 1);
         case 787: return launch_layout<PipeCfg{.diag = 1, .sk = 1, .stg = 16384, .spec = true, .wpe = 8, .canon = true}>(p, fl, epoch, stream, 1, 2);
         case 768: return launch_layout<PipeCfg{.sk = 1, .stg = 16384, .spec = true, .wpe = 8, .canon = true}>(p, fl, epoch, stream, 1, 2);
         case 763: return launch_layout<PipeCfg{.sk = 1, .stg = 16384, .spec = true, .wpe = 8, .loc = true}>(p, fl, epoch, stream, 1, 2);
