@@ -1018,13 +1018,14 @@ hipError_t launch_encode_mixed(EncodeParams p, void* ws, hipStream_t stream) {
     if (ncu <= 0) return hipErrorInvalidDevice;
     // sizers: two per CU (kPipeGroup tiles per workgroup step).  Round 5, tools/mixed_ab.py, 30
     // rounds: one per 2 CUs (round 4, variant 32) 102.7 us, one per CU (31) 101.2, two per CU 100.6;
-    // the trace replay 563.0 / 561.4 / 560.4 us
+    // the trace replay 563.0 / 561.4 / 560.4 us; four per CU (33) 99.9 vs 100.5 us, within noise
     u64 P = (u64)ncu * 2;
     p.pipe_lookback = impl == SYM_ENCODE_LOOKBACK;
 #ifdef SYMHIP_TUNING
     if (p.variant == 30) P = (u64)ncu / 4;
     if (p.variant == 31) P = (u64)ncu;
     if (p.variant == 32) P = (u64)ncu / 2;
+    if (p.variant == 33) P = (u64)ncu * 4;
 #endif
     if (P > mixed_npgroups(p.n)) P = mixed_npgroups(p.n);
     p.pipe_sizers = (unsigned)P;
