@@ -166,7 +166,9 @@ __device__ __forceinline__ uint8_t chunk_byte(const u32 r[4], int t) {
 // they cost 1-8 % (config3_trace decode 1.40 -> 1.51 ms), so the kernels pass nt = their tile's span
 // <= kNtSpan.  `sc1` stores (the line leaves the XCD's L2) gained nothing.  Span-gated library against
 // plain stores, two runs each on one box: headline 4995 -> 5100 GB/s (decode 151 -> 146 us), N3
-// reassembly 2670 -> 2840 GB/s, config 3 / the trace replays / the N5 legs within +-2 %.
+// reassembly 2670 -> 2840 GB/s, config 3 / the trace replays / the N5 legs within +-2 %.  The threshold,
+// two runs each: 16 KB loses config 2's 22 KB tiles (headline 5100 -> 4945 GB/s), 64 KB takes config 3's
+// ~53 KB tiles (4590 -> 4525 GB/s).
 constexpr i64 kNtSpan = 32768;
 __device__ __forceinline__ void st16(uint8_t* p, u32x4 v, bool nt = true) {
     if (nt) {
