@@ -281,8 +281,8 @@ static hipError_t scan_and_gather(raw::GatherArgs& a, bool fw, raw::Pair* agg, r
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     a.pre = pre;
-    if (fw) hipLaunchKernelGGL(raw::gather_kernel<true>, dim3((unsigned)nt), dim3(256), 0, stream, a);
-    else hipLaunchKernelGGL(raw::gather_kernel<false>, dim3((unsigned)nt), dim3(256), 0, stream, a);
+    if (fw) hipLaunchKernelGGL((raw::gather_kernel<true, 4, true>), dim3((unsigned)nt), dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL((raw::gather_kernel<false, 4, true>), dim3((unsigned)nt), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 
