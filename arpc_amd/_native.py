@@ -38,6 +38,7 @@ SIGNATURES = {
     "sym_ctx_reserve": (_int, [_ctx, _u64]),
     "sym_ctx_check": (_int, [_ctx, _vp]),
     "sym_ctx_set_decode_impl": (_int, [_ctx, _int]),
+    "sym_ctx_decode_redos": (_int, [_ctx, _vp, _u64p]),
     "sym_ctx_set_encode_impl": (_int, [_ctx, _int]),
     "sym_schema_info": (_int, [_int, ctypes.POINTER(_int), ctypes.POINTER(_int)]),
     "sym_record_overhead": (_u64, [_int]),

@@ -101,6 +101,14 @@ class Codec:
         """SYM_DECODE_PIPELINE (default), SYM_DECODE_THREE_KERNEL or SYM_DECODE_LOOKBACK (same results)."""
         _native.check(self._lib.sym_ctx_set_decode_impl(self._ctx, impl), "sym_ctx_set_decode_impl")
 
+    def decode_redos(self, stream=None) -> int:
+        """Re-decodes the speculative decode's gate has run on this ctx so far (synchronizes `stream`)."""
+        import ctypes
+        v = ctypes.c_uint64(0)
+        _native.check(self._lib.sym_ctx_decode_redos(self._ctx, _stream_handle(self.device, stream), ctypes.byref(v)),
+                      "sym_ctx_decode_redos")
+        return int(v.value)
+
     def set_encode_impl(self, impl: int):
         """Mixed Get/Set encodes' size scan: SYM_ENCODE_PIPELINE (default), SYM_ENCODE_THREE_KERNEL or
         SYM_ENCODE_LOOKBACK (same results)."""

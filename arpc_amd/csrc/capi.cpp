@@ -133,7 +133,7 @@ int sym_ctx_create(int device, sym_ctx** out_ctx) {
     sym_ctx* c = new (std::nothrow) sym_ctx;
     if (!c) return fail(SYM_ERR_NOMEM, "sym_ctx_create: out of host memory");
     c->device = device;
-    if ((e = hipMalloc(&c->err, 16)) != hipSuccess || (e = hipMemset(c->err, 0, 16)) != hipSuccess) {
+    if ((e = hipMalloc(&c->err, 32)) != hipSuccess || (e = hipMemset(c->err, 0, 32)) != hipSuccess) {
         sym_ctx_destroy(c);
         return hip_fail(e, "sym_ctx_create");
     }
@@ -186,6 +186,15 @@ int sym_ctx_check(sym_ctx* ctx, void* stream) {
     return fail(SYM_ERR_CAPACITY, "output capacity exceeded (decode column, Raw getter values or firewall kept bytes; device error bits 0x%x)", bits);
 }
 
+int sym_ctx_decode_redos(sym_ctx* ctx, void* stream, uint64_t* out) {
+    if (!ctx || !out) return fail(SYM_ERR_INVALID, "sym_ctx_decode_redos: ctx or out is NULL");
+    DeviceGuard g(ctx->device);
+    if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
+    hipError_t e = hipStreamSynchronize((hipStream_t)stream);
+    if (e == hipSuccess) e = hipMemcpy(out, ctx->err + 6, sizeof(uint64_t), hipMemcpyDeviceToHost);
+    return e == hipSuccess ? SYM_OK : hip_fail(e, "sym_ctx_decode_redos");
+}
+
 int sym_ctx_set_decode_impl(sym_ctx* ctx, int impl) {
     if (!ctx) return fail(SYM_ERR_INVALID, "sym_ctx_set_decode_impl: ctx is NULL");
     if (impl != SYM_DECODE_PIPELINE && impl != SYM_DECODE_THREE_KERNEL && impl != SYM_DECODE_LOOKBACK)
@@ -193,8 +202,9 @@ int sym_ctx_set_decode_impl(sym_ctx* ctx, int impl) {
     ctx->decode_impl = impl;
     // A new choice starts without a speculation hold: every hold an earlier call set (or a call still
     // running sets) names a call number below the ones from now on, so it is stale (decode_pipe.hip
-    // spec_held).  Host-side only: nothing to order against decodes still on the caller's streams.
-    ctx->decode_seq += symhip::kSpecHoldCalls + 1;
+    // spec_held, spec_tile_held).  Host-side only: nothing to order against decodes still on the
+    // caller's streams.
+    ctx->decode_seq += (symhip::kSpecHoldCalls > symhip::kTileHoldCalls ? symhip::kSpecHoldCalls : symhip::kTileHoldCalls) + 1;
     return SYM_OK;
 }
 

@@ -116,6 +116,9 @@ size_t decode_pipe_flag_bytes(int nvar, uint64_t n);
 constexpr unsigned kEpochLimit = 1u << 20;
 // Decode calls that parse exactly after a batch whose speculative lengths missed (decode_pipe.hip).
 constexpr uint64_t kSpecHoldCalls = 64;
+// Decode calls that read every SetRequest's own key length (instead of one per tile) after a batch
+// whose tiles did not share one key length (decode_pipe.hip, tile-uniform speculation).
+constexpr uint64_t kTileHoldCalls = 1024;
 hipError_t launch_decode_pipe(const DecodeParams& p, void* flags, unsigned epoch, hipStream_t stream);
 
 #ifdef SYMHIP_TUNING

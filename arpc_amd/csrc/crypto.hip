@@ -101,7 +101,7 @@ __device__ inline u32x4 wave_xor_u32x4(u32x4 v) {
 
 __device__ inline u32 ld_le32(uintptr_t p) { return ld_u32(p); }
 __device__ __forceinline__ u64 lane_u64c(u64 v, int l) {
-    return (u64)__builtin_amdgcn_readlane((u32)v, l) | ((u64)__builtin_amdgcn_readlane((u32)(v >> 32), l) << 32);
+    return (u64)(u32)__builtin_amdgcn_readlane((u32)v, l) | ((u64)(u32)__builtin_amdgcn_readlane((u32)(v >> 32), l) << 32);
 }
 
 // bytes [0, m) at p (m <= 16) as little-endian words, zero above m; reads only aligned blocks that

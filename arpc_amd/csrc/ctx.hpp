@@ -29,7 +29,9 @@ struct sym_ctx {
     size_t flag_bytes = 0;
     unsigned epoch = 0;     // tag of the last decode call's look-back words
     unsigned* err = nullptr;  // [0] device error word (kErr* bits); [1] unused; [2..3] the decode's
-                              // speculation hold (decode_pipe.hip spec_held), a u64 epoch
+                              // speculation hold (decode_pipe.hip spec_held), [4..5] its tile-key
+                              // hold (spec_tile_held), u64 call numbers; [6..7] the gate's re-decode
+                              // count (sym_ctx_decode_redos)
     // scan workspace of the packetizer, the field getters, the flat decode and the mixed encode
     // (stream-ordered, so calls on one stream share it)
     void* frag = nullptr;

@@ -247,7 +247,7 @@ __global__ __launch_bounds__(kScanThreads) void decode_scan_kernel(DecodeParams 
             if (e0 + 64 * k >= te) v[k] = 0;
             const u64 inc = wave_incl_scan_u32w_dpp(v[k]);
             ex[k] = run + inc - v[k];
-            run += (u64)__builtin_amdgcn_readlane((u32)inc, 63) | ((u64)__builtin_amdgcn_readlane((u32)(inc >> 32), 63) << 32);
+            run += (u64)(u32)__builtin_amdgcn_readlane((u32)inc, 63) | ((u64)(u32)__builtin_amdgcn_readlane((u32)(inc >> 32), 63) << 32);
         }
         if (lane == 0) s_wsum[wave] = run;
         __syncthreads();

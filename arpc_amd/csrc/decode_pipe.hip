@@ -13,7 +13,9 @@
 //               lengths only, and publishes the tile's per-column aggregate word.  They never wait.
 //               kv layouts (no int32 fields) by default parse SPECULATIVELY: the lengths a record
 //               laid out as the generator writes it has, from its length alone and at most one
-//               4-byte load (spec_flen) -- the parsers' header reads were ~10 % of the decode time.
+//               4-byte load (spec_flen) -- the parsers' header reads were ~10 % of the decode time --
+//               and (round 6) that one load only once per tile, for the tile's first SetRequest
+//               (tile-key speculation: the copier's stage is then the only read of a record's head).
 //               Every copier checks them against Go's exact parse of its staged bytes; a second
 //               launch (the gate) decodes the batch again exactly if any was wrong.
 //   P           scanner: walks the tiles in order, 1024 per step, and publishes every tile's
@@ -70,6 +72,7 @@ __host__ __device__ inline u64 num_tiles(u64 n) { return (n + kRecs - 1) / kRecs
 // calls (other tags, or another call's words where a larger batch put them) are ignored.
 constexpr int kCtrlMismatch = 0;
 constexpr int kCtrlSpecErr = 1;
+constexpr int kCtrlTileMiss = 2;  // tile-key speculation: a record's own key length differed from its tile's
 __device__ __forceinline__ u64* ctrl_words(u64* flags, int nv, u64 ntiles) { return flags + (size_t)2 * nv * ntiles + 32; }
 
 template <int NV, int STG>
@@ -174,8 +177,8 @@ __device__ __forceinline__ void parse_tiles(const DecodeParams& p, u64* aw, u64 
 #pragma unroll
             for (int f = 0; f < NV; ++f) {
                 const u64 inc = wave_incl_scan_u32w_dpp((u32)flen[f]);
-                const u64 agg = (u64)__builtin_amdgcn_readlane((u32)inc, 63) |
-                                ((u64)__builtin_amdgcn_readlane((u32)(inc >> 32), 63) << 32);
+                const u64 agg = (u64)(u32)__builtin_amdgcn_readlane((u32)inc, 63) |
+                                ((u64)(u32)__builtin_amdgcn_readlane((u32)(inc >> 32), 63) << 32);
                 if (lane == f) store_word(&aw[(size_t)f * ntiles + th[h]], make_word(epoch, kStAgg, agg));
             }
         }
@@ -215,9 +218,31 @@ __device__ __forceinline__ bool spec_held(const DecodeParams& p) {
     return p.seq < h && h - p.seq <= kSpecHold;
 }
 
+// Tile-key speculation (PipeCfg::tilek): a speculative parser reads ONE first length prefix per tile
+// -- the first two-field record's k0 -- and takes it for every two-field record of the tile, so the
+// parsers touch one stream line per 64 records instead of one per SetRequest (the copier's stage is
+// then the only other read of the record heads).  Every copier checks its records' own k0 (from the
+// staged bytes) against its tile's; a difference tags ctrl[kCtrlTileMiss], the gate decodes the batch
+// again exactly, and the next kTileHold calls read every record's own k0 (parse_tiles_spec's
+// per-record form): a producer whose key lengths vary pays the re-decode once per kTileHold calls.
+constexpr u64 kTileHold = kTileHoldCalls;  // decode calls (codec.hpp)
+__device__ __forceinline__ u64* spec_tile_hold_word(const DecodeParams& p) { return (u64*)(p.err + 4); }
+__device__ __forceinline__ bool spec_tile_held(const DecodeParams& p) {
+    const u64 h = *spec_tile_hold_word(p);
+    return p.seq < h && h - p.seq <= kTileHold;
+}
+
+// The tile's key length under tile-key speculation (wave-uniform; lane = record): the first length
+// prefix of the first record that has two fields and at least 30 bytes (the only records spec_flen
+// reads k0 for), 0 when there is none.  `cand` / `k0own`: this lane's record qualifies / its own k0.
+__device__ __forceinline__ u32 tile_k0_of(bool cand, u32 k0own) {
+    const u64 bm = __ballot(cand);
+    return bm ? (u32)__builtin_amdgcn_readlane(k0own, (int)__builtin_ctzll(bm)) : 0u;
+}
+
 // parse_tiles with speculative lengths: the record offsets (and types), plus one 4-byte load per
-// two-field record.
-template <int NV, bool MIX, int R>
+// two-field record, or (TILEK) per tile: the first two-field record's, taken for the whole tile.
+template <int NV, bool MIX, int R, bool TILEK = false>
 __device__ __forceinline__ void parse_tiles_spec(const DecodeParams& p, u64* aw, u64 ntiles, u32 epoch, const u64 (&th)[R]) {
     const int lane = threadIdx.x & 63;
     const u64 n = p.n;
@@ -226,16 +251,35 @@ __device__ __forceinline__ void parse_tiles_spec(const DecodeParams& p, u64* aw,
     u64 L[R];
     int nvr[R];
     u32 k0[R];
+    u64 st[R];
 #pragma unroll
     for (int h = 0; h < R; ++h) {
         const u64 r = th[h] * kRecs + lane;
         live[h] = th[h] < ntiles && r < n;
         const u64 rc = live[h] ? r : n;
-        const u64 st = p.rec_off[rc];
-        L[h] = p.rec_off[live[h] ? rc + 1 : rc] - st;
+        st[h] = p.rec_off[rc];
+        L[h] = p.rec_off[live[h] ? rc + 1 : rc] - st[h];
         nvr[h] = rec_nvar<NV, MIX>(p, live[h] ? r : 0);
-        const bool rd = live[h] && nvr[h] == 2 && L[h] >= 30;
-        k0[h] = *(gc_u32*)(rd ? in + st + 22 : (uintptr_t)aw);
+        if constexpr (!TILEK) {
+            const bool rd = live[h] && nvr[h] == 2 && L[h] >= 30;
+            k0[h] = *(gc_u32*)(rd ? in + st[h] + 22 : (uintptr_t)aw);
+        }
+    }
+    if constexpr (TILEK) {
+        // one line per tile: the first qualifying record's start, broadcast, and one lane's load
+#pragma unroll
+        for (int h = 0; h < R; ++h) {
+            const u64 bm = __ballot(NV == 2 && live[h] && nvr[h] == 2 && L[h] >= 30);
+            const int fl = bm ? (int)__builtin_ctzll(bm) : 0;
+            const u64 sf = (u64)(u32)__builtin_amdgcn_readlane((u32)st[h], fl) |
+                           ((u64)(u32)__builtin_amdgcn_readlane((u32)(st[h] >> 32), fl) << 32);
+            k0[h] = *(gc_u32*)(bm && lane == fl ? in + sf + 22 : (uintptr_t)aw);
+        }
+#pragma unroll
+        for (int h = 0; h < R; ++h) {
+            const u64 bm = __ballot(NV == 2 && live[h] && nvr[h] == 2 && L[h] >= 30);
+            k0[h] = bm ? (u32)__builtin_amdgcn_readlane(k0[h], (int)__builtin_ctzll(bm)) : 0u;
+        }
     }
 #pragma unroll
     for (int h = 0; h < R; ++h) {
@@ -245,8 +289,8 @@ __device__ __forceinline__ void parse_tiles_spec(const DecodeParams& p, u64* aw,
 #pragma unroll
             for (int f = 0; f < NV; ++f) {
                 const u64 inc = wave_incl_scan_u32w_dpp((u32)flen[f]);
-                const u64 agg = (u64)__builtin_amdgcn_readlane((u32)inc, 63) |
-                                ((u64)__builtin_amdgcn_readlane((u32)(inc >> 32), 63) << 32);
+                const u64 agg = (u64)(u32)__builtin_amdgcn_readlane((u32)inc, 63) |
+                                ((u64)(u32)__builtin_amdgcn_readlane((u32)(inc >> 32), 63) << 32);
                 if (lane == f) store_word(&aw[(size_t)f * ntiles + th[h]], make_word(epoch, kStAgg, agg));
             }
         }
@@ -255,15 +299,17 @@ __device__ __forceinline__ void parse_tiles_spec(const DecodeParams& p, u64* aw,
 
 // Parser workgroup blockIdx.x of P: each wave takes R consecutive tiles per step, steps P * 4 * R
 // tiles apart.  SPEC: speculative lengths unless the ctx holds exact parsing (spec_held).
-template <int NF, int NV, bool MIX, int R = 2, int WB = 32, bool SPEC = false>
+template <int NF, int NV, bool MIX, int R = 2, int WB = 32, bool SPEC = false, bool TILEK = false>
 __device__ void parser(const DecodeParams& p, u64* aw, u64 ntiles, u32 epoch, u32 P) {
     const int wave = threadIdx.x >> 6;
     const bool held = SPEC && NF == 0 && spec_held(p);  // exact parsing this call (wave-uniform)
+    const bool tile = TILEK && NV == 2 && SPEC && NF == 0 && !held && !spec_tile_held(p);  // one k0 per tile
     for (u64 j = ((u64)blockIdx.x * 4 + wave) * R; j < ntiles; j += (u64)P * 4 * R) {
         u64 th[R];
 #pragma unroll
         for (int h = 0; h < R; ++h) th[h] = j + h < ntiles ? j + h : ntiles;  // past the end: skipped
-        if (SPEC && NF == 0 && !held) parse_tiles_spec<NV, MIX, R>(p, aw, ntiles, epoch, th);
+        if (TILEK && tile) parse_tiles_spec<NV, MIX, R, true>(p, aw, ntiles, epoch, th);
+        else if (SPEC && NF == 0 && !held) parse_tiles_spec<NV, MIX, R>(p, aw, ntiles, epoch, th);
         else parse_tiles<NF, NV, MIX, R, WB>(p, aw, ntiles, epoch, th);
     }
 }
@@ -371,6 +417,24 @@ __device__ __forceinline__ void exact_parse(bool live, u64 L, int nvr, Rd8&& rd8
     }
 }
 
+// Tile-key check (wave 0 of a copier, lane = record): `own` are the speculative lengths from the
+// record's own first length prefix k0 (staged bytes); the parsers took the tile's k0 instead
+// (tile_k0_of, the same rule).  Any record whose lengths differ tags ctrl[kCtrlTileMiss] (once).
+template <int NV>
+__device__ __forceinline__ void tile_check(u64* flags, u64 ntiles, u32 epoch, bool live, u64 L, int nvr, u32 k0,
+                                           const u64 (&own)[NV]) {
+    const bool cand = live && nvr == 2 && L >= 30;
+    const u32 kt = tile_k0_of(cand, cand ? k0 : 0u);
+    u64 tf[NV];
+    spec_flen<NV>(live ? L : 0, nvr, kt, tf);
+    bool tm = false;
+#pragma unroll
+    for (int f = 0; f < NV; ++f) tm |= tf[f] != own[f];
+    u64* const ctrl = ctrl_words(flags, NV, ntiles);
+    if (__ballot(tm) && (threadIdx.x & 63) == 0 && !tagged(load_word(&ctrl[kCtrlTileMiss]), epoch))
+        store_word(&ctrl[kCtrlTileMiss], make_word(epoch, kStAgg, 1));
+}
+
 // ---------------------------------------------------------------- the copier
 // Tile `tile`: stage, parse (wave 0), prefix, copy.  forced: no parsers / scanner in this launch, so
 // the prefix comes from look-back at once.  SPEC: the parsers published speculative aggregates
@@ -379,7 +443,7 @@ __device__ __forceinline__ void exact_parse(bool live, u64 L, int nvr, Rd8&& rd8
 // a capacity error is tagged in ctrl[kCtrlSpecErr] (it may come from a speculative prefix), merged
 // into p.err by the gate when the speculation held.
 template <int NF, int NV, bool MIX, int MODE, int DIAG, int STG, bool SPEC, int UK = kU, bool FAST = false, bool LOC = false,
-          bool CANON = false>
+          bool CANON = false, bool TILEK = false>
 __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 epoch, u64 tile, bool forced, Lds<NV, STG>& S) {
     constexpr int kLoads = (STG / 16 + kThreads - 1) / kThreads;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -410,6 +474,9 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
     // after the stage, and wave 0 runs Go's exact parse as the check WHILE waves 1-3 copy
     const bool fast = FAST && SPEC && NF == 0 && !held;
     const bool canon = CANON && SPEC && NF == 0 && !held && !fast;
+    // TILEK: the parsers took one key length per tile (spec_tile_held: unless held); the check also
+    // compares every record's own k0 with its tile's
+    const bool tilek_on = TILEK && NV == 2 && SPEC && NF == 0 && !held && !fast && !spec_tile_held(p);
     u32 ty = 1;  // mixed batches: the record's type, loaded with its offsets (not after the stage)
     if (wave == 0) {
         start = p.rec_off[r0 + min(lane, cnt)];
@@ -478,6 +545,7 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
             spec_flen<NV>(live ? L : 0, nvr, k0, flen);
             fpos[0] = nvr == 2 ? 26 : 22;
             if constexpr (NV == 2) fpos[1] = 30 + (u64)k0;
+            if (TILEK && tilek_on) tile_check<NV>(flags, ntiles, epoch, live, L, nvr, k0, flen);
             if (__ballot(live && !ok)) {
                 if (DIAG && lane == 0) atomicAdd((unsigned long long*)&p.dbg[ntiles * 8], 1ull);  // waves off the image
                 u64 elen[NV], epos[NV];
@@ -514,6 +582,7 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
             bool mm = false;
 #pragma unroll
             for (int f = 0; f < NV; ++f) mm |= sf[f] != flen[f];
+            if (TILEK && tilek_on) tile_check<NV>(flags, ntiles, epoch, live, L, nvr, k0, sf);
             // (tag once: when every record misses, 16k copiers storing to one word contend)
             if (__ballot(mm) && lane == 0 && !tagged(load_word(&ctrl[kCtrlMismatch]), epoch))
                 store_word(&ctrl[kCtrlMismatch], make_word(epoch, kStAgg, 1));
@@ -525,8 +594,8 @@ __device__ __forceinline__ void copier(const DecodeParams& p, u64* flags, u32 ep
 #pragma unroll
         for (int f = 0; f < NV; ++f) {
             const u64 inc = wave_incl_scan_u32w_dpp((u32)flen[f]);
-            agg[f] = (u64)__builtin_amdgcn_readlane((u32)inc, 63) |
-                     ((u64)__builtin_amdgcn_readlane((u32)(inc >> 32), 63) << 32);
+            agg[f] = (u64)(u32)__builtin_amdgcn_readlane((u32)inc, 63) |
+                     ((u64)(u32)__builtin_amdgcn_readlane((u32)(inc >> 32), 63) << 32);
             excl[f] = inc - flen[f];
             too_large |= agg[f] >= ((u64)1 << 31);  // positions inside a tile's range are 32-bit
             nch[f] = (u32)((flen[f] + 15) >> 4);
@@ -736,6 +805,7 @@ struct PipeCfg {
     bool loc = false;   // copy chunks find their record by ballots instead of a binary search
     bool canon = false; // speculative kv decodes: the copier checks the generator's header image, Go's
                         // exact parse only for records that differ from it
+    bool tilek = false; // speculative two-field kv decodes: one key length read per tile (spec_tile_held)
 };
 
 template <int NF, int NV, bool MIX, PipeCfg C>
@@ -752,7 +822,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(C.wpe,
     const bool forced = p.impl == kImplLookback;  // parsers and scanner idle: look-back only
     constexpr bool kRoles = C.mode == 0;
     if (kRoles && blockIdx.x < P) {
-        if (!forced) parser<NF, NV, MIX, C.pr, 32, C.spec>(p, aw, ntiles, epoch, P);
+        if (!forced) parser<NF, NV, MIX, C.pr, 32, C.spec, C.tilek>(p, aw, ntiles, epoch, P);
         return;
     }
     if (kRoles && blockIdx.x == P) {
@@ -761,8 +831,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(C.wpe,
     }
     const u64 tile = kRoles ? blockIdx.x - P - 1 : blockIdx.x;
     if (tile >= ntiles) return;
-    copier<NF, NV, MIX, C.mode, C.diag, C.stg, C.spec && C.mode == 0 && C.specx != 1, C.uk, C.fast, C.loc, C.canon>(p, flags, epoch,
-                                                                                                           tile, forced, S);
+    copier<NF, NV, MIX, C.mode, C.diag, C.stg, C.spec && C.mode == 0 && C.specx != 1, C.uk, C.fast, C.loc, C.canon, C.tilek>(
+        p, flags, epoch, tile, forced, S);
 }
 
 // ---------------------------------------------------------------- the gate
@@ -778,13 +848,19 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
     __shared__ Lds<NV, kStage> S;
     const u64 ntiles = num_tiles(p.n);
     u64* const ctrl = ctrl_words(flags, NV, ntiles);
-    const bool redo = tagged((u64)uniform_i64((i64)load_word(&ctrl[kCtrlMismatch])), epoch);
+    const bool miss = tagged((u64)uniform_i64((i64)load_word(&ctrl[kCtrlMismatch])), epoch);
+    const bool tmiss = tagged((u64)uniform_i64((i64)load_word(&ctrl[kCtrlTileMiss])), epoch);
+    const bool redo = miss || tmiss;
     if (!redo && blockIdx.x == 0 && threadIdx.x == 0) {
         const u64 e = load_word(&ctrl[kCtrlSpecErr]);
         if (tagged(e, epoch)) atomicOr(p.err, (unsigned)(e & kValMask));
     }
     if (!redo) return;
-    if (blockIdx.x == 0 && threadIdx.x == 0) *spec_hold_word(p) = p.seq + kSpecHold + 1;  // the next kSpecHold calls parse exactly
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (miss) *spec_hold_word(p) = p.seq + kSpecHold + 1;        // the next kSpecHold calls parse exactly
+        if (tmiss) *spec_tile_hold_word(p) = p.seq + kTileHold + 1;  // the next kTileHold calls read every k0
+        *(u64*)(p.err + 6) += 1;  // the ctx's re-decode count (sym_ctx_decode_redos; stream-ordered)
+    }
     // the exact pipeline on a persistent grid: a quarter of the workgroups parse every tile exactly,
     // one scans, the rest copy tiles c, c + C, ... (a copier whose prefix is late looks back, so no
     // role waits on residency)
@@ -877,12 +953,14 @@ namespace pipe {
 // kv layouts: copy chunks located by ballots, the copier's check on the generator's header image
 // (round 5, tools/kbench.py: config 2 159 -> 155 us, config 3 393 -> 385 us; variant 730 is the
 // round-4 form)
-constexpr PipeCfg kSpecCfg{.sk = 1, .spec = true, .loc = true, .canon = true};
+// round 6: one key length read per tile (tilek; tools/kbench.py, one process: config 2 162.6 -> 156.1 us,
+// config 3 386.9 -> 369.7 us, the mix 101.7 -> 100.8 us; profiles/r06_*)
+constexpr PipeCfg kSpecCfg{.sk = 1, .spec = true, .loc = true, .canon = true, .tilek = true};
 constexpr PipeCfg kExactCfg{.spec = true};          // int32 layouts (exact parsers: spec needs NF == 0)
 // mixed Get/Set batches: 8 waves per SIMD (<= 64 VGPRs) with a 16 KiB stage, 8 copiers per CU
 // (tuning variant 740; r04b: 117.7 -> 102.4 us for the 2^20-record mix, trace mix 551 -> 554 us;
 // config 2's 350-byte records run slower so, 159 -> 188 us, and keep kSpecCfg)
-constexpr PipeCfg kMixCfg{.sk = 1, .stg = 16384, .spec = true, .wpe = 8};
+constexpr PipeCfg kMixCfg{.sk = 1, .stg = 16384, .spec = true, .wpe = 8, .tilek = true};
 }  // namespace pipe
 
 hipError_t launch_decode_pipe(const DecodeParams& p, void* flags, unsigned epoch, hipStream_t stream) {
@@ -957,6 +1035,10 @@ hipError_t launch_decode_pipe(const DecodeParams& p, void* flags, unsigned epoch
         case 787: return launch_layout<PipeCfg{.diag = 1, .sk = 1, .stg = 16384, .spec = true, .wpe = 8, .canon = true}>(p, fl, epoch, stream, 1, 2);
         case 768: return launch_layout<PipeCfg{.sk = 1, .stg = 16384, .spec = true, .wpe = 8, .canon = true}>(p, fl, epoch, stream, 1, 2);
         case 763: return launch_layout<PipeCfg{.sk = 1, .stg = 16384, .spec = true, .wpe = 8, .loc = true}>(p, fl, epoch, stream, 1, 2);
+        // round 6: one key length read per tile (tile-key speculation), kv layouts / the mixed batch
+        case 792: return launch_layout<PipeCfg{.sk = 1, .spec = true, .loc = true, .canon = true, .tilek = true}>(p, fl, epoch, stream, 1, 2);
+        case 793: return launch_layout<PipeCfg{.sk = 1, .stg = 16384, .spec = true, .wpe = 8, .tilek = true}>(p, fl, epoch, stream, 1, 2);
+        case 794: return launch_layout<PipeCfg{.mode = 1, .sk = 1, .loc = true, .canon = true}>(p, fl, epoch, stream, 1, 2);
         default: break;
     }
 #endif

@@ -928,7 +928,7 @@ __global__ __launch_bounds__(256) void mixed_size_kernel(EncodeParams p, MixedWs
         const u64 t = t0 + k, a = t * kWaveRecs, r = a + lane;
         const u32 extra = r < n && ty[k] != 0 ? (u32)(8 + (v1[k] - v0[k])) : 0u;  // < 2^32 (u32 lengths)
         const u64 inc = wave_incl_scan_u32w_dpp(extra);
-        const u64 sum = (u64)__builtin_amdgcn_readlane((u32)inc, 63) | ((u64)__builtin_amdgcn_readlane((u32)(inc >> 32), 63) << 32);
+        const u64 sum = (u64)(u32)__builtin_amdgcn_readlane((u32)inc, 63) | ((u64)(u32)__builtin_amdgcn_readlane((u32)(inc >> 32), 63) << 32);
         if (lane == 0)
             s_agg[wave * kTilesPerWave + k] = t < ntiles ? 22 * (min(a + kWaveRecs, n) - a) + (kb[k] - ka[k]) + sum : 0;
     }

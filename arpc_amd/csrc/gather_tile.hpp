@@ -19,7 +19,7 @@ struct WaveLds {
 };
 
 __device__ __forceinline__ u64 readlane_u64(u64 v, int l) {
-    return (u64)__builtin_amdgcn_readlane((u32)v, l) | ((u64)__builtin_amdgcn_readlane((u32)(v >> 32), l) << 32);
+    return (u64)(u32)__builtin_amdgcn_readlane((u32)v, l) | ((u64)(u32)__builtin_amdgcn_readlane((u32)(v >> 32), l) << 32);
 }
 
 // One 256-segment tile (a workgroup loop body of gather_kernel, or of flat.hip's dec_emit_kernel).

@@ -24,7 +24,7 @@ constexpr u64 kFallbackTicks = 100000; // 1 ms: a copier waits this long for its
 __device__ __forceinline__ u64 now_ticks() { return __builtin_amdgcn_s_memrealtime(); }
 
 __device__ __forceinline__ u64 lane_u64_pub(u64 v, int l) {
-    return (u64)__builtin_amdgcn_readlane((u32)v, l) | ((u64)__builtin_amdgcn_readlane((u32)(v >> 32), l) << 32);
+    return (u64)(u32)__builtin_amdgcn_readlane((u32)v, l) | ((u64)(u32)__builtin_amdgcn_readlane((u32)(v >> 32), l) << 32);
 }
 __device__ __forceinline__ bool tagged(u64 w, u32 epoch) { return (u32)(w >> kEpochShift) == epoch; }
 __device__ __forceinline__ u64 make_word(u32 epoch, u64 st, u64 v) {

@@ -130,7 +130,7 @@ def launch_check(args) -> None:
         dist.all_gather_object(got, (rank, local, os.getpid()))
         ranks = got
     if rank == 0:
-        print(json.dumps({"launch_check": True, "n_gpus": world, "gpus_requested": args.gpus,
+        print(json.dumps({"launch_check": True, "n_gpus": world, "gpus_requested": args.gpus, "config": args.config,
                           "ranks": ranks, "elapsed_max_s": el}), flush=True)
     if world > 1:
         import torch.distributed as dist
@@ -278,7 +278,7 @@ def cpu_baseline(kw: dict, seconds: float) -> dict:
                              "note": "EchoRequest{42, 300, alice, hello world} (54 B), marshal then unmarshal, "
                                      "one record per call with Go's allocations (oracle/bench_oracle.c, "
                                      "testcases/simple/main.go:248-420 methodology), 1 thread"},
-            "sample": f"the headline batch itself: {b.n} {s.go_type} records (seed {kw['seed']:#x}), encode into a "
+            "sample": f"the headline workload: {b.n} {s.go_type} records (seed {kw['seed']:#x}), encode into a "
                       f"preallocated stream + decode into preallocated columns, {len(rates)} rounds on 1 thread "
                       f"pinned to CPU {cpus[0]} (median, spread min..max), {rounds} rounds on {threads} pinned "
                       "threads over record shards (aggregate); oracle/symphony_oracle.c (-O2): the C "
@@ -290,12 +290,13 @@ def decode_kernel_name(s, mixed: bool = False) -> str:
     kv layouts (no int32 fields) run the speculative parsers with 256-tile scanner steps
     (decode_pipe.hip kSpecCfg), followed by the small gate launch; int32 layouts the exact parsers
     (kExactCfg); the mixed batch 8 waves per SIMD with a 16 KiB stage (kMixCfg).
-    PipeCfg{mode, diag, sk, pr, stg, spec, specx, wpe, uk, fast, loc, canon} (trailing defaults are
-    not printed); kSpecCfg's copiers locate chunks by ballots and check the generator's header image."""
+    PipeCfg{mode, diag, sk, pr, stg, spec, specx, wpe, uk, fast, loc, canon, tilek} (trailing defaults
+    are not printed); kSpecCfg's copiers locate chunks by ballots and check the generator's header image;
+    both speculative configs read one key length per tile (tilek)."""
     if mixed:
-        cfg = "0, 0, 1, 2, 16384, true, 0, 8, 2"
+        cfg = "0, 0, 1, 2, 16384, true, 0, 8, 2, false, false, false, true"
     else:
-        cfg = "0, 0, 1, 2, 22528, true, 0, 6, 2, false, true, true" if s.nfixed == 0 else "0, 0, 2, 2, 22528, false, 0, 6, 2"
+        cfg = "0, 0, 1, 2, 22528, true, 0, 6, 2, false, true, true, true" if s.nfixed == 0 else "0, 0, 2, 2, 22528, false, 0, 6, 2"
     return f"decode_pipe_kernel<{s.nfixed}, {s.nvar}, {'true' if mixed else 'false'}, symhip::pipe::PipeCfg{{{cfg}}}>"
 
 
@@ -970,9 +971,11 @@ def mixed_leg(codec: Codec, dev, reps: int, cfg=None) -> dict:
                     "groups, scanner, encode tiles); client IDs: service 1, Get 1, Set 2"}
 
 
-def config3_leg(codec: Codec, dev, reps: int, cfg=None) -> dict:
+def config3_leg(codec: Codec, dev, reps: int, cfg=None, workload: str | None = "config3") -> dict:
     """2^20 SetRequests, K=64, V log-uniform 16-4096 B (mean ~736 B, 774 MB stream:
-    no set fits the Infinity Cache), encode + decode device-resident, HIP events, two buffer sets."""
+    no set fits the Infinity Cache), encode + decode device-resident, HIP events, two buffer sets.
+    `cfg` another SetRequest workload (the trace sizes, config 4's shard); `workload` names its traffic
+    entry in profiles/traffic.json for the leg's roofline (None: no traffic figure)."""
     b = datagen.make_batch(**(cfg or datagen.CONFIG3))
     s = b.schema
     n = b.n
@@ -1006,14 +1009,73 @@ def config3_leg(codec: Codec, dev, reps: int, cfg=None) -> dict:
     ok = all(bool((dec.status == 0).all()) and torch.equal(dec.var[1][0][:caps[1]], var[1][0])
              for var, _, dec in sets)
     enc_b, dec_b = alg_bytes(n, s.nvar, var_total, total)
-    return {"records": n, "stream_bytes": total, "round_trip_ok": ok,
+    dname = decode_kernel_name(s)
+    kname, dom_ms, dom_b = (ENCODE_KERNEL, enc_ms, enc_b) if enc_ms >= dec_ms else (dname, dec_ms, dec_b)
+    ach = dom_b / (dom_ms * 1e-3) / 1e9
+    roof = {"bound": "hbm", "kernel": kname, "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": load_traffic(kname, workload) if workload else None}
+    return {"records": n, "stream_bytes": total, "round_trip_ok": ok, "roofline": roof,
             "encode_ms": round(enc_ms, 4), "encode_gbps": round(enc_b / enc_ms / 1e6, 1),
             "decode_ms": round(dec_ms, 4), "decode_gbps": round(dec_b / dec_ms / 1e6, 1),
             "ms_per_pair": round(pair_ms, 4),
             "gbps_algorithmic": round((enc_b + dec_b) / pair_ms / 1e6, 1),
             "gbps_algorithmic_per_call_events": round((enc_b + dec_b) / (enc_ms + dec_ms) / 1e6, 1),
-            "kernels": {"encode": ENCODE_KERNEL, "decode": decode_kernel_name(schemas.BY_NAME["kv_set_request"])},
+            "kernels": {"encode": ENCODE_KERNEL, "decode": dname},
             "note": "config 3 (seed 0x5EED0002), the headline's algorithmic byte definition"}
+
+
+def summary_of(line: dict) -> dict:
+    """A compact digest of the line's legs (GB/s, roofline fraction, ms), printed LAST so that a reader
+    keeping only the tail of the line (the driver's record) still sees every BASELINE configuration."""
+    r = lambda x, k=1: None if x is None else round(x, k)  # noqa: E731
+    frac = lambda g: r(g / HBM_PEAK_GBPS, 4)  # noqa: E731
+    out = {"headline": {"config": line["config"]["workload"].split(":")[0], "gbps": line["value"],
+                        "frac": line["roofline"]["frac"], "kernel": line["roofline"]["kernel"].split("<")[0],
+                        "enc_ms": line["kernels"]["encode"]["avg_ms"], "dec_ms": line["kernels"]["decode"]["avg_ms"],
+                        "n_gpus": line["n_gpus"]}}
+    for k in ("mixed", "config3", "config4_shard", "config3_trace", "mixed_trace"):
+        if k in line:
+            x = line[k]
+            rf = x.get("roofline", {})
+            out[k] = {"gbps": x["gbps_algorithmic"], "frac": rf.get("frac"),
+                      "frac_of": "dec" if rf.get("kernel", "").startswith("decode") else "enc", "enc_ms": x["encode_ms"], "dec_ms": x["decode_ms"],
+                      "ms_per_pair": x["ms_per_pair"]}
+    for k in ("reassembly", "reassembly_config3"):
+        if k in line:
+            out[k] = {"gbps": line[k]["gbps_algorithmic"], "frac": frac(line[k]["gbps_algorithmic"]),
+                      "ms": line[k]["reassemble_ms"]}
+    if "packetize" in line:
+        out["packetize"] = {"gbps": line["packetize"]["gbps_algorithmic"], "frac": frac(line["packetize"]["gbps_algorithmic"])}
+    if "crypto" in line:
+        c = line["crypto"]
+        out["crypto"] = {"enc_gbps": c["encrypt_gbps"], "dec_gbps": c["decrypt_gbps"], "enc_ms": c["encrypt_ms"],
+                         "dec_ms": c["decrypt_ms"]}
+    if "proxy" in line:
+        out["firewall"] = {"gbps": line["proxy"]["firewall_gbps"], "ms": line["proxy"]["firewall_ms"]}
+    if "flat" in line:
+        out["flat"] = {"enc_gbps": line["flat"]["encode_gbps"], "dec_gbps": line["flat"]["decode_gbps"]}
+    if "boutique" in line:
+        b = line["boutique"]
+        out["boutique"] = {"graph_enc_ms": b["graph"]["encode_ms"], "graph_dec_ms": b["graph"]["decode_ms"],
+                           "eager_enc_ms": b["encode_ms"], "eager_dec_ms": b["decode_ms"]}
+    if "boutique_payloads" in line:
+        b = line["boutique_payloads"]
+        out["boutique_payloads"] = {"graph_enc_msg_s": b["graph"]["encode_msg_per_s"],
+                                    "graph_dec_msg_s": b["graph"]["decode_msg_per_s"]}
+    if "host_inclusive" in line:
+        h = line["host_inclusive"]
+        out["host_inclusive"] = {"pinned_gbps": h["pinned"].get("gbps_algorithmic"),
+                                 "e2e_rpc_s": h["e2e_loopback"].get("rpc_per_s")}
+    if "per_record" in line:
+        pr = line["per_record"]
+        many = [v for k, v in pr.items() if k.startswith("batcher_") and k != "batcher_1_thread"]
+        out["per_record"] = {"us_1_thread": pr["batcher_1_thread"]["us_per_record_enc_plus_dec"],
+                             "records_s_many": many[0]["records_per_s"] if many else None}
+    if "cpu_baseline" in line:
+        c = line["cpu_baseline"]
+        out["cpu_baseline"] = {"gbps_1_core": c["value"], "gbps_all": c["all_cores"]["value"],
+                               "cores_all": c["all_cores"]["cores"], "kind": c["kind"]}
+    return out
 
 
 def main():
@@ -1028,7 +1090,8 @@ def main():
                          "before it); 1: every step; 0: none (the roofline is then unmeasured)")
     ap.add_argument("--overlap", type=int, default=0,
                     help="1: encode and decode of a step on two HIP streams (independent buffer sets), overlapped")
-    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4))
+    ap.add_argument("--config", type=int, default=None, choices=(2, 3, 4),
+                    help="workload (SURVEY 8d): default 2 at one GPU, 4 (a 2^23-record shard per GPU) at --gpus >= 2")
     ap.add_argument("--records", type=int, default=0, help="records per GPU (default: the config's 2^20)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--host-steps", type=int, default=5, help="host-inclusive steps (0 = skip)")
@@ -1042,6 +1105,8 @@ def main():
                     help="online-boutique reference payloads leg (all 30 types) repetitions (0 = skip)")
     ap.add_argument("--mixed-reps", type=int, default=10, help="mixed Get/Set leg repetitions (0 = skip)")
     ap.add_argument("--config3-reps", type=int, default=6, help="config 3 leg repetitions (0 = skip)")
+    ap.add_argument("--config4-reps", type=int, default=4,
+                    help="config 4 shard leg (2^23 records on this GPU) repetitions at N=1 (0 = skip)")
     ap.add_argument("--trace-reps", type=int, default=3,
                     help="trace-replay legs (config 3 trace sizes, Get/Set trace sequence) repetitions (0 = skip)")
     ap.add_argument("--per-record", type=int, default=2000,
@@ -1051,6 +1116,8 @@ def main():
     ap.add_argument("--launch-check", action="store_true",
                     help="exercise the N-rank launch only (gloo, no GPU) and print the world rank 0 saw")
     args = ap.parse_args()
+    if args.config is None:  # BASELINE config 4 is the multi-GPU configuration; config 2 the 1-GPU one
+        args.config = 4 if args.gpus > 1 or int(os.environ.get("WORLD_SIZE", "1")) > 1 else 2
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
@@ -1270,6 +1337,12 @@ def main():
         line["mixed"] = mixed_leg(codec, dev, args.mixed_reps)
     if world == 1 and args.config3_reps > 0 and args.config == 2:
         line["config3"] = config3_leg(codec, dev, args.config3_reps)
+    if world == 1 and args.config4_reps > 0 and args.config == 2:
+        # the single-GPU anchor of the config-4 scaling curve: rank 0's 2^23-record shard on this GPU
+        c4 = config3_leg(codec, dev, args.config4_reps, datagen.config4_shard(0), workload="config4")
+        c4["note"] = ("SURVEY 8d config 4's shard 0 (2^23 SetRequests, K=64, V=256, seed 0x5EED0003): what each "
+                      "rank of `bench.py --gpus N` (default config 4 at N >= 2) encodes and decodes per step")
+        line["config4_shard"] = c4
     if world == 1 and args.reassembly_reps > 0:  # the general (multi-datagram) reassembly path
         b3 = datagen.make_batch(**datagen.CONFIG3)
         f3, v3 = to_device(b3, dev)
@@ -1309,8 +1382,9 @@ def main():
         line["boutique_payloads"] = boutique_payloads_leg(codec, dev, args.payload_reps)
     if world == 1 and args.per_record > 0:
         line["per_record"] = per_record_leg(args.per_record, 64)
-    if world == 1 and args.cpu_seconds > 0:
-        line["cpu_baseline"] = cpu_baseline(kw, args.cpu_seconds)
+    if args.cpu_seconds > 0:  # rank 0 at any N, after the timed region: a bounded sample of <= 2^20 records
+        line["cpu_baseline"] = cpu_baseline(dict(kw, n=min(kw["n"], 1 << 20)), args.cpu_seconds)
+    line["summary"] = summary_of(line)
     print(json.dumps(line), flush=True)
 
 

@@ -100,8 +100,11 @@ int sym_ctx_check(sym_ctx* ctx, void* stream);
  *                           layout and the copiers check them against the exact parse; a second small
  *                           launch on the same stream (no host sync) merges the error bits, or decodes
  *                           the batch again exactly when a record did not follow that layout; the
- *                           ctx then parses exactly for its next 64 decode calls (setting the impl
- *                           clears that hold).
+ *                           ctx then parses exactly for its next 64 decode calls.  Two-field records
+ *                           (SetRequest) also take one key length per 64-record tile (the first
+ *                           SetRequest's); a tile whose keys differ makes the batch decode again the
+ *                           same way, and the ctx then reads every record's own key length for its
+ *                           next 1024 decode calls.  Setting the impl clears both holds.
  *   SYM_DECODE_THREE_KERNEL parse -> scan -> copy as three stream-ordered launches (no
  *                           inter-workgroup waiting at all).
  *   SYM_DECODE_LOOKBACK     the pipeline with its parsers and scanner idle: every copier takes the
@@ -110,6 +113,9 @@ int sym_ctx_check(sym_ctx* ctx, void* stream);
 #define SYM_DECODE_THREE_KERNEL 1
 #define SYM_DECODE_LOOKBACK 2
 int sym_ctx_set_decode_impl(sym_ctx* ctx, int impl);
+/* Re-decodes the speculative pipeline's gate has run on this ctx so far, after synchronizing `stream`
+ * (a test and tuning aid; results are identical either way). */
+int sym_ctx_decode_redos(sym_ctx* ctx, void* stream, uint64_t* out);
 /* Size-scan implementation of this ctx's mixed Get/Set encodes (sym_encode_kv_mixed; identical results):
  *   SYM_ENCODE_PIPELINE     (default) one launch: sizer workgroups publish every 64-record tile's byte
  *                           total, a scanner workgroup chains them into prefixes, encode workgroups
@@ -192,9 +198,9 @@ int sym_decode_kv_mixed(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec
 
 /* ---- host-memory entry points (synchronous) -------------------------------------
  * Same contracts with every pointer in host memory: what the per-record Go Serializer adapter and
- * the UDP buffers of pkg/transport hand over.  The batch moves through the GPU in chunks of about
- * 8 MiB of records on three streams of the ctx, so one chunk's H2D, another's kernel and a third's
- * D2H overlap.  Host memory that is pinned (sym_host_alloc, hipHostMalloc, a hipHostRegister'ed
+ * the UDP buffers of pkg/transport hand over.  The batch moves through the GPU in record chunks of
+ * about 32 MiB in three slots of the ctx over one stream per direction (H2D copies and kernels on one,
+ * D2H copies on the other), so one chunk's H2D and kernel overlap another's D2H.  Host memory that is pinned (sym_host_alloc, hipHostMalloc, a hipHostRegister'ed
  * range) is transferred by DMA in place; pageable memory is staged through the ctx's pinned buffers
  * with a host copy.  sym_decode_host: caps[f] is the capacity of h_bytes[f]; a column that does not
  * fit returns SYM_ERR_CAPACITY with the bytes that fit written.  Device-side errors of the chunks
@@ -435,8 +441,8 @@ int sym_decrypt(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec_off, ui
  * kv-store and echo schemas above are the all-private cases of this (and keep their specialised kernels).
  *   sym_flat_encode  output record i = MarshalSymphony + the client's ID patch; d_out holds
  *                    sym_flat_encoded_size(...) bytes; d_out_off[n+1] computed on the device.
- *                    A run of 64 records spanning 2 GiB or more is reported by sym_check as
- *                    SYM_ERR_TOO_LARGE.
+ *                    A run of 64 records spanning 2 GiB or more is reported by sym_ctx_check as
+ *                    SYM_ERR_INVALID ("64 consecutive records span >= 2 GiB").
  *   sym_flat_decode  UnmarshalSymphony into fresh structs: fixed columns (zero when not read),
  *                    string columns of caps[k] bytes (rec_off[n] - rec_off[0] always suffices)
  *                    with d_offs[k][n+1]; d_status[n] SYM_STATUS_*. */

@@ -31,6 +31,7 @@ def _run(args, env_extra=None, timeout=240):
 def test_launch_check_spawns_n_ranks(n):
     line = _run(["--gpus", str(n), "--launch-check"])
     assert line["n_gpus"] == n and line["gpus_requested"] == n
+    assert line["config"] == 4  # BASELINE config 4 (a 2^23-record shard per GPU) is the N >= 2 default
     ranks = sorted(tuple(r) for r in line["ranks"])
     assert [r[0] for r in ranks] == list(range(n))  # every rank joined
     assert [r[1] for r in ranks] == list(range(n))  # LOCAL_RANK = GPU index
@@ -40,6 +41,12 @@ def test_launch_check_spawns_n_ranks(n):
 def test_launch_check_world1_no_spawn():
     line = _run(["--launch-check"])
     assert line["n_gpus"] == 1 and line["ranks"] == [0]
+    assert line["config"] == 2  # the 1-GPU headline: BASELINE config 2's 2^20 SetRequests
+
+
+def test_launch_check_explicit_config_kept():
+    line = _run(["--gpus", "2", "--config", "2", "--launch-check"])
+    assert line["n_gpus"] == 2 and line["config"] == 2
 
 
 def test_failed_rank_ends_the_launch():
@@ -52,7 +59,7 @@ def test_failed_rank_ends_the_launch():
 
 @pytest.mark.gpu
 def test_bench_world2_one_gpu():
-    off = ["--cpu-seconds", "0", "--host-steps", "0", "--packetize-reps", "0", "--proxy-reps", "0",
+    off = ["--cpu-seconds", "1", "--host-steps", "0", "--packetize-reps", "0", "--proxy-reps", "0",
            "--reassembly-reps", "0", "--crypto-reps", "0", "--flat-reps", "0", "--boutique-reps", "0",
            "--payload-reps", "0", "--mixed-reps", "0", "--config3-reps", "0", "--trace-reps", "0",
            "--per-record", "0", "--ref-reps", "0"]
@@ -63,3 +70,6 @@ def test_bench_world2_one_gpu():
     assert line["value"] > 0 and line["per_gpu_gbps"] > 0
     assert 0 < line["roofline"]["frac"] < 1
     assert line["config"]["global"]["global_records"] == 2 * 65536
+    assert line["config"]["workload"].startswith("config4")  # the N >= 2 default
+    assert line["cpu_baseline"]["value"] > 0  # rank 0 carries the CPU baseline at N > 1 too
+    assert line["summary"]["headline"]["n_gpus"] == 2 and "cpu_baseline" in line["summary"]

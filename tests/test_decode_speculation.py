@@ -193,3 +193,110 @@ def test_random_batches_with_random_misfits(codec, dev, seed):
     data, rec_off = _with_trailers(stream, off, which, extra=int(rng.integers(1, 9)), seed=seed)
     got = decode_gpu(codec, s, data, rec_off, dev, misalign=int(rng.integers(0, 16)))
     assert_decode_equal(got, oracle.decode_batch(s.nfixed, s.nvar, data, rec_off), f"{schema}/{n}/{density}")
+
+
+# ---------------------------------------------------------------- tile-key speculation (round 6)
+# The parsers read one first length prefix per 64-record tile -- the tile's first SetRequest's -- and
+# take it for every SetRequest of the tile; a tile whose keys differ is caught by its copier, the gate
+# decodes the batch again exactly and the ctx reads every record's own key length for 1024 calls.
+# sym_ctx_decode_redos counts the gate's re-decodes, so these tests see which path ran.
+
+def _pipe_only(decode_impl):
+    if decode_impl != "pipe":
+        pytest.skip("the speculation and its gate run under the pipeline only")
+
+
+def _odd_key(b, which, delta=-1):
+    """The batch's key column with record(s) `which` given a key `delta` bytes longer (or shorter)."""
+    kb, ko = b.var[0]
+    keys = [kb[int(ko[i]):int(ko[i + 1])] for i in range(len(ko) - 1)]
+    for i in which:
+        k = keys[i]
+        keys[i] = k[:len(k) + delta] if delta < 0 else np.concatenate([k, np.full(delta, 0x5A, np.uint8)])
+    off = np.zeros(len(keys) + 1, np.uint64)
+    np.cumsum([len(k) for k in keys], out=off[1:])
+    return np.concatenate(keys).astype(np.uint8), off
+
+
+def test_tile_key_fixed_keys_no_redo(codec, dev, decode_impl):
+    _pipe_only(decode_impl)
+    n = 70001  # ragged last tile
+    b = datagen.make_batch(schema="kv_set_request", n=n, lens=(64, ("uniform", 0, 300)), seed=41)
+    stream, off = oracle.encode_batch(b.fixed, b.var)
+    want = oracle.decode_batch(0, 2, stream, off)
+    r0 = codec.decode_redos()
+    for k in range(3):
+        assert_decode_equal(decode_gpu(codec, "kv_set_request", stream, off, dev, misalign=k), want, f"call {k}")
+    assert codec.decode_redos() == r0  # one key length per tile was right every time
+
+
+@pytest.mark.parametrize("where", ["tile_head", "middle", "last"])
+def test_tile_key_one_odd_key_is_redecoded(codec, dev, decode_impl, where):
+    _pipe_only(decode_impl)
+    n = 30000
+    b = datagen.make_batch(schema="kv_set_request", n=n, lens=(64, 256), seed=42)
+    i = {"tile_head": 64 * 17, "middle": 64 * 200 + 31, "last": n - 1}[where]
+    var = [_odd_key(b, [i], -1 if where != "last" else 5), b.var[1]]
+    stream, off = oracle.encode_batch(b.fixed, var)
+    want = oracle.decode_batch(0, 2, stream, off)
+    r0 = codec.decode_redos()
+    assert_decode_equal(decode_gpu(codec, "kv_set_request", stream, off, dev), want, where)
+    assert codec.decode_redos() == r0 + 1
+    # held: the next calls read every record's own key length (no re-decode), results unchanged
+    assert_decode_equal(decode_gpu(codec, "kv_set_request", stream, off, dev), want, where + " held")
+    assert codec.decode_redos() == r0 + 1
+
+
+def test_tile_key_hold_then_layout_miss_then_impl_reset(codec, dev, decode_impl):
+    """Varying keys: one re-decode, then the tile hold (per-record key lengths, no re-decode); a batch
+    off the generator's layout during it re-decodes too; set_decode_impl clears the holds."""
+    _pipe_only(decode_impl)
+    n = 20000
+    b = datagen.make_batch(schema="kv_set_request", n=n, lens=(("uniform", 0, 80), ("uniform", 0, 300)), seed=43)
+    stream, off = oracle.encode_batch(b.fixed, b.var)
+    want = oracle.decode_batch(0, 2, stream, off)
+    bad, bad_off = _with_trailers(stream, off, [5, 9000], extra=3, seed=4)
+    want_bad = oracle.decode_batch(0, 2, bad, bad_off)
+    r0 = codec.decode_redos()
+    steps = [(False, 1), (False, 1), (False, 1), (True, 2), (False, 2), (False, 2)]
+    for k, (misfit, redos) in enumerate(steps):
+        got = decode_gpu(codec, "kv_set_request", bad if misfit else stream, bad_off if misfit else off, dev)
+        assert_decode_equal(got, want_bad if misfit else want, f"step {k}")
+        assert codec.decode_redos() == r0 + redos, f"step {k}"
+    codec.set_decode_impl(0)  # clears both holds: tile-key speculation again, which misses again
+    assert_decode_equal(decode_gpu(codec, "kv_set_request", stream, off, dev), want, "after reset")
+    assert codec.decode_redos() == r0 + 3
+
+
+def test_tile_key_mixed_batches(codec, dev, decode_impl):
+    """Mixed Get/Set batches: the tile's key length is its first SetRequest's (tiles may start with
+    GetRequests, whose key lengths are never read); fixed keys never re-decode, one odd SetRequest key
+    re-decodes once."""
+    _pipe_only(decode_impl)
+    m = datagen.make_mixed_batch(n=50000, key=64, value=("uniform", 0, 256), set_fraction=datagen.TRACE_SET_FRACTION,
+                                 seed=44)
+    t = torch.from_numpy(m.type).to(dev)
+
+    def run(key):
+        stream, off = oracle.encode_kv_mixed(m.type, key, m.val)
+        _, d = put(stream, dev, 1)
+        _, ro = put(off, dev)
+        out = codec.decode_kv_mixed(d, ro, t)
+        codec.check()
+        wcols, wst = oracle.decode_kv_mixed(stream, off, m.type)
+        np.testing.assert_array_equal(out.status.cpu().numpy()[:m.n], wst)
+        for (gb, go), (wb, wo) in zip(out.var, wcols):
+            go = go.cpu().numpy().view(np.uint64)
+            np.testing.assert_array_equal(go, wo)
+            np.testing.assert_array_equal(gb.cpu().numpy()[:int(wo[-1])], wb)
+
+    r0 = codec.decode_redos()
+    run(m.key)
+    run(m.key)
+    assert codec.decode_redos() == r0
+    sets = np.flatnonzero(m.type != 0)
+    tile = int(sets[500]) // 64
+    first_set = int(sets[np.searchsorted(sets, 64 * tile)])  # the first SetRequest of that tile
+    odd = _odd_key(type("B", (), {"var": [m.key]})(), [first_set], -3)
+    run(odd)
+    assert codec.decode_redos() == r0 + 1

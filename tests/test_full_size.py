@@ -196,3 +196,49 @@ def test_world2_hip_shards(pins, tmp_path):
     want, woff = oracle.encode_batch([], cols)
     assert sha(stream) == sha(want)
     np.testing.assert_array_equal(goff, woff)
+
+
+def test_columns_over_2gib(codec, dev):
+    """A value column and a stream past 2 GiB (2^20 SetRequests with 2100-byte values: 2.2 GB of values,
+    2.3 GB of records): every 64-bit position the kernels move between lanes (prefix words, tile bases,
+    readlane broadcasts) carries bits 31 and up.  Encode against the oracle's digest, decode round trip."""
+    from arpc_amd.codec import to_device
+    kw = dict(schema="kv_set_request", n=1 << 20, lens=(64, 2100), seed=0x5EED0042)
+    b = datagen.make_batch(**kw)
+    assert int(b.var[1][1][-1]) > (1 << 31)
+    fixed, var = to_device(b, dev)
+    enc = codec.encode(b.schema, fixed, var, var_total=b.encoded_size() - b.n * b.schema.overhead)
+    dec = codec.decode(b.schema, enc.data, enc.offsets, caps=[int(o[-1]) for _, o in b.var])
+    codec.check()
+    assert int(dec.status.sum().item()) == 0
+    for f, (bcol, ocol) in enumerate(var):
+        assert torch.equal(dec.var[f][1], ocol - ocol[0]), f"offsets {f}"
+        assert torch.equal(dec.var[f][0][:bcol.numel()], bcol), f"bytes {f}"
+    stream = enc.data[:b.encoded_size()].cpu().numpy()
+    del enc, dec, fixed, var
+    torch.cuda.empty_cache()
+    ws, wo = oracle.encode_batch(b.fixed, b.var)
+    assert sha(stream) == sha(ws)
+
+
+def test_mixed_over_2gib(codec, dev):
+    """The one-launch mixed encode's prefix words and the mixed decode past 2 GiB of stream."""
+    m = datagen.make_mixed_batch(n=1 << 20, key=64, value=4000, set_fraction=0.6, seed=0x5EED0043)
+    assert m.encoded_size() > (1 << 31)
+    t = torch.from_numpy(m.type).to(dev)
+    key = (torch.from_numpy(m.key[0]).to(dev), torch.from_numpy(m.key[1].view(np.int64)).to(dev))
+    val = (torch.from_numpy(m.val[0]).to(dev), torch.from_numpy(m.val[1].view(np.int64)).to(dev))
+    out = codec.encode_kv_mixed(t, key, val, 1, 1, 2, out_bytes=m.encoded_size())
+    dec = codec.decode_kv_mixed(out.data, out.offsets, t)
+    codec.check()
+    assert int(dec.status.sum().item()) == 0
+    for f, (bcol, ocol) in enumerate((key, val)):
+        assert torch.equal(dec.var[f][1], ocol - ocol[0]), f"offsets {f}"
+        assert torch.equal(dec.var[f][0][:bcol.numel()], bcol), f"bytes {f}"
+    stream = out.data[:m.encoded_size()].cpu().numpy()
+    off = out.offsets.cpu().numpy().view(np.uint64)
+    del out, dec, key, val, t
+    torch.cuda.empty_cache()
+    ws, wo = oracle.encode_kv_mixed(m.type, m.key, m.val, 1, 1, 2)
+    np.testing.assert_array_equal(off, wo)
+    assert sha(stream) == sha(ws)

@@ -5,7 +5,7 @@
 set -u
 mkdir -p gpurun_out
 TAG=${TAG:-final}
-LEGS0="--cpu-seconds 0 --host-steps 0 --packetize-reps 0 --proxy-reps 0 --reassembly-reps 0 --crypto-reps 0 --flat-reps 0 --boutique-reps 0 --payload-reps 0 --mixed-reps 0 --config3-reps 0 --trace-reps 0 --per-record 0 --ref-reps 0"
+LEGS0="--cpu-seconds 0 --host-steps 0 --packetize-reps 0 --proxy-reps 0 --reassembly-reps 0 --crypto-reps 0 --flat-reps 0 --boutique-reps 0 --payload-reps 0 --mixed-reps 0 --config3-reps 0 --config4-reps 0 --trace-reps 0 --per-record 0 --ref-reps 0"
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests_$TAG.log 2>&1 \
     || { echo "gpu tests FAILED"; tail -30 gpurun_out/gpu_tests_$TAG.log; exit 1; }
 tail -1 gpurun_out/gpu_tests_$TAG.log

@@ -24,7 +24,7 @@ from arpc_amd.codec import Codec, DecodedBatch  # noqa: E402
 
 
 # timing-only decode variants that give wrong output by design (tools/kbench.py)
-WRONG_OUTPUT = {402, 412, 475, 476, 482, 483, 492, 504, 601, 701, 702, 711, 712, 742}
+WRONG_OUTPUT = {402, 412, 475, 476, 482, 483, 492, 504, 601, 701, 702, 711, 712, 742, 794}
 
 
 def main():

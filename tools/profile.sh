@@ -7,7 +7,7 @@
 # Each pass under its own timeout; stop at the first failure.
 set -u
 OUT=${OUT:-gpurun_out/prof}
-ARGS=${BENCH_ARGS:---steps 10 --warmup 2 --cpu-seconds 0 --host-steps 0 --packetize-reps 0 --proxy-reps 0 --reassembly-reps 0 --crypto-reps 0 --flat-reps 0 --mixed-reps 0 --config3-reps 0 --ref-reps 0 --boutique-reps 0 --payload-reps 0 --trace-reps 0}
+ARGS=${BENCH_ARGS:---steps 10 --warmup 2 --cpu-seconds 0 --host-steps 0 --packetize-reps 0 --proxy-reps 0 --reassembly-reps 0 --crypto-reps 0 --flat-reps 0 --mixed-reps 0 --config3-reps 0 --config4-reps 0 --ref-reps 0 --boutique-reps 0 --payload-reps 0 --trace-reps 0}
 PROG=${PROG:-bench.py}   # e.g. PROG=tools/kbench.py BENCH_ARGS="--enc 0 --dec 0,102 --rounds 3"
 REPO=$(pwd)
 mkdir -p "$OUT"
