@@ -35,7 +35,8 @@
 // waits behind it -- two persistent workers whose streams share a queue serve in turns of their idle
 // timeout (measured: 40 ms per record, DESIGN.md section 4, per-record path).  The worker also hands
 // over to a fresh launch every kLifeTicks (2 ms), busy or idle, so such a launch (a batch of large
-// records, a caller's own kernels) waits at most that long.  Larger records keep the batched path above.  Both give the same bytes and statuses.
+// records, a caller's own kernels) waits at most that long.  Larger records keep the batched path
+// above.  Both give the same bytes and statuses.
 #include <hip/hip_runtime.h>
 
 #include <immintrin.h>
@@ -418,8 +419,21 @@ int ring_ensure_worker(Ring& r, bool waited) {
         if (e != hipSuccess) return hip_fail(e, "sym_batcher: record worker");
         gone = true;
     }
-    while (!gone) {  // announced: it serves what it owes, then leaves
-        _mm_pause();
+    // announced: it serves what it owes, then leaves.  A launch that ended without storing `gone`
+    // (a fault, an abort) must not hang every batcher of the device here: every few thousand spins the
+    // stream is asked whether the launch is over (done: treat it as gone; an error: report it).
+    for (uint64_t i = 0; !gone; ++i) {
+        if (i < 256) {
+            _mm_pause();
+        } else {
+            sched_yield();
+            if ((i & 4095) == 0) {
+                DeviceGuard g(r.device);
+                const hipError_t e = hipStreamQuery(r.stream);
+                if (e == hipSuccess) break;
+                if (e != hipErrorNotReady) return hip_fail(e, "sym_batcher: record worker");
+            }
+        }
         gone = __atomic_load_n(&r.ctl->gone, __ATOMIC_ACQUIRE) == gen;
     }
     r.gen.store(gen + 1, std::memory_order_release);
@@ -454,7 +468,7 @@ int ring_call(sym_batcher* b, int dir, uint64_t in_len, Fill&& fill, Drain&& dra
     int rc = ring_wait(r, &sc->turn, t);
     if (rc != SYM_OK) return rc;
     fill(slot + symhip::kSlotInAt);
-    sc->in_len = in_len | symhip::slot_kind(dir, b->lay, b->bid);
+    sc->in_len = in_len | symhip::slot_tag(t) | symhip::slot_kind(dir, b->lay, b->bid);
     __atomic_store_n(&sc->req, t + 1, __ATOMIC_RELEASE);
     __atomic_fetch_add(&r.ctl->posted[t % symhip::kGroups], 1, __ATOMIC_SEQ_CST);  // then look at quit (hand-shake)
     rc = ring_ensure_worker(r, false);

@@ -116,7 +116,7 @@ __device__ inline u32x4 load_partial(uintptr_t p, int m) {
 __device__ inline void store_bytes(uint8_t* p, u32x4 v, int m) {
     const u32 r[4] = {v.x, v.y, v.z, v.w};
     if (m == 16) {
-        st16((uint8_t*)p, v);
+        st16((uint8_t*)p, v, true);  // nontemporal: the cipher's records are written once
         return;
     }
     for (int t = 0; t < m; ++t) *(g_u8*)(p + t) = chunk_byte(r, t);

@@ -386,11 +386,11 @@ __global__ __launch_bounds__(kThreads) void decode_copy_kernel(DecodeParams p, D
         const i64 hi = min((i64)(P + nb), pick<NV>(lim, second));
         uint8_t* base = (second ? p.bytes[NV - 1] : p.bytes[0]) + pick<NV>(pre, second);
         const bool full = P >= 0 && (i64)P + 16 <= hi;
-        if (full) st16(base + P, v);
+        if (full) st16(base + P, v, true);  // (nontemporal: measured on, DESIGN.md section 4 Stores)
         const bool part = P >= 0 && !full && (i64)P < hi;
         if (__ballot(part)) {
             const u32 rr[4] = {v.x, v.y, v.z, v.w};
-            if (part) store_chunk(base, P, 0, hi, rr);
+            if (part) store_chunk(base, P, 0, hi, rr, true);
         }
     };
 

@@ -168,9 +168,11 @@ __device__ __forceinline__ uint8_t chunk_byte(const u32 r[4], int t) {
 // plain stores, two runs each on one box: headline 4995 -> 5100 GB/s (decode 151 -> 146 us), N3
 // reassembly 2670 -> 2840 GB/s, config 3 / the trace replays / the N5 legs within +-2 %.  The threshold,
 // two runs each: 16 KB loses config 2's 22 KB tiles (headline 5100 -> 4945 GB/s), 64 KB takes config 3's
-// ~53 KB tiles (4590 -> 4525 GB/s).
+// ~53 KB tiles (4590 -> 4525 GB/s).  Every call site passes nt explicitly: the span-gated kernels above,
+// and `true` where the kernel was measured with nontemporal stores at every span (the cipher, the N5
+// copies, the packetizer, the three-kernel decode; round-5 A/B of the libraries, every leg).
 constexpr i64 kNtSpan = 32768;
-__device__ __forceinline__ void st16(uint8_t* p, u32x4 v, bool nt = true) {
+__device__ __forceinline__ void st16(uint8_t* p, u32x4 v, bool nt) {
     if (nt) {
         // the empty asm statements keep the compiler from hoisting or sinking the two stores into
         // one (merged, the store loses its nontemporal flag)
@@ -185,7 +187,7 @@ __device__ __forceinline__ void st16(uint8_t* p, u32x4 v, bool nt = true) {
 // Store a 16-byte chunk at dst (absolute, 16-byte aligned) keeping only the bytes
 // whose position P+t lies in [lo, hi).  Full chunks use one global_store_dwordx4;
 // the partial chunks at a workgroup's range edges fall back to byte stores.
-__device__ __forceinline__ void store_chunk(uint8_t* base, i64 P, i64 lo, i64 hi, const u32 r[4], bool nt = true) {
+__device__ __forceinline__ void store_chunk(uint8_t* base, i64 P, i64 lo, i64 hi, const u32 r[4], bool nt) {
     if (P >= lo && P + 16 <= hi) {
         st16(base + P, u32x4{r[0], r[1], r[2], r[3]}, nt);
     } else {

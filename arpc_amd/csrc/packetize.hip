@@ -297,7 +297,7 @@ __global__ __launch_bounds__(kWaves * 64) void frag_write_kernel(WriteParams p) 
             const int P = B + 16 * 64 * u + 16 * lane;
             if (P >= span) continue;
             const u32 rr[4] = {r[u].x, r[u].y, r[u].z, r[u].w};
-            store_chunk(out_t, P, 0, span, rr);
+            store_chunk(out_t, P, 0, span, rr, true);  // (nontemporal: measured on, DESIGN.md section 4 Stores)
         }
     }
 }

@@ -12,8 +12,9 @@
 //            that it is quitting, see that the next one runs (batcher.cpp); spin until done == t + 1;
 //            copy the result out; turn = t + kRingSlots
 //   worker   poll `posted` (one 8-byte PCIe read) while cold; when it passed the records served -- or
-//            at once while hot (a record within the last 50 us) -- each of the first kWin (128) threads
-//            looks at one slot of the group's window (req and in_len|kind in one round trip)
+//            at once while hot (a record within the last 50 us) -- each of the first kWin threads
+//            (kRingSlots / kGroups = 64) looks at one slot of the group's window (req and
+//            in_len|tag|kind in one round trip; the tag is the ticket's low bits, checked against req)
 //            and the ready ones are served, one wave per record, 16 at once: the record is read into
 //            LDS with system-scope 8-byte loads and encoded or parsed there exactly as MarshalSymphony /
 //            UnmarshalSymphony (kv.syn.go:611-745, echo.syn.go:111-263), each 8-byte word of the result
@@ -266,10 +267,12 @@ __global__ __launch_bounds__(kThreads) void worker_kernel(RingCtl* ctl, uint8_t*
             // req and in_len in one system-coherent 16-byte load (volatile: sc0 sc1, as ld_sys)
             const u64x2 ri = *(const volatile u64x2*)&sc->req;
             const u64 rq = ri.x, il = ri.y;
-            if (S.served[widx(t)] != t + 1 && rq == t + 1) {
+            // (in_len carries the ticket's low bits: a length and kind left by the slot's previous
+            // ticket never pair with this req -- the slot is then simply not ready yet)
+            if (S.served[widx(t)] != t + 1 && rq == t + 1 && (il & 0xffff0000ull) == slot_tag(t)) {
                 const int k = atomicAdd(&S.nlist, 1);
                 S.list[k] = tid;
-                S.len[k] = (u32)min(il & 0xffffffffull, (u64)kRingRecordMax);  // (the caller checked it)
+                S.len[k] = (u32)min(il & kSlotLenMask, (u64)kRingRecordMax);  // (the caller checked it)
                 S.kind[k] = (u32)(il >> 32);
                 const u32 bd = 2 * ((u32)(il >> 56) & 0xffu) + (u32)((il >> 32) & 1);  // batcher, direction
                 atomicOr(&S.bseen[bd >> 5], 1u << (bd & 31));

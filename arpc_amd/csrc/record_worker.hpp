@@ -47,6 +47,12 @@ struct RingCtl {          // one per device, written as commented
 constexpr uint64_t slot_kind(int dir, Layout lay, int bid) {
     return ((uint64_t)dir | ((uint64_t)lay.nfixed << 8) | ((uint64_t)lay.nvar << 16) | ((uint64_t)bid << 24)) << 32;
 }
+// The low half of SlotCtl::in_len: the length (< 2^16, at most kRingRecordMax) in bits 0..15 and the
+// ticket's low 16 bits in bits 16..31.  The worker reads req and in_len with one 16-byte load and
+// takes the slot only when both name the same ticket, so a load that the fabric split into two
+// 8-byte reads cannot pair a new req with the previous ticket's length and kind.
+constexpr uint64_t kSlotLenMask = 0xffff;
+constexpr uint64_t slot_tag(uint64_t ticket) { return (ticket & 0xffff) << 16; }
 
 struct SlotCtl {          // the first 64 bytes of a slot
     uint64_t req;         // caller: ticket + 1 once the in area is written
@@ -57,6 +63,7 @@ struct SlotCtl {          // the first 64 bytes of a slot
     uint64_t pad[4];
 };
 static_assert(offsetof(SlotCtl, in_len) == 8, "req and in_len in one 16-byte load");
+static_assert(kRingRecordMax <= kSlotLenMask, "the length fits below the ticket tag");
 
 struct EncIn {            // encode in area: the record's scalars, then its var fields' bytes back to back
     int32_t fixed[kMaxFixed];

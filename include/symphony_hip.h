@@ -254,7 +254,10 @@ int sym_decode_host(sym_ctx* ctx, int schema, uint64_t n, const uint8_t* h_in, c
  *                           status, as Go returns an error value); a field longer than its cap
  *                           returns SYM_ERR_CAPACITY with the bytes that fit copied.
  * A record larger than max_bytes is SYM_ERR_INVALID.  The caller's memory is read and written only
- * during the call (cgo's pointer rules hold: nothing is kept after return). */
+ * during the call (cgo's pointer rules hold: nothing is kept after return).
+ * At most 256 batchers exist per device and process at once (they share the device's record ring,
+ * which counts each one's passes); sym_batcher_create beyond that returns SYM_ERR_INVALID (the
+ * message says so) until one is destroyed. */
 typedef struct sym_batcher sym_batcher;
 int sym_batcher_create(int device, int schema, uint32_t max_records, uint64_t max_bytes, uint32_t max_wait_us,
                        sym_batcher** out);

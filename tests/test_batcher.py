@@ -130,10 +130,21 @@ def test_python_threads_every_schema(gpu):
         x.join(timeout=120)
     assert not errors, errors[:3]
     st = ser.stats()
-    assert sum(v["encode_records"] for v in st.values()) == 32 * 60
-    # every record was served in some pass; Python threads mostly take turns on the GIL, so passes
-    # shared between them are rare here (test_c_threads_through_batcher asserts the sharing)
-    assert 0 < sum(v["encode_batches"] for v in st.values()) <= 32 * 60
+    # the per-batcher statistics are exact: every schema's batcher counts exactly the records of its
+    # schema, in both directions (thread t's k-th message is of kind (k + t) % 5).  Passes shared between
+    # Python threads are rare (they mostly take turns on the GIL); test_c_threads_through_batcher
+    # asserts the sharing.
+    from arpc_amd.serializer import EchoRequest, GetRequest, GetResponse, SetRequest, SetResponse
+    kinds = [SetRequest, GetRequest, GetResponse, SetResponse, EchoRequest]
+    want = {}
+    for t in range(32):
+        for k in range(60):
+            sid = kinds[(k + t) % 5].SCHEMA.schema_id
+            want[sid] = want.get(sid, 0) + 1
+    assert {sid: v["encode_records"] for sid, v in st.items()} == want
+    assert {sid: v["decode_records"] for sid, v in st.items()} == want
+    for v in st.values():  # a pass serves at least one record
+        assert 1 <= v["encode_batches"] <= v["encode_records"] and 1 <= v["decode_batches"] <= v["decode_records"]
     ser.close()
 
 

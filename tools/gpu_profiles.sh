@@ -6,7 +6,7 @@
 #   decode), trace: the trace-replay mixed batch (tools/mixed_ab.py --trace), crypto: the bench's segment
 #   cipher leg (its encrypt / decrypt kernels; $PMC_CRYPTO adds counter sets for it alone).
 set -o pipefail
-Z="--cpu-seconds 0 --host-steps 0 --packetize-reps 0 --proxy-reps 0 --reassembly-reps 0 --crypto-reps 0 --flat-reps 0 --mixed-reps 0 --config3-reps 0 --ref-reps 0 --boutique-reps 0 --payload-reps 0 --trace-reps 0 --per-record 0"
+Z="--cpu-seconds 0 --host-steps 0 --packetize-reps 0 --proxy-reps 0 --reassembly-reps 0 --crypto-reps 0 --flat-reps 0 --mixed-reps 0 --config3-reps 0 --config4-reps 0 --ref-reps 0 --boutique-reps 0 --payload-reps 0 --trace-reps 0 --per-record 0"
 W=${WHICH:-c2 c3 mixed}
 X=${PMC_EXTRA:-}
 LIB=$(pwd)/arpc_amd/lib/libsymphony_hip.so
