@@ -42,28 +42,47 @@ struct Tables {
 };
 static_assert(sizeof(Tables) % 16 == 0, "Tables is copied to LDS in 16-byte pieces");
 
+// The tables as the cipher reads them, in LDS, laid out against bank conflicts (round 6; round 5's
+// counters: 52 % of the LDS-active cycles were bank conflicts, profiles/r05_counters_summary.txt):
+//  * the T-table in 32 copies interleaved by word, te[x][c]: lane l reads copy l % 32, whose words all
+//    sit in bank l % 32 (ds_read_b32 serves 32 lanes per cycle from banks (a/4) mod 32), so a wave's
+//    random lookups never collide;
+//  * the Shoup tables transposed, gh[key][nibble][power - 1]: the 16 entries of one power share one
+//    group of 4 banks (ds_read_b128: 16 lanes per cycle over 64 banks), and the lanes of a window hash
+//    consecutive powers, so their random nibbles hit different bank groups.
+struct LdsTables {
+    u32 te[256 * 32];
+    u32 rk[2][60];
+    u32 red[16];
+    u32 pad[8];
+    u32x4 gh[2][16][64];
+};
+static_assert(offsetof(LdsTables, gh) % 16 == 0, "16-byte GHASH entries");
+
 __device__ __forceinline__ u32 rotl(u32 x, int s) { return (x << s) | (x >> (32 - s)); }
 __device__ __forceinline__ u32 bswap(u32 x) { return __builtin_bswap32(x); }
 
-// AES-256 encryption of one block (little-endian column words), T-table rounds.
-__device__ inline u32x4 aes_block(const u32* T, const u32* rk, u32x4 in) {
+// AES-256 encryption of one block (little-endian column words), T-table rounds.  T: this lane's copy
+// of the interleaved table (LdsTables::te + lane % 32); entry x is T[32 x].
+__device__ inline u32x4 aes_block(const u32* Tc, const u32* rk, u32x4 in) {
+    auto T = [&](u32 x) { return Tc[x << 5]; };
     u32 w0 = in.x ^ rk[0], w1 = in.y ^ rk[1], w2 = in.z ^ rk[2], w3 = in.w ^ rk[3];
 #pragma unroll
     for (int r = 1; r < 14; ++r) {
-        const u32 t0 = T[w0 & 0xff] ^ rotl(T[(w1 >> 8) & 0xff], 8) ^ rotl(T[(w2 >> 16) & 0xff], 16) ^
-                       rotl(T[w3 >> 24], 24) ^ rk[4 * r];
-        const u32 t1 = T[w1 & 0xff] ^ rotl(T[(w2 >> 8) & 0xff], 8) ^ rotl(T[(w3 >> 16) & 0xff], 16) ^
-                       rotl(T[w0 >> 24], 24) ^ rk[4 * r + 1];
-        const u32 t2 = T[w2 & 0xff] ^ rotl(T[(w3 >> 8) & 0xff], 8) ^ rotl(T[(w0 >> 16) & 0xff], 16) ^
-                       rotl(T[w1 >> 24], 24) ^ rk[4 * r + 2];
-        const u32 t3 = T[w3 & 0xff] ^ rotl(T[(w0 >> 8) & 0xff], 8) ^ rotl(T[(w1 >> 16) & 0xff], 16) ^
-                       rotl(T[w2 >> 24], 24) ^ rk[4 * r + 3];
+        const u32 t0 = T(w0 & 0xff) ^ rotl(T((w1 >> 8) & 0xff), 8) ^ rotl(T((w2 >> 16) & 0xff), 16) ^
+                       rotl(T(w3 >> 24), 24) ^ rk[4 * r];
+        const u32 t1 = T(w1 & 0xff) ^ rotl(T((w2 >> 8) & 0xff), 8) ^ rotl(T((w3 >> 16) & 0xff), 16) ^
+                       rotl(T(w0 >> 24), 24) ^ rk[4 * r + 1];
+        const u32 t2 = T(w2 & 0xff) ^ rotl(T((w3 >> 8) & 0xff), 8) ^ rotl(T((w0 >> 16) & 0xff), 16) ^
+                       rotl(T(w1 >> 24), 24) ^ rk[4 * r + 2];
+        const u32 t3 = T(w3 & 0xff) ^ rotl(T((w0 >> 8) & 0xff), 8) ^ rotl(T((w1 >> 16) & 0xff), 16) ^
+                       rotl(T(w2 >> 24), 24) ^ rk[4 * r + 3];
         w0 = t0;
         w1 = t1;
         w2 = t2;
         w3 = t3;
     }
-    auto S = [&](u32 x) { return (T[x] >> 8) & 0xffu; };
+    auto S = [&](u32 x) { return (T(x) >> 8) & 0xffu; };
     const u32 o0 = S(w0 & 0xff) | (S((w1 >> 8) & 0xff) << 8) | (S((w2 >> 16) & 0xff) << 16) | (S(w3 >> 24) << 24);
     const u32 o1 = S(w1 & 0xff) | (S((w2 >> 8) & 0xff) << 8) | (S((w3 >> 16) & 0xff) << 16) | (S(w0 >> 24) << 24);
     const u32 o2 = S(w2 & 0xff) | (S((w3 >> 8) & 0xff) << 8) | (S((w0 >> 16) & 0xff) << 16) | (S(w1 >> 24) << 24);
@@ -71,7 +90,8 @@ __device__ inline u32x4 aes_block(const u32* T, const u32* rk, u32x4 in) {
     return u32x4{o0 ^ rk[56], o1 ^ rk[57], o2 ^ rk[58], o3 ^ rk[59]};
 }
 
-// x * P in GF(2^128) (GCM bit order; big-endian words), M = the 4-bit table of P.
+// x * P in GF(2^128) (GCM bit order; big-endian words), M = the 4-bit table of P: entry v at M[64 v]
+// (LdsTables::gh[key][.][power - 1]).
 __device__ inline u32x4 gf_mul(u32x4 x, const u32x4* M, const u32* red) {
     u32x4 z = {0, 0, 0, 0};
     const u32 xw[4] = {x.x, x.y, x.z, x.w};
@@ -83,7 +103,7 @@ __device__ inline u32x4 gf_mul(u32x4 x, const u32x4* M, const u32* red) {
         z.z = (z.z >> 4) | (z.y << 28);
         z.y = (z.y >> 4) | (z.x << 28);
         z.x = (z.x >> 4) ^ red[t];
-        z ^= M[nib];
+        z ^= M[nib << 6];
     }
     return z;
 }
@@ -215,11 +235,11 @@ __device__ inline u32x4 subwave_xor_u32x4(u32x4 v) {
 }
 
 template <int W>
-__device__ inline u32x4 ghash_fold(u32x4 y, bool first, bool mine, u32x4 term, u32 cnt, const Tables& T, int key) {
+__device__ inline u32x4 ghash_fold(u32x4 y, bool first, bool mine, u32x4 term, u32 cnt, const LdsTables& T, int key) {
     u32x4 c = mine ? term : u32x4{0, 0, 0, 0};
     c = subwave_xor_u32x4<W>(c);
     if (cnt == 0) return y;
-    return first ? c : (gf_mul(y, T.ghash[key][cnt - 1], T.red) ^ c);
+    return first ? c : (gf_mul(y, &T.gh[key][0][cnt - 1], T.red) ^ c);
 }
 
 // A record's geometry (the lane's own record, loaded one pair ahead).
@@ -261,7 +281,7 @@ __device__ inline Geo lane_geo(const Geo& g, int l) {  // lane l's geometry, wav
 
 // One record on a sub-wave of W lanes (sl = lane within it).  W = 32 packs two records per wave.
 template <bool ENC, int W>
-__device__ void seal_or_open(const Args& a, const Tables& T, const u32* ts, u64 r, const Geo& G, int sl) {
+__device__ void seal_or_open(const Args& a, const LdsTables& T, const u32* ts, u64 r, const Geo& G, int sl) {
     const u64 L = G.L, o = G.o;
     const uintptr_t d = (uintptr_t)(a.in + G.s);
     uint8_t* const q = a.out + G.oo;
@@ -333,7 +353,7 @@ __device__ void seal_or_open(const Args& a, const Tables& T, const u32* ts, u64 
         const u32x4 X = is_len ? u32x4{0, 0, (u32)(bits >> 32), (u32)bits} : to_be(c);
         const u32 e = min(is_priv ? ns : nsp, w0 + W);
         u32x4 term = {0, 0, 0, 0};
-        if (act) term = gf_mul(X, T.ghash[is_priv ? 1 : 0][e - g - 1], T.red);
+        if (act) term = gf_mul(X, &T.gh[is_priv ? 1 : 0][0][e - g - 1], T.red);
         if (is_len) term ^= to_be(ks);
         const u32 cnt_pub = w0 < nsp ? min(nsp, w0 + W) - w0 : 0;
         y_pub = ghash_fold<W>(y_pub, w0 == 0, act && !is_priv, term, cnt_pub, T, 0);
@@ -345,17 +365,25 @@ __device__ void seal_or_open(const Args& a, const Tables& T, const u32* ts, u64 
     if (!ENC) version = (u32)__shfl((int)version, (int)(nsp & (W - 1)), W);  // the lane of private slot 0
     const u32x4 tag_pub = to_be(y_pub), tag_priv = to_be(y_priv);  // little-endian words
     if (ENC) {
-        if (sl == 0) {  // header (offsetToPrivate patched), nonces, tags
-            for (int t = 0; t < 13; ++t) q[t] = ld_u8(d + t);
-            const u32 no = (u32)(13 + 28 + np);
-            for (int t = 0; t < 4; ++t) q[1 + t] = (uint8_t)(no >> (8 * t));
-            for (int t = 0; t < 12; ++t) q[13 + t] = ld_u8(non_pub + t);
+        // header (offsetToPrivate patched) and nonces: 37 bytes, one per lane of the sub-wave (lanes
+        // 0..4 take a second when W = 32), every load issued before any store -- byte copies by one
+        // lane are a chain of round trips (a store may alias the next load), and were most of the
+        // cipher's time (round 6: 2.1 -> see DESIGN.md section 4)
+        const u32 no = (u32)(13 + 28 + np);
+        auto src = [&](int t) -> uintptr_t {  // 0: a patched byte (no load)
+            return t < 13 ? (t >= 1 && t <= 4 ? 0 : d + t) : t < 25 ? non_pub + (t - 13) : non_priv + (t - 25);
+        };
+        auto dst = [&](int t) -> uint8_t* { return t < 25 ? q + t : q + 41 + np + (t - 25); };
+        const int t0 = sl, t1 = sl + W, nt = priv ? 37 : 25;
+        const uintptr_t a0 = t0 < nt ? src(t0) : 0, a1 = t1 < nt ? src(t1) : 0;
+        auto patched = [&](int t) { return t >= 1 && t <= 4 ? (no >> (8 * (t - 1))) & 0xffu : 0u; };
+        const u32 b0 = a0 ? ld_u8(a0) : patched(t0);
+        const u32 b1 = a1 ? ld_u8(a1) : patched(t1);
+        if (t0 < nt) *dst(t0) = (uint8_t)b0;
+        if (t1 < nt) *dst(t1) = (uint8_t)b1;
+        if (sl == 0) {  // tags
             store_bytes(q + 25 + np, tag_pub, 16);
-            if (priv) {
-                uint8_t* p2 = q + 41 + np;
-                for (int t = 0; t < 12; ++t) p2[t] = ld_u8(non_priv + t);
-                store_bytes(p2 + 12 + nv, tag_priv, 16);
-            }
+            if (priv) store_bytes(q + 41 + np + 12 + nv, tag_priv, 16);
         }
         return;
     }
@@ -387,10 +415,9 @@ __device__ void seal_or_open(const Args& a, const Tables& T, const u32* ts, u64 
         const u32x4 ks = aes_block(ts, T.rk[is_priv ? 1 : 0], counter_block(is_priv ? nonce_priv : nonce_pub, b + 2));
         store_bytes((is_priv ? dst_priv : dst_pub) + 16 * (u64)b, x ^ ks, m);
     }
-    if (sl == 0) {
-        for (int t = 0; t < 13; ++t) q[t] = ld_u8(d + t);
+    if (sl < 13) {  // the header, offsetToPrivate patched: one byte per lane (see ENC above)
         const u32 no = (u32)(13 + np);
-        for (int t = 0; t < 4; ++t) q[1 + t] = (uint8_t)(no >> (8 * t));
+        q[sl] = sl >= 1 && sl <= 4 ? (uint8_t)(no >> (8 * (sl - 1))) : (uint8_t)ld_u8(d + sl);
     }
 }
 
@@ -398,15 +425,35 @@ __device__ void seal_or_open(const Args& a, const Tables& T, const u32* ts, u64 
 // of the wave seals one of them; otherwise the whole wave takes them one after the other.
 template <bool ENC>
 __global__ __launch_bounds__(kWaves * 64) void cipher_kernel(Args a) {
-    __shared__ Tables T;
-    {  // stage the tables (34 KiB) once per workgroup; the grid is persistent
-        const u32x4* src = (const u32x4*)a.tables;
-        u32x4* dst = (u32x4*)&T;
-        for (int k = threadIdx.x; k < (int)(sizeof(Tables) / 16); k += kWaves * 64) dst[k] = src[k];
+    __shared__ LdsTables T;
+    {  // stage the tables (65 KiB in LdsTables' layout) once per workgroup; the grid is persistent
+        // (every thread's loads issued before its LDS stores: one round trip, not one per entry)
+        const Tables& g = *a.tables;
+        const int tid = threadIdx.x;
+        static_assert(kWaves * 64 == 512, "staging assumes 512 threads");
+        if (tid < 256) {  // T-table entry tid -> its 32 copies
+            const u32 v = g.te0[tid];
+#pragma unroll
+            for (int c = 0; c < 32; ++c) T.te[32 * tid + c] = v;
+        } else {  // GHASH entries 8 (tid - 256) .. +7, transposed
+            u32x4 v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int k = 8 * (tid - 256) + j;
+                v[j] = g.ghash[k >> 10][k & 63][(k >> 6) & 15];
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int k = 8 * (tid - 256) + j;
+                T.gh[k >> 10][(k >> 6) & 15][k & 63] = v[j];
+            }
+        }
+        if (tid < 2 * 60) T.rk[tid / 60][tid % 60] = g.rk[tid / 60][tid % 60];
+        if (tid >= 128 && tid < 144) T.red[tid - 128] = g.red[tid - 128];
     }
     __syncthreads();
     const int lane = threadIdx.x & 63;
-    const u32* ts = T.te0;
+    const u32* ts = T.te + (lane & 31);  // this lane's copy of the T-table
     const u64 nw = (u64)gridDim.x * kWaves;
     const u64 npairs = (a.n + 1) / 2;
     // lanes 0..31 hold the pair's first record's geometry, 32..63 the second's; the next pair's is
@@ -586,7 +633,7 @@ hipError_t launch_crypt(bool enc, const uint8_t* in, const u64* rec_off, u64 n, 
     if ((e = hipGetLastError()) != hipSuccess) return e;
     crypt::Args a{in, rec_off, n, nonces, out_off, status, out, (const crypt::Tables*)d_tables, desc};
     const u64 want = (n + crypt::kWaves - 1) / crypt::kWaves;
-    const u64 cap = (u64)num_cus * 4;
+    const u64 cap = (u64)num_cus * 2;  // resident: 66 KB of LDS tables per workgroup, two per CU
     const unsigned grid = (unsigned)(want < cap ? want : cap);
     if (enc) hipLaunchKernelGGL(crypt::cipher_kernel<true>, dim3(grid), dim3(crypt::kWaves * 64), 0, stream, a);
     else hipLaunchKernelGGL(crypt::cipher_kernel<false>, dim3(grid), dim3(crypt::kWaves * 64), 0, stream, a);
