@@ -1039,6 +1039,13 @@ hipError_t launch_decode_pipe(const DecodeParams& p, void* flags, unsigned epoch
         case 792: return launch_layout<PipeCfg{.sk = 1, .spec = true, .loc = true, .canon = true, .tilek = true}>(p, fl, epoch, stream, 1, 2);
         case 793: return launch_layout<PipeCfg{.sk = 1, .stg = 16384, .spec = true, .wpe = 8, .tilek = true}>(p, fl, epoch, stream, 1, 2);
         case 794: return launch_layout<PipeCfg{.mode = 1, .sk = 1, .loc = true, .canon = true}>(p, fl, epoch, stream, 1, 2);
+        // round 6, the mixed batch with tile-key parsers: parsers on 1/4, 3/8 of the CUs; the header-image
+        // check; with ballot-located chunks; config 2's geometry (22.5 KB stage, 6 waves)
+        case 795: return launch_layout<PipeCfg{.sk = 1, .stg = 16384, .spec = true, .wpe = 8, .tilek = true}>(p, fl, epoch, stream, 1, 4);
+        case 796: return launch_layout<PipeCfg{.sk = 1, .stg = 16384, .spec = true, .wpe = 8, .tilek = true}>(p, fl, epoch, stream, 3, 8);
+        case 797: return launch_layout<PipeCfg{.sk = 1, .stg = 16384, .spec = true, .wpe = 8, .canon = true, .tilek = true}>(p, fl, epoch, stream, 1, 2);
+        case 798: return launch_layout<PipeCfg{.sk = 1, .stg = 16384, .spec = true, .wpe = 8, .loc = true, .canon = true, .tilek = true}>(p, fl, epoch, stream, 1, 2);
+        case 799: return launch_layout<PipeCfg{.sk = 1, .spec = true, .loc = true, .canon = true, .tilek = true}>(p, fl, epoch, stream, 1, 2);
         default: break;
     }
 #endif
