@@ -1105,7 +1105,7 @@ def main():
                     help="online-boutique reference payloads leg (all 30 types) repetitions (0 = skip)")
     ap.add_argument("--mixed-reps", type=int, default=10, help="mixed Get/Set leg repetitions (0 = skip)")
     ap.add_argument("--config3-reps", type=int, default=6, help="config 3 leg repetitions (0 = skip)")
-    ap.add_argument("--config4-reps", type=int, default=4,
+    ap.add_argument("--config4-reps", type=int, default=8,
                     help="config 4 shard leg (2^23 records on this GPU) repetitions at N=1 (0 = skip)")
     ap.add_argument("--trace-reps", type=int, default=3,
                     help="trace-replay legs (config 3 trace sizes, Get/Set trace sequence) repetitions (0 = skip)")
