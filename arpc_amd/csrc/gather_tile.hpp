@@ -22,6 +22,66 @@ __device__ __forceinline__ u64 readlane_u64(u64 v, int l) {
     return (u64)(u32)__builtin_amdgcn_readlane((u32)v, l) | ((u64)(u32)__builtin_amdgcn_readlane((u32)(v >> 32), l) << 32);
 }
 
+// ---- two-level tile prefixes without a scan launch (round 6): the kernel that produces the tiles'
+// totals also adds each one into the total of its group of kSuperTiles tiles (agent-scope atomics into
+// Pairs zeroed before the call, one 128-byte line per group: with 256-tile groups packed into a few
+// lines the atomics of thousands of workgroups serialised on them, +55 us per launch); a consumer of
+// tile b then sums, in one workgroup reduction, the totals of the groups before b's and of the tiles
+// before b inside its group.  Saves the single-workgroup scan launch (~9 us of launch boundaries)
+// between producer and consumer.  (Not used by the gather itself: inside gather_tile the prefix code
+// cost 10-18 VGPRs, a wave per SIMD, more than the launch it saves.)
+constexpr u64 kSuperTiles = 64;
+constexpr u64 kSuperStride = 8;  // Pairs per group total: one 128-byte line each
+__host__ __device__ inline u64 super_bytes(u64 ntiles) { return ((ntiles + kSuperTiles - 1) / kSuperTiles + 1) * kSuperStride * 16; }
+__device__ __forceinline__ void publish_tile_total(Pair* agg, Pair* super, u64 tile, Pair t) {
+    agg[tile] = t;
+    Pair* g = super + (tile / kSuperTiles) * kSuperStride;
+    if (t.bytes) atomicAdd((unsigned long long*)&g->bytes, (unsigned long long)t.bytes);
+    if (t.count) atomicAdd((unsigned long long*)&g->count, (unsigned long long)t.count);
+}
+// Whole workgroup of 256 threads (every thread calls it): tile's exclusive prefix; the grand total of the
+// ntiles tiles into *total when given.
+__device__ inline Pair tile_prefix_2l(const Pair* agg, const Pair* super, u64 tile, u64 ntiles, Pair* total = nullptr) {
+    __shared__ u64 rb[4], rc[4], sb[4], sc[4];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const u64 g = tile / kSuperTiles, r = tile % kSuperTiles, nsup = (ntiles + kSuperTiles - 1) / kSuperTiles;
+    u64 b = 0, c = 0, tb = 0, tc = 0;
+    if ((u64)threadIdx.x < r) {
+        const Pair v = agg[g * kSuperTiles + threadIdx.x];
+        b = v.bytes;
+        c = v.count;
+    }
+    for (u64 j = threadIdx.x; j < nsup; j += 256) {
+        const Pair v = super[j * kSuperStride];
+        if (j < g) {
+            b += v.bytes;
+            c += v.count;
+        }
+        tb += v.bytes;
+        tc += v.count;
+    }
+    b = wave_sum_u64(b);
+    c = wave_sum_u64(c);
+    if (total) {
+        tb = wave_sum_u64(tb);
+        tc = wave_sum_u64(tc);
+    }
+    if (lane == 0) {
+        rb[wave] = b;
+        rc[wave] = c;
+        sb[wave] = tb;
+        sc[wave] = tc;
+    }
+    __syncthreads();
+    // (wave-uniform, and made provably so: the callers' arithmetic on them stays scalar, as it is on a
+    // prefix loaded from a scan's output)
+    const Pair out{(u64)uniform_i64((i64)(rb[0] + rb[1] + rb[2] + rb[3])), (u64)uniform_i64((i64)(rc[0] + rc[1] + rc[2] + rc[3]))};
+    if (total)
+        *total = Pair{(u64)uniform_i64((i64)(sb[0] + sb[1] + sb[2] + sb[3])), (u64)uniform_i64((i64)(sc[0] + sc[1] + sc[2] + sc[3]))};
+    __syncthreads();  // rb.. are rewritten by the next call
+    return out;
+}
+
 // One 256-segment tile (a workgroup loop body of gather_kernel, or of flat.hip's dec_emit_kernel).
 // pre[ntiles] is the total: a scan over the capacity's tiles has it there too, at the exclusive
 // prefix of the first empty tile.
@@ -51,11 +111,11 @@ __device__ __forceinline__ void gather_tile(const GatherArgs& a, u64 tile, u64 n
     }
     __syncthreads();  // the only workgroup barrier
     const Pair total = a.pre[ntiles];
+    const Pair tp = a.pre[tile];
     if (total.bytes > a.cap) {  // output does not fit: nothing is written (uniform)
         if (i == 0) atomicOr(a.err, kErrCapacity);
         return;
     }
-    const Pair tp = a.pre[tile];
     u64 wb = tp.bytes, wc = tp.count;
     for (int q = 0; q < wave; ++q) {
         wb += wsum_b[q];

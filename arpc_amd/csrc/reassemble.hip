@@ -32,6 +32,7 @@
 #include "../../include/symphony_hip.h"
 #include "codec.hpp"
 #include "device_util.hpp"
+#include "gather_tile.hpp"
 
 #include <algorithm>
 
@@ -88,6 +89,8 @@ struct Args {
     uint8_t* status;
     Pair* cnt;             // per arrival (n+1): (message bytes, segments << 32 | messages)
     Pair* agg;             // its tile totals (simple batches: written by parse_kernel)
+    Pair* super_p;         // their two-level group totals (gather_tile.hpp publish_tile_total): the parse's
+    Pair* super_c;         // and the general path's (group pass 0's triples)
     const Pair* pre;       // its exclusive scan
     u64* msg_off;
     u64* msg_rpc;
@@ -101,28 +104,21 @@ __device__ inline void block_scan_pair(Pair v, Pair& excl, Pair& tile_total);
 // The general path's kernels run only when the parse flagged the batch as not simple (uniform).
 __device__ __forceinline__ bool gated_off(const unsigned* gate) { return *gate == 0; }
 
-// ---- 1a'. the hash table and first-arrival slots set to "empty" (general path only)
-__global__ __launch_bounds__(256) void init_kernel(u64* table, u32* first, u64 ts, const unsigned* gate) {
-    if (gated_off(gate)) return;
+// ---- 1a'. the hash table and first-arrival slots set to "empty" (general path, RPCIDs out of order)
+__global__ __launch_bounds__(256) void init_kernel(u64* table, u32* first, u64 ts, const unsigned* gate,
+                                                   const unsigned* nonmono) {
+    if (gated_off(gate) || gated_off(nonmono)) return;
     for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; i <= ts; i += (u64)gridDim.x * 256) {
         if (i < ts) table[i] = kEmpty;
         first[i] = ~0u;
     }
 }
 
-// ---- 1. When every datagram is a DataPacket and the RPCIDs never decrease, each RPCID's datagrams
-// form one contiguous run, so its group is that run and its first arrival the run's head: the hash
-// table (and the sort, the keys being in order) is not needed.  This kernel finds out; the hash
-// and key kernels branch on its word (the packetizer's send order and one client's increasing
-// RPCIDs are this case).
-__global__ __launch_bounds__(256) void order_kernel(Args a, const unsigned* gate, unsigned* nonmono) {
-    if (gated_off(gate)) return;
-    const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
-    bool bad = false;
-    if (i < a.n)
-        bad = a.status[i] != SYM_RX_PENDING || (i > 0 && (a.status[i - 1] != SYM_RX_PENDING || a.rpc[i] < a.rpc[i - 1]));
-    if (__syncthreads_or(bad) && threadIdx.x == 0) atomicOr(nonmono, 1u);
-}
+// When every datagram is a DataPacket and the RPCIDs never decrease, each RPCID's datagrams form one
+// contiguous run, so its group is that run and its first arrival the run's head: the hash table (and
+// the sort, the keys being in order) is not needed.  The parse finds out (round 6: before, a launch of
+// its own); the hash and key kernels branch on its word (the packetizer's send order and one client's
+// increasing RPCIDs are this case).
 
 // ---- 2. stable LSD radix sort of (key, value) u32 pairs, 8 key bits per pass, 2048 pairs a tile.
 // A pass: per-tile digit counts (digit-major, so a row scan per digit gives every tile its offset
@@ -149,13 +145,11 @@ __device__ __forceinline__ u32 rank_below(u64 m) {
     return __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u));
 }
 
-__global__ __launch_bounds__(256) void sort_hist_kernel(const u32* keys, u64 n, int shift, u32* hist, u64 ntiles,
-                                                        const unsigned* gate) {
-    if (gated_off(gate)) return;
+__device__ __forceinline__ void sort_hist_tile(const u32* keys, u64 n, int shift, u32* hist, u64 ntiles, u64 tile) {
     __shared__ u32 h[kDigits];
     h[threadIdx.x] = 0;
     __syncthreads();
-    const u64 base = (u64)blockIdx.x * kSortTile;
+    const u64 base = tile * kSortTile;
     for (int k = 0; k < kSortTile / 256; ++k) {
         const u64 j = base + (u64)k * 256 + threadIdx.x;
         const bool valid = j < n;
@@ -164,7 +158,13 @@ __global__ __launch_bounds__(256) void sort_hist_kernel(const u32* keys, u64 n, 
         if (valid && rank_below(m) == 0) atomicAdd(&h[d], (u32)__popcll(m));  // one add per digit and wave
     }
     __syncthreads();
-    hist[(u64)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
+    hist[(u64)threadIdx.x * ntiles + tile] = h[threadIdx.x];
+}
+
+__global__ __launch_bounds__(256) void sort_hist_kernel(const u32* keys, u64 n, int shift, u32* hist, u64 ntiles,
+                                                        const unsigned* gate) {
+    if (gated_off(gate)) return;
+    sort_hist_tile(keys, n, shift, hist, ntiles, blockIdx.x);
 }
 
 // block-wide exclusive scan of one u32 per thread (256 threads)
@@ -181,9 +181,8 @@ __device__ __forceinline__ u32 block_excl_u32(u32 v, u32& total) {
     return pre + inc - v;
 }
 
-__global__ __launch_bounds__(256) void sort_rowscan_kernel(u32* hist, u64 ntiles, u32* rowtot, const unsigned* gate) {
-    if (gated_off(gate)) return;
-    u32* row = hist + (u64)blockIdx.x * ntiles;
+__device__ __forceinline__ void sort_rowscan_row(u32* hist, u64 ntiles, u32* rowtot, int digit) {
+    u32* row = hist + (u64)digit * ntiles;
     u32 carry = 0;
     for (u64 b = 0; b < ntiles; b += 256) {  // uniform loop
         const u64 i = b + threadIdx.x;
@@ -193,24 +192,27 @@ __global__ __launch_bounds__(256) void sort_rowscan_kernel(u32* hist, u64 ntiles
         if (i < ntiles) row[i] = carry + ex;
         carry += tot;
     }
-    if (threadIdx.x == 0) rowtot[blockIdx.x] = carry;
+    if (threadIdx.x == 0) rowtot[digit] = carry;
 }
 
-__global__ __launch_bounds__(256) void sort_scatter_kernel(const u32* kin, const u32* vin, u32* kout, u32* vout, u64 n,
-                                                           int shift, const u32* hist, u64 ntiles, const u32* rowtot,
-                                                           const unsigned* gate) {
+__global__ __launch_bounds__(256) void sort_rowscan_kernel(u32* hist, u64 ntiles, u32* rowtot, const unsigned* gate) {
     if (gated_off(gate)) return;
+    sort_rowscan_row(hist, ntiles, rowtot, blockIdx.x);
+}
+
+__device__ __forceinline__ void sort_scatter_tile(const u32* kin, const u32* vin, u32* kout, u32* vout, u64 n, int shift,
+                                                  const u32* hist, u64 ntiles, const u32* rowtot, u64 tile) {
     __shared__ u32 cnt[4][kDigits];  // per wave: running count of each digit, then its output base
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     u32 tot;
     const u32 dstart = block_excl_u32(rowtot[threadIdx.x], tot);  // the digit's first output position
-    const u32 tbase = dstart + hist[(u64)threadIdx.x * ntiles + blockIdx.x];
+    const u32 tbase = dstart + hist[(u64)threadIdx.x * ntiles + tile];
 #pragma unroll
     for (int w = 0; w < 4; ++w) cnt[w][threadIdx.x] = 0;
     __syncthreads();
     constexpr int kSteps = kSortWaveItems / 64;
     u32 key[kSteps], val[kSteps], pos[kSteps];
-    const u64 base = (u64)blockIdx.x * kSortTile + (u64)wave * kSortWaveItems;
+    const u64 base = tile * kSortTile + (u64)wave * kSortWaveItems;
 #pragma unroll
     for (int k = 0; k < kSteps; ++k) {
         const u64 j = base + (u64)k * 64 + lane;
@@ -250,21 +252,96 @@ __global__ __launch_bounds__(256) void sort_scatter_kernel(const u32* kin, const
     }
 }
 
+__global__ __launch_bounds__(256) void sort_scatter_kernel(const u32* kin, const u32* vin, u32* kout, u32* vout, u64 n,
+                                                           int shift, const u32* hist, u64 ntiles, const u32* rowtot,
+                                                           const unsigned* gate) {
+    if (gated_off(gate)) return;
+    sort_scatter_tile(kin, vin, kout, vout, n, shift, hist, ntiles, rowtot, blockIdx.x);
+}
+
+// The whole sort in ONE launch (round 6): the passes' phases (tile counts, row scans, scatter) are
+// separated by a software grid barrier instead of launch boundaries, so a batch whose keys are in
+// order already -- an in-order stream, the common case -- pays one gated launch, not nine (~5 us
+// each).  The grid is at most one workgroup per CU, so all of it becomes resident; a barrier that
+// still has not filled after kBarrierTicks (another stream's kernels holding the CUs that long) gives
+// up with kErrTimeout (SYM_ERR_DEVICE from sym_ctx_check), so the launch always ends.
+constexpr u64 kBarrierTicks = 50000000;  // 500 ms of s_memrealtime (100 MHz)
+struct SortArgs {
+    u32* kb[2];
+    u32* vb[2];
+    u64 n;
+    u32* hist;
+    u64 ntiles;
+    u32* rowtot;
+    const unsigned* unsorted;
+    unsigned* bar;  // arrivals, zeroed per call
+    unsigned* err;
+    unsigned bits;
+};
+__device__ __forceinline__ bool grid_barrier(unsigned* bar, unsigned target, unsigned* err) {
+    __threadfence();  // every wave's stores of the phase, released at agent scope
+    __syncthreads();
+    __shared__ int ok;
+    if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        const u64 t0 = __builtin_amdgcn_s_memrealtime();
+        int good = 1;
+        while (__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            __builtin_amdgcn_s_sleep(1);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > kBarrierTicks) {
+                atomicOr(err, kErrTimeout);
+                good = 0;
+                break;
+            }
+        }
+        ok = good;
+    }
+    __syncthreads();
+    __threadfence();  // acquire: the other workgroups' stores
+    return ok != 0;
+}
+__global__ __launch_bounds__(256) void sort_all_kernel(SortArgs s) {
+    if (gated_off(s.unsorted)) return;  // uniform: every workgroup leaves at once
+    const u64 G = gridDim.x;
+    unsigned arrivals = 0;
+    int cur = 0;
+    for (unsigned shift = 0; shift < s.bits; shift += 8, cur ^= 1) {
+        for (u64 t = blockIdx.x; t < s.ntiles; t += G) {
+            sort_hist_tile(s.kb[cur], s.n, (int)shift, s.hist, s.ntiles, t);
+            __syncthreads();  // the tile's LDS counts are reset by the next tile
+        }
+        if (!grid_barrier(s.bar, arrivals += (unsigned)G, s.err)) return;
+        for (u64 d = blockIdx.x; d < kDigits; d += G) sort_rowscan_row(s.hist, s.ntiles, s.rowtot, (int)d);
+        if (!grid_barrier(s.bar, arrivals += (unsigned)G, s.err)) return;
+        for (u64 t = blockIdx.x; t < s.ntiles; t += G) {
+            sort_scatter_tile(s.kb[cur], s.vb[cur], s.kb[cur ^ 1], s.vb[cur ^ 1], s.n, (int)shift, s.hist, s.ntiles,
+                              s.rowtot, t);
+            __syncthreads();
+        }
+        if (shift + 8 < s.bits && !grid_barrier(s.bar, arrivals += (unsigned)G, s.err)) return;
+    }
+}
+
 // ---- 1. parse (transport.go:266-283, builtin_packets.go:118-161): status, RPCID, meta, payload
 // length, and whether the batch is "simple" -- every DataPacket a whole message in one datagram
 // (TotalPackets 1, sequence 0, fragment 0, last).  Then each DataPacket completes its own message on
 // arrival whatever else the batch holds (no RPCID ever keeps state), so the messages are the
 // DataPackets in arrival order: cnt[i] = (payload bytes, one segment, one message) is already the
 // per-arrival triple the general path computes.
-__global__ __launch_bounds__(256) void parse_kernel(Args a, unsigned* complex_flag) {
-    const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
-    Pair c = {0, 0};  // entries past the datagrams (entry n included) are zero
-    bool simple = true;
-    if (i < a.n) {
+// One datagram's header (the parse below): status, RPCID, meta and payload length (the last three
+// only for a pending DataPacket).
+struct Parsed {
+    uint8_t st;
+    u32 pl;
+    u64 r, m;
+};
+__device__ __forceinline__ Parsed parse_one(const Args& a, u64 i) {
+    Parsed q{SYM_RX_PENDING, 0, 0, 0};
+    {
         const u64 s = a.dg_off[i], L = a.dg_off[i + 1] - s;
         const uintptr_t p = (uintptr_t)(a.wire + s);
-        uint8_t st = SYM_RX_PENDING;
-        u32 pl = 0;
+        uint8_t& st = q.st;
+        u32& pl = q.pl;
         if (L >= kHdr && s + 32 <= a.dg_off[a.n]) {
             // the whole header in two byte-unaligned 16-byte loads, issued together (the common case)
             const u32x4 w0 = ld16u(p), w1 = ld16u(p + 16);
@@ -279,13 +356,9 @@ __global__ __launch_bounds__(256) void parse_kernel(Args a, unsigned* complex_fl
             } else if (L < (u64)kHdr + pl) {
                 st = SYM_RX_BAD_LENGTH;                  // "too short for declared payload length"
             } else {
-                const u64 r = (u64)u32_at(1) | ((u64)u32_at(5) << 32);
-                const u64 m = (u64)(u32_at(11) & 0xffff) | ((u64)(u32_at(9) & 0xffff) << 16) |
-                              ((u64)(((w[3] >> 8) & 0xff) != 0) << 32) | ((u64)((w[3] >> 16) & 0xff) << 40);
-                a.rpc[i] = r;
-                a.meta[i] = m;
-                a.plen[i] = pl;
-                simple = m_total(m) == 1 && m_seq(m) == 0 && m_fidx(m) == 0 && !m_more(m);
+                q.r = (u64)u32_at(1) | ((u64)u32_at(5) << 32);
+                q.m = (u64)(u32_at(11) & 0xffff) | ((u64)(u32_at(9) & 0xffff) << 16) |
+                      ((u64)(((w[3] >> 8) & 0xff) != 0) << 32) | ((u64)((w[3] >> 16) & 0xff) << 40);
             }
         } else if (L < 1) {
             st = SYM_RX_TOO_SHORT;                       // "data too short to read packet type"
@@ -298,19 +371,57 @@ __global__ __launch_bounds__(256) void parse_kernel(Args a, unsigned* complex_fl
             if (L < (u64)kHdr + pl) {
                 st = SYM_RX_BAD_LENGTH;
             } else {
-                const u64 r = (u64)ld_u32(p + 1) | ((u64)ld_u32(p + 5) << 32);
-                const u64 m = (u64)(ld_u32(p + 11) & 0xffff) | ((u64)(ld_u32(p + 9) & 0xffff) << 16) |
-                              ((u64)(ld_u8(p + 13) != 0) << 32) | ((u64)ld_u8(p + 14) << 40);
-                a.rpc[i] = r;
-                a.meta[i] = m;
-                a.plen[i] = pl;
-                simple = m_total(m) == 1 && m_seq(m) == 0 && m_fidx(m) == 0 && !m_more(m);
+                q.r = (u64)ld_u32(p + 1) | ((u64)ld_u32(p + 5) << 32);
+                q.m = (u64)(ld_u32(p + 11) & 0xffff) | ((u64)(ld_u32(p + 9) & 0xffff) << 16) |
+                      ((u64)(ld_u8(p + 13) != 0) << 32) | ((u64)ld_u8(p + 14) << 40);
             }
         }
-        a.status[i] = st;
-        if (st == SYM_RX_PENDING) c = Pair{pl, ((u64)1 << 32) | 1u};
+    }
+    return q;
+}
+
+__global__ __launch_bounds__(256) void parse_kernel(Args a, unsigned* complex_flag) {
+    __shared__ u64 s_rpc[256];
+    __shared__ uint8_t s_ok[256];
+    const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
+    Pair c = {0, 0};  // entries past the datagrams (entry n included) are zero
+    bool simple = true, pend = false;
+    u64 r = 0;
+    if (i < a.n) {
+        const Parsed q = parse_one(a, i);
+        pend = q.st == SYM_RX_PENDING;
+        if (pend) {
+            r = q.r;
+            a.rpc[i] = q.r;
+            a.meta[i] = q.m;
+            a.plen[i] = q.pl;
+            simple = m_total(q.m) == 1 && m_seq(q.m) == 0 && m_fidx(q.m) == 0 && !m_more(q.m);
+            c = Pair{q.pl, ((u64)1 << 32) | 1u};
+        }
+        a.status[i] = q.st;
     }
     if (i <= a.n) a.cnt[i] = c;
+    // RPCID order (the general path's nonmono word): every datagram a pending DataPacket, RPCIDs never
+    // decreasing; the workgroup's first datagram compares with the previous one, parsed again here
+    s_rpc[threadIdx.x] = r;
+    s_ok[threadIdx.x] = pend;
+    __syncthreads();
+    bool bad = false;
+    if (i < a.n) {
+        bool pp = true;
+        u64 pr = 0;
+        if (threadIdx.x > 0) {
+            pp = s_ok[threadIdx.x - 1] != 0;
+            pr = s_rpc[threadIdx.x - 1];
+        } else if (i > 0) {
+            const Parsed q = parse_one(a, i - 1);
+            pp = q.st == SYM_RX_PENDING;
+            pr = q.r;
+        }
+        bad = !pend || (i > 0 && (!pp || r < pr));
+    }
+    if (__syncthreads_or(bad) && threadIdx.x == 0 && __hip_atomic_load(a.nonmono, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+        atomicOr((unsigned*)a.nonmono, 1u);
     // one flag check per workgroup, and the atomic only while the flag is still clear: a wave-level
     // atomicOr on one word serialised ~20k atomics per batch of multi-datagram messages (~200 us)
     if (__syncthreads_or(!simple) && threadIdx.x == 0 &&
@@ -318,7 +429,7 @@ __global__ __launch_bounds__(256) void parse_kernel(Args a, unsigned* complex_fl
         atomicOr(complex_flag, 1u);
     Pair e, t;  // this tile's totals, for the scan of the triples (simple batches)
     block_scan_pair(c, e, t);
-    if (threadIdx.x == 0) a.agg[blockIdx.x] = t;
+    if (threadIdx.x == 0) raw::publish_tile_total(a.agg, a.super_p, blockIdx.x, t);
 }
 
 // ---- 1a. general path: the RPCID into an open-addressing hash table (agent-scope CAS) that
@@ -355,8 +466,7 @@ __global__ __launch_bounds__(256) void hash_kernel(Args a, const unsigned* gate)
 // ---- simple batches: each DataPacket is message number (its rank among the DataPackets).  The
 // kernel is queued before the host knows the batch kind and does nothing for other batches
 // (except zeroing the segment count, so the speculative gather after it is empty too).
-__global__ __launch_bounds__(256) void emit_simple_kernel(Args a, const Pair* tpre, const unsigned* complex_flag,
-                                                          u64* nmsg, u64* nseg) {
+__global__ __launch_bounds__(256) void emit_simple_kernel(Args a, const unsigned* complex_flag, u64* nmsg, u64* nseg) {
     const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
     if (*complex_flag) {
         if (i == 0) *nseg = 0;
@@ -366,7 +476,7 @@ __global__ __launch_bounds__(256) void emit_simple_kernel(Args a, const Pair* tp
     const u32 pl = data ? a.plen[i] : 0u;
     Pair e, t;
     block_scan_pair(data ? Pair{pl, ((u64)1 << 32) | 1u} : Pair{0, 0}, e, t);
-    const Pair b = tpre[blockIdx.x];
+    const Pair b = raw::tile_prefix_2l(a.agg, a.super_p, blockIdx.x, (a.n + 256) / 256);  // the parse's totals
     const u64 bytes = b.bytes + e.bytes, mi = (b.count + e.count) & 0xffffffffull;
     if (data) {
         a.msg_off[mi] = bytes;
@@ -581,32 +691,33 @@ __device__ inline void block_scan_pair(Pair v, Pair& excl, Pair& tile_total) {
     tile_total = Pair{wb[0] + wb[1] + wb[2] + wb[3], wc[0] + wc[1] + wc[2] + wc[3]};
 }
 
-__global__ __launch_bounds__(256) void pair_tile_total_kernel(const Pair* v, u64 m, Pair* agg, const unsigned* gate) {
-    if (gated_off(gate)) return;
-    const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
-    Pair e, t;
-    block_scan_pair(i < m ? v[i] : Pair{0, 0}, e, t);
-    if (threadIdx.x == 0) agg[blockIdx.x] = t;
-}
-
-__global__ __launch_bounds__(256) void pair_scan_apply_kernel(const Pair* v, u64 m, const Pair* tpre, Pair* out,
+__global__ __launch_bounds__(256) void pair_tile_total_kernel(const Pair* v, u64 m, Pair* agg, Pair* super,
                                                               const unsigned* gate) {
     if (gated_off(gate)) return;
     const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
     Pair e, t;
     block_scan_pair(i < m ? v[i] : Pair{0, 0}, e, t);
-    const Pair b = tpre[blockIdx.x];
-    if (i < m) out[i] = Pair{b.bytes + e.bytes, b.count + e.count};
+    if (threadIdx.x == 0) raw::publish_tile_total(agg, super, blockIdx.x, t);
 }
 
-// message count, closing offset and segment count from the grand total
-__global__ void finalize_kernel(const Pair* total, u64* msg_off, u64* nmsg, u64* nseg, const unsigned* gate) {
+// The exclusive scan applied (tile prefixes from the two-level totals), and at the last entry (m - 1:
+// a zero triple, so its prefix is the grand total) the message count, closing offset and segment count.
+__global__ __launch_bounds__(256) void pair_scan_apply_kernel(const Pair* v, u64 m, const Pair* agg, const Pair* super,
+                                                              Pair* out, u64* msg_off, u64* nmsg, u64* nseg,
+                                                              const unsigned* gate) {
     if (gated_off(gate)) return;
-    const Pair t = *total;
-    const u64 nm = t.count & 0xffffffffull;
-    *nmsg = nm;
-    msg_off[nm] = t.bytes;
-    *nseg = t.count >> 32;
+    const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
+    Pair e, t;
+    block_scan_pair(i < m ? v[i] : Pair{0, 0}, e, t);
+    const Pair b = raw::tile_prefix_2l(agg, super, blockIdx.x, (m + 255) / 256);
+    if (i < m) out[i] = Pair{b.bytes + e.bytes, b.count + e.count};
+    if (i == m - 1) {
+        const u64 tb = b.bytes + e.bytes, tc = b.count + e.count;
+        const u64 nm = tc & 0xffffffffull;
+        *nmsg = nm;
+        msg_off[nm] = tb;
+        *nseg = tc >> 32;
+    }
 }
 
 // ---- 6. tile totals of the segment lengths (segment count on the device)
@@ -634,8 +745,8 @@ inline unsigned log2u(u64 t) {
 inline unsigned key_bits(u64 n) { return log2u(n + 1) + 1; }  // keys in [0, n]
 
 struct Layout {
-    size_t table, first, slot, rpc, meta, plen, gid, idx, gs, is, state, cnt, pre, agg, tpre, seg_src, seg_len, agg2,
-        pre2, agg3, pre3, nseg, nseg2, flag, unsorted, nonmono, hist, rowtot, total;
+    size_t table, first, slot, rpc, meta, plen, gid, idx, gs, is, state, cnt, pre, agg, seg_src, seg_len, agg2, pre2, agg3,
+        pre3, nseg, nseg2, flag, unsorted, nonmono, bar, sup_p, sup_c, zero_bytes, hist, rowtot, total;
 };
 
 inline u64 sort_tiles(u64 n) { return (n + kSortTile - 1) / kSortTile; }
@@ -663,7 +774,6 @@ inline Layout layout(u64 n) {
     L.cnt = take((n + 1) * sizeof(Pair));
     L.pre = take((n + 1) * sizeof(Pair));
     L.agg = take((tiles(n + 1) + 1) * sizeof(Pair));
-    L.tpre = take((tiles(n + 1) + 1) * sizeof(Pair));
     L.seg_src = take(n * 8);
     L.seg_len = take(n * 8);
     L.agg2 = take((tiles(n) + 1) * sizeof(Pair));
@@ -671,10 +781,18 @@ inline Layout layout(u64 n) {
     L.agg3 = take((tiles(n) + 1) * sizeof(Pair));  // the single-datagram path's own (it runs beside the general path)
     L.pre3 = take((tiles(n) + 1) * sizeof(Pair));
     L.nseg = take(8);
-    L.nseg2 = take(32);  // the general path's segment count, the parse's flag, the key order and
-    L.flag = L.nseg2 + 8;  // RPCID order flags: zeroed together
+    // the general path's segment count, the parse's flag, the key order and RPCID order flags, the
+    // sort's barrier, then the two two-level total arrays (the parse's, the group triples'): zeroed
+    // together, one memset per call
+    const size_t sup = raw::super_bytes(tiles(n + 1));
+    L.zero_bytes = 128 + 2 * sup;
+    L.nseg2 = take(L.zero_bytes);
+    L.sup_p = L.nseg2 + 128;  // (its own lines: the atomics on the totals stay off the flags' line)
+    L.sup_c = L.sup_p + sup;
+    L.flag = L.nseg2 + 8;
     L.unsorted = L.nseg2 + 12;
     L.nonmono = L.nseg2 + 16;
+    L.bar = L.nseg2 + 20;
     L.hist = take((size_t)kDigits * sort_tiles(n) * 4);
     L.rowtot = take(kDigits * 4);
     L.total = o;
@@ -723,8 +841,9 @@ hipError_t launch_reassemble(const uint8_t* wire, const u64* dg_off, u64 n, uint
     const dim3 gq((unsigned)rx::tiles(n));
     const u64 nt = rx::tiles(n + 1), ns = rx::tiles(n);
     Pair* agg = (Pair*)(w + L.agg);
-    Pair* tpre = (Pair*)(w + L.tpre);
     a.agg = agg;
+    a.super_p = (Pair*)(w + L.sup_p);
+    a.super_c = (Pair*)(w + L.sup_c);
     // the payload segments' tile prefixes, then the gather (segment count on the device); gate:
     // the general path's copy, which does nothing for a simple batch
     auto seg_tail = [&](u64* nseg, const unsigned* gate, hipStream_t st) -> hipError_t {
@@ -756,11 +875,10 @@ hipError_t launch_reassemble(const uint8_t* wire, const u64* dg_off, u64 n, uint
     // the emit writes no message and zero segments, so this gather is empty.
     u64* nseg = (u64*)(w + L.nseg);
     u64* nseg2 = (u64*)(w + L.nseg2);
-    hipError_t e = hipMemsetAsync(w + L.nseg2, 0, 32, stream);  // nseg2 and the flags
+    hipError_t e = hipMemsetAsync(w + L.nseg2, 0, L.zero_bytes, stream);  // nseg2, the flags, the group totals
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(rx::parse_kernel, dim3((unsigned)nt), b256, 0, stream, a, (unsigned*)flag);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    if ((e = launch_tile_scan(agg, tpre, nt, stream)) != hipSuccess) return e;
     // The general path is queued for every batch; each of its kernels exits at once unless the
     // parse set the flag (no host read: the call stays asynchronous).  It runs on `aux`, forked
     // here and joined at the end, so for a simple batch its ~20 empty launches overlap the copy
@@ -773,13 +891,11 @@ hipError_t launch_reassemble(const uint8_t* wire, const u64* dg_off, u64 n, uint
         if ((e = hipStreamWaitEvent(aux, fork, 0)) != hipSuccess) return e;
         gs = aux;
     }
-    hipLaunchKernelGGL(rx::emit_simple_kernel, dim3((unsigned)nt), b256, 0, stream, a, (const Pair*)tpre, flag, nmsg,
-                       nseg);
+    hipLaunchKernelGGL(rx::emit_simple_kernel, dim3((unsigned)nt), b256, 0, stream, a, flag, nmsg, nseg);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = seg_tail(nseg, nullptr, stream)) != hipSuccess) return e;
-    hipLaunchKernelGGL(rx::order_kernel, gq, b256, 0, gs, a, flag, (unsigned*)a.nonmono);
     hipLaunchKernelGGL(rx::init_kernel, dim3((unsigned)std::min<u64>(rx::tiles(TS + 1), 4096)), b256, 0, gs, a.table,
-                       a.first, TS, a.nonmono);
+                       a.first, TS, flag, a.nonmono);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(rx::hash_kernel, gq, b256, 0, gs, a, flag);
     if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -794,14 +910,32 @@ hipError_t launch_reassemble(const uint8_t* wire, const u64* dg_off, u64 n, uint
         u32* rowtot = (u32*)(w + L.rowtot);
         const unsigned bits = rx::key_bits(n);
         int cur = 0;
-        for (unsigned shift = 0; shift < bits; shift += 8, cur ^= 1) {
-            hipLaunchKernelGGL(rx::sort_hist_kernel, dim3((unsigned)st), b256, 0, gs, (const u32*)kb[cur], n,
-                               (int)shift, hist, st, a.unsorted);
-            hipLaunchKernelGGL(rx::sort_rowscan_kernel, dim3(rx::kDigits), b256, 0, gs, hist, st, rowtot, a.unsorted);
-            hipLaunchKernelGGL(rx::sort_scatter_kernel, dim3((unsigned)st), b256, 0, gs, (const u32*)kb[cur],
-                               (const u32*)vb[cur], kb[cur ^ 1], vb[cur ^ 1], n, (int)shift, (const u32*)hist, st,
-                               (const u32*)rowtot, a.unsorted);
+        bool one_launch = true;
+#ifdef SYMHIP_TUNING
+        one_launch = tuning_variant("SYMHIP_RX_VARIANT") != 1;  // 1: the round-5 form, three launches a pass
+#endif
+        if (one_launch) {
+            static int cus[16] = {0};
+            int dev = 0;
+            if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
+            int& ncu = cus[dev & 15];
+            if (ncu == 0 && (e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess)
+                return e;
+            rx::SortArgs sa{{kb[0], kb[1]}, {vb[0], vb[1]}, n, hist, st, rowtot, a.unsorted,
+                            (unsigned*)(w + L.bar), err, bits};
+            hipLaunchKernelGGL(rx::sort_all_kernel, dim3((unsigned)std::min<u64>(st, (u64)ncu)), b256, 0, gs, sa);
             if ((e = hipGetLastError()) != hipSuccess) return e;
+            cur = (int)(((bits + 7) / 8) & 1);
+        } else {
+            for (unsigned shift = 0; shift < bits; shift += 8, cur ^= 1) {
+                hipLaunchKernelGGL(rx::sort_hist_kernel, dim3((unsigned)st), b256, 0, gs, (const u32*)kb[cur], n,
+                                   (int)shift, hist, st, a.unsorted);
+                hipLaunchKernelGGL(rx::sort_rowscan_kernel, dim3(rx::kDigits), b256, 0, gs, hist, st, rowtot, a.unsorted);
+                hipLaunchKernelGGL(rx::sort_scatter_kernel, dim3((unsigned)st), b256, 0, gs, (const u32*)kb[cur],
+                                   (const u32*)vb[cur], kb[cur ^ 1], vb[cur ^ 1], n, (int)shift, (const u32*)hist, st,
+                                   (const u32*)rowtot, a.unsorted);
+                if ((e = hipGetLastError()) != hipSuccess) return e;
+            }
         }
         a.gs = kb[cur];
         a.is = vb[cur];
@@ -809,14 +943,10 @@ hipError_t launch_reassemble(const uint8_t* wire, const u64* dg_off, u64 n, uint
     hipLaunchKernelGGL(rx::group_kernel<0>, gq, b256, 0, gs, a, flag);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(rx::pair_tile_total_kernel, dim3((unsigned)nt), b256, 0, gs, (const Pair*)a.cnt, n + 1, agg,
-                       flag);
+                       a.super_c, flag);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    if ((e = launch_tile_scan_gated(agg, tpre, nt, flag, gs)) != hipSuccess) return e;
     hipLaunchKernelGGL(rx::pair_scan_apply_kernel, dim3((unsigned)nt), b256, 0, gs, (const Pair*)a.cnt, n + 1,
-                       (const Pair*)tpre, (Pair*)(w + L.pre), flag);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(rx::finalize_kernel, dim3(1), dim3(1), 0, gs, (const Pair*)(w + L.pre) + n, msg_off, nmsg,
-                       nseg2, flag);
+                       (const Pair*)agg, (const Pair*)a.super_c, (Pair*)(w + L.pre), msg_off, nmsg, nseg2, flag);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(rx::group_kernel<1>, gq, b256, 0, gs, a, flag);
     if ((e = hipGetLastError()) != hipSuccess) return e;

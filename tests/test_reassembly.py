@@ -228,6 +228,16 @@ def test_reassembly_round_trip_gpu(gcodec, gdev, cfg, mtu):
 
 
 @pytest.mark.gpu
+def test_reassembly_large_shuffled_gpu(gcodec, gdev):
+    """More sort tiles (2048 datagrams each) than the one-launch sort has workgroups (one per CU):
+    every workgroup takes several tiles per phase, across the grid barriers of three passes."""
+    stream, off, rpc, wire, dg_off = packetized(datagen.CONFIG2, 600000, 1400)
+    perm = np.random.default_rng(11).permutation(len(dg_off) - 1)
+    want = _gpu_vs_oracle(gcodec, gdev, *shuffled(wire, dg_off, perm))
+    assert len(want[2]) == 600000 and (want[4] == C).all()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n", [1, 63, 64, 257, 5000])
 def test_reassembly_simple_batch_gpu(gcodec, gdev, n):
     """Batches of complete single-datagram messages take the device fast path (no grouping): parse

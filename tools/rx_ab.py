@@ -28,6 +28,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--variants", default="0,3")
     ap.add_argument("--rounds", type=int, default=10)
+    ap.add_argument("--env", default="SYMHIP_GATHER_VARIANT", help="the tuning variable the variants set")
     a = ap.parse_args()
     variants = [int(v) for v in a.variants.split(",")]
     dev = torch.device("cuda", 0)
@@ -55,7 +56,7 @@ def main():
     for rnd in range(a.rounds + 1):
         for w, (fn, outs) in work.items():
             for v in variants:
-                os.environ["SYMHIP_GATHER_VARIANT"] = str(v)
+                os.environ[a.env] = str(v)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 r = fn()
@@ -75,7 +76,7 @@ def main():
                 else:
                     times[(w, v)].append(e0.elapsed_time(e1) * 1e3)
     for (w, v), ts in times.items():
-        print(f"{w:12s} gather variant {v}: median {statistics.median(ts):8.1f} us  min {min(ts):8.1f} us")
+        print(f"{w:12s} {a.env} {v}: median {statistics.median(ts):8.1f} us  min {min(ts):8.1f} us")
 
 
 if __name__ == "__main__":
