@@ -104,7 +104,7 @@ struct DecodeWsHeader {
     unsigned int pad[3];
 };
 constexpr unsigned kErrCapacity = 1u;
-constexpr unsigned kErrTimeout = 2u;   // a bounded device-side wait gave up (no kernel sets it today)
+constexpr unsigned kErrTimeout = 2u;   // a bounded device-side wait gave up (the reassembly sort's grid barrier)
 constexpr unsigned kErrTooLarge = 4u;  // 64 consecutive records spanning >= 2 GiB
 constexpr unsigned kErrBadNested = 16u;  // flat encode: a (non-repeated) nested field given more than one item
 constexpr unsigned kErrBadLength = 8u;  // flat encode: a repeated field's byte length is not a multiple of its width

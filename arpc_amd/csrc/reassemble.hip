@@ -97,9 +97,12 @@ struct Args {
     u64* msg_dg;
     u64* seg_src;
     u64* seg_len;
+    Pair* seg_pre;         // the segment gather's tile prefixes (the general path's): written where the
+                           // segments are, see emit_simple_kernel
 };
 
 __device__ inline void block_scan_pair(Pair v, Pair& excl, Pair& tile_total);
+__host__ __device__ inline u64 tiles(u64 m) { return (m + 255) / 256; }
 
 // The general path's kernels run only when the parse flagged the batch as not simple (uniform).
 __device__ __forceinline__ bool gated_off(const unsigned* gate) { return *gate == 0; }
@@ -466,7 +469,11 @@ __global__ __launch_bounds__(256) void hash_kernel(Args a, const unsigned* gate)
 // ---- simple batches: each DataPacket is message number (its rank among the DataPackets).  The
 // kernel is queued before the host knows the batch kind and does nothing for other batches
 // (except zeroing the segment count, so the speculative gather after it is empty too).
-__global__ __launch_bounds__(256) void emit_simple_kernel(Args a, const unsigned* complex_flag, u64* nmsg, u64* nseg) {
+//   The segment gather's tile prefixes come from here too (round 6): segment mi is message mi, whose
+// output offset is known, so the first segment of every 256-segment tile writes its tile's prefix and
+// entry n the total at tile ceil(nseg / 256) -- no tile-total and scan launches before the gather.
+__global__ __launch_bounds__(256) void emit_simple_kernel(Args a, const unsigned* complex_flag, u64* nmsg, u64* nseg,
+                                                          Pair* seg_pre) {
     const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
     if (*complex_flag) {
         if (i == 0) *nseg = 0;
@@ -485,11 +492,13 @@ __global__ __launch_bounds__(256) void emit_simple_kernel(Args a, const unsigned
         a.seg_src[mi] = a.dg_off[i] + kHdr;
         a.seg_len[mi] = pl;
         a.status[i] = SYM_RX_CONSUMED;
+        if ((mi & 255) == 0) seg_pre[mi >> 8] = Pair{bytes, 0};
     }
     if (i == a.n) {  // entry n: the totals
         *nmsg = mi;
         a.msg_off[mi] = bytes;
         *nseg = mi;
+        seg_pre[tiles(mi)] = Pair{bytes, 0};
     }
 }
 
@@ -588,10 +597,14 @@ __global__ __launch_bounds__(256) void group_kernel(Args a, const unsigned* gate
                 a.msg_off[mi] = pp.bytes;
                 a.msg_rpc[mi] = a.rpc[jl];
                 a.msg_dg[mi] = jl;
+                u64 at = pp.bytes;  // the segment's output offset
                 for (u64 t = 0; t < k; ++t) {
                     const u32 j = a.is[q0 + t];
+                    const u32 pl = a.plen[j];
                     a.seg_src[sb + t] = a.dg_off[j] + kHdr;
-                    a.seg_len[sb + t] = a.plen[j];
+                    a.seg_len[sb + t] = pl;
+                    if (((sb + t) & 255) == 0) a.seg_pre[(sb + t) >> 8] = Pair{at, 0};
+                    at += pl;
                 }
             }
             return;
@@ -654,6 +667,7 @@ __global__ __launch_bounds__(256) void group_kernel(Args a, const unsigned* gate
                 if constexpr (PASS == 1) {
                     a.seg_src[sb + segs] = a.dg_off[src] + kHdr;
                     a.seg_len[sb + segs] = a.plen[src];
+                    if (((sb + segs) & 255) == 0) a.seg_pre[(sb + segs) >> 8] = Pair{ob + bytes, 0};
                 }
                 bytes += a.plen[src];
                 ++segs;
@@ -704,7 +718,7 @@ __global__ __launch_bounds__(256) void pair_tile_total_kernel(const Pair* v, u64
 // a zero triple, so its prefix is the grand total) the message count, closing offset and segment count.
 __global__ __launch_bounds__(256) void pair_scan_apply_kernel(const Pair* v, u64 m, const Pair* agg, const Pair* super,
                                                               Pair* out, u64* msg_off, u64* nmsg, u64* nseg,
-                                                              const unsigned* gate) {
+                                                              Pair* seg_pre, const unsigned* gate) {
     if (gated_off(gate)) return;
     const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
     Pair e, t;
@@ -717,21 +731,11 @@ __global__ __launch_bounds__(256) void pair_scan_apply_kernel(const Pair* v, u64
         *nmsg = nm;
         msg_off[nm] = tb;
         *nseg = tc >> 32;
+        seg_pre[tiles(tc >> 32)] = Pair{tb, 0};  // the segments' total (group pass 1 writes the tile prefixes)
     }
 }
 
-// ---- 6. tile totals of the segment lengths (segment count on the device)
-__global__ __launch_bounds__(256) void seg_tile_total_kernel(const u64* seg_len, const u64* nseg, Pair* agg,
-                                                             const unsigned* gate) {
-    if (gate && gated_off(gate)) return;
-    const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
-    Pair e, t;
-    block_scan_pair(Pair{i < *nseg ? seg_len[i] : 0, 0}, e, t);
-    if (threadIdx.x == 0) agg[blockIdx.x] = t;
-}
-
 inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
-inline u64 tiles(u64 m) { return (m + 255) / 256; }
 inline u64 table_size(u64 n) {
     u64 t = 1024;
     while (t < 2 * n) t <<= 1;
@@ -745,8 +749,7 @@ inline unsigned log2u(u64 t) {
 inline unsigned key_bits(u64 n) { return log2u(n + 1) + 1; }  // keys in [0, n]
 
 struct Layout {
-    size_t table, first, slot, rpc, meta, plen, gid, idx, gs, is, state, cnt, pre, agg, seg_src, seg_len, agg2, pre2, agg3,
-        pre3, nseg, nseg2, flag, unsorted, nonmono, bar, sup_p, sup_c, zero_bytes, hist, rowtot, total;
+    size_t table, first, slot, rpc, meta, plen, gid, idx, gs, is, state, cnt, pre, agg, seg_src, seg_len, pre2, pre3, nseg, nseg2, flag, unsorted, nonmono, bar, sup_p, sup_c, zero_bytes, hist, rowtot, total;
 };
 
 inline u64 sort_tiles(u64 n) { return (n + kSortTile - 1) / kSortTile; }
@@ -776,10 +779,8 @@ inline Layout layout(u64 n) {
     L.agg = take((tiles(n + 1) + 1) * sizeof(Pair));
     L.seg_src = take(n * 8);
     L.seg_len = take(n * 8);
-    L.agg2 = take((tiles(n) + 1) * sizeof(Pair));
     L.pre2 = take((tiles(n) + 1) * sizeof(Pair));
-    L.agg3 = take((tiles(n) + 1) * sizeof(Pair));  // the single-datagram path's own (it runs beside the general path)
-    L.pre3 = take((tiles(n) + 1) * sizeof(Pair));
+    L.pre3 = take((tiles(n) + 1) * sizeof(Pair));  // the single-datagram path's own (it runs beside the general path)
     L.nseg = take(8);
     // the general path's segment count, the parse's flag, the key order and RPCID order flags, the
     // sort's barrier, then the two two-level total arrays (the parse's, the group triples'): zeroed
@@ -834,26 +835,23 @@ hipError_t launch_reassemble(const uint8_t* wire, const u64* dg_off, u64 n, uint
     a.msg_dg = msg_dg;
     a.seg_src = (u64*)(w + L.seg_src);
     a.seg_len = (u64*)(w + L.seg_len);
+    a.seg_pre = (Pair*)(w + L.pre2);
     a.unsorted = (unsigned*)(w + L.unsorted);
     a.nonmono = (const unsigned*)(w + L.nonmono);
     const dim3 b256(256);
     const unsigned* flag = (const unsigned*)(w + L.flag);
     const dim3 gq((unsigned)rx::tiles(n));
-    const u64 nt = rx::tiles(n + 1), ns = rx::tiles(n);
+    const u64 nt = rx::tiles(n + 1);
     Pair* agg = (Pair*)(w + L.agg);
     a.agg = agg;
     a.super_p = (Pair*)(w + L.sup_p);
     a.super_c = (Pair*)(w + L.sup_c);
     // the payload segments' tile prefixes, then the gather (segment count on the device); gate:
     // the general path's copy, which does nothing for a simple batch
-    auto seg_tail = [&](u64* nseg, const unsigned* gate, hipStream_t st) -> hipError_t {
-        Pair* agg2 = (Pair*)(w + (gate ? L.agg2 : L.agg3));
-        Pair* pre2 = (Pair*)(w + (gate ? L.pre2 : L.pre3));
-        hipLaunchKernelGGL(rx::seg_tile_total_kernel, dim3((unsigned)ns), b256, 0, st, (const u64*)a.seg_len,
-                           (const u64*)nseg, agg2, gate);
-        hipError_t r = hipGetLastError();
-        if (r == hipSuccess) r = launch_tile_scan_gated(agg2, pre2, ns, gate, st);
-        if (r != hipSuccess) return r;
+    // the payload gather (segment count and tile prefixes on the device); general: the general path's
+    // copy, which does nothing for a simple batch (its segment count stays 0)
+    auto seg_tail = [&](u64* nseg, bool general, hipStream_t st) -> hipError_t {
+        Pair* pre2 = (Pair*)(w + (general ? L.pre2 : L.pre3));
         raw::GatherArgs ga{};
         ga.in = wire;
         ga.n = n;
@@ -867,7 +865,7 @@ hipError_t launch_reassemble(const uint8_t* wire, const u64* dg_off, u64 n, uint
         ga.cap = msg_cap;
         ga.err = err;
         ga.seg_bytes_hint = msg_cap / n;  // (the capacity is usually the wire size)
-        ga.nt = gate == nullptr;  // the simple path's gather (one A/B: +6 %; the general path's -5 %)
+        ga.nt = !general;  // the simple path's gather (one A/B: +6 %; the general path's -5 %)
         return launch_segment_gather(ga, st);
     };
     // Simple batches (every DataPacket one whole message) complete here: parse (with the tile
@@ -881,19 +879,20 @@ hipError_t launch_reassemble(const uint8_t* wire, const u64* dg_off, u64 n, uint
     if ((e = hipGetLastError()) != hipSuccess) return e;
     // The general path is queued for every batch; each of its kernels exits at once unless the
     // parse set the flag (no host read: the call stays asynchronous).  It runs on `aux`, forked
-    // here and joined at the end, so for a simple batch its ~20 empty launches overlap the copy
+    // here and joined at the end, so for a simple batch its nine empty launches overlap the copy
     // below.  The two branches share no buffer that both write for the same batch: every write of
-    // the simple branch past this point is for a simple batch (its segment scan excepted, which
-    // has agg3 / pre3 to itself), every write of the general branch for a complex one.
+    // the simple branch past this point is for a simple batch (its zero segment count for a complex
+    // one excepted, in a word of its own), every write of the general branch for a complex one.
     hipStream_t gs = stream;
     if (aux && fork && join) {
         if ((e = hipEventRecord(fork, stream)) != hipSuccess) return e;
         if ((e = hipStreamWaitEvent(aux, fork, 0)) != hipSuccess) return e;
         gs = aux;
     }
-    hipLaunchKernelGGL(rx::emit_simple_kernel, dim3((unsigned)nt), b256, 0, stream, a, flag, nmsg, nseg);
+    hipLaunchKernelGGL(rx::emit_simple_kernel, dim3((unsigned)nt), b256, 0, stream, a, flag, nmsg, nseg,
+                       (Pair*)(w + L.pre3));
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    if ((e = seg_tail(nseg, nullptr, stream)) != hipSuccess) return e;
+    if ((e = seg_tail(nseg, false, stream)) != hipSuccess) return e;
     hipLaunchKernelGGL(rx::init_kernel, dim3((unsigned)std::min<u64>(rx::tiles(TS + 1), 4096)), b256, 0, gs, a.table,
                        a.first, TS, flag, a.nonmono);
     if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -946,11 +945,12 @@ hipError_t launch_reassemble(const uint8_t* wire, const u64* dg_off, u64 n, uint
                        a.super_c, flag);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(rx::pair_scan_apply_kernel, dim3((unsigned)nt), b256, 0, gs, (const Pair*)a.cnt, n + 1,
-                       (const Pair*)agg, (const Pair*)a.super_c, (Pair*)(w + L.pre), msg_off, nmsg, nseg2, flag);
+                       (const Pair*)agg, (const Pair*)a.super_c, (Pair*)(w + L.pre), msg_off, nmsg, nseg2,
+                       (Pair*)(w + L.pre2), flag);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(rx::group_kernel<1>, gq, b256, 0, gs, a, flag);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    if ((e = seg_tail(nseg2, flag, gs)) != hipSuccess) return e;
+    if ((e = seg_tail(nseg2, true, gs)) != hipSuccess) return e;
     if (gs != stream) {
         if ((e = hipEventRecord(join, gs)) != hipSuccess) return e;
         if ((e = hipStreamWaitEvent(stream, join, 0)) != hipSuccess) return e;
