@@ -39,6 +39,18 @@ __device__ __forceinline__ void publish_tile_total(Pair* agg, Pair* super, u64 t
     if (t.bytes) atomicAdd((unsigned long long*)&g->bytes, (unsigned long long)t.bytes);
     if (t.count) atomicAdd((unsigned long long*)&g->count, (unsigned long long)t.count);
 }
+// The same totals built by adding contributions (agg and super zeroed before the producer runs).
+__device__ __forceinline__ void add_tile_total(Pair* agg, Pair* super, u64 tile, Pair t) {
+    Pair* g = super + (tile / kSuperTiles) * kSuperStride;
+    if (t.bytes) {
+        atomicAdd((unsigned long long*)&agg[tile].bytes, (unsigned long long)t.bytes);
+        atomicAdd((unsigned long long*)&g->bytes, (unsigned long long)t.bytes);
+    }
+    if (t.count) {
+        atomicAdd((unsigned long long*)&agg[tile].count, (unsigned long long)t.count);
+        atomicAdd((unsigned long long*)&g->count, (unsigned long long)t.count);
+    }
+}
 // Whole workgroup of 256 threads (every thread calls it): tile's exclusive prefix; the grand total of the
 // ntiles tiles into *total when given.
 __device__ inline Pair tile_prefix_2l(const Pair* agg, const Pair* super, u64 tile, u64 ntiles, Pair* total = nullptr) {

@@ -90,7 +90,8 @@ struct Args {
     Pair* cnt;             // per arrival (n+1): (message bytes, segments << 32 | messages)
     Pair* agg;             // its tile totals (simple batches: written by parse_kernel)
     Pair* super_p;         // their two-level group totals (gather_tile.hpp publish_tile_total): the parse's
-    Pair* super_c;         // and the general path's (group pass 0's triples)
+    Pair* agg_c;           // the general path's tile totals of the triples (added up by group pass 0)
+    Pair* super_c;         // and their group totals
     const Pair* pre;       // its exclusive scan
     u64* msg_off;
     u64* msg_rpc;
@@ -559,16 +560,25 @@ __device__ inline bool seq_complete(const SeqState& x) {
     return true;
 }
 
+// Group pass 0's triple for arrival j, and its share of j's tile total: the workgroup's own tile and
+// the next one (where a run that starts here usually completes) in LDS, flushed once at the end;
+// farther tiles (long runs, or sorted groups) by global atomics.  (Round 6: this replaced a
+// tile-total launch over the triples between the group pass and the scan.)
+__device__ __forceinline__ void put_cnt(const Args& a, u64 j, Pair v, u64* sb, u64* sc) {
+    a.cnt[j] = v;
+    const u64 t = j >> 8, d = t - blockIdx.x;
+    if (d < 2) {
+        atomicAdd((unsigned long long*)&sb[d], (unsigned long long)v.bytes);
+        atomicAdd((unsigned long long*)&sc[d], (unsigned long long)v.count);
+    } else {
+        raw::add_tile_total(a.agg_c, a.super_c, t, v);
+    }
+}
+
 // ---- 3 / 5. the ProcessFragment state machine over one group's run (fragmentation.go:62-181)
 template <int PASS>
-__global__ __launch_bounds__(256) void group_kernel(Args a, const unsigned* gate) {
-    if (gated_off(gate)) return;
-    const u64 q0 = (u64)blockIdx.x * 256 + threadIdx.x;
+__device__ __forceinline__ void group_one(const Args& a, u64 q0, u64* lb, u64* lc) {
     if (q0 >= a.n) return;
-    if (!*a.unsorted) {  // the keys were in order already: the sort left them in gid / idx
-        a.gs = a.gid;
-        a.is = a.idx;
-    }
     const u32 g = a.gs[q0];
     if (g == a.nodata) return;                   // not a DataPacket (sorted last)
     if (q0 > 0 && a.gs[q0 - 1] == g) return;     // not the first of its group
@@ -589,7 +599,7 @@ __global__ __launch_bounds__(256) void group_kernel(Args a, const unsigned* gate
         if (fast) {
             const u32 jl = a.is[e - 1];
             if constexpr (PASS == 0) {
-                a.cnt[jl] = Pair{bytes, (k << 32) | 1u};
+                put_cnt(a, jl, Pair{bytes, (k << 32) | 1u}, lb, lc);
                 for (u64 t = 0; t < k; ++t) a.status[a.is[q0 + t]] = SYM_RX_CONSUMED;
             } else {
                 const Pair pp = a.pre[jl];
@@ -673,7 +683,7 @@ __global__ __launch_bounds__(256) void group_kernel(Args a, const unsigned* gate
                 ++segs;
             }
         }
-        if constexpr (PASS == 0) a.cnt[j] = Pair{bytes, (segs << 32) | 1u};
+        if constexpr (PASS == 0) put_cnt(a, j, Pair{bytes, (segs << 32) | 1u}, lb, lc);
         for (u64 b = r; b <= q; ++b) {              // :175-178: the RPCID's state is deleted
             const u32 jb = a.is[b];
             if constexpr (PASS == 0) a.status[jb] = SYM_RX_CONSUMED;
@@ -683,6 +693,25 @@ __global__ __launch_bounds__(256) void group_kernel(Args a, const unsigned* gate
         r = q + 1;
         distinct = ncomplete = maxseq = 0;
         big = false;
+    }
+}
+template <int PASS>
+__global__ __launch_bounds__(256) void group_kernel(Args a, const unsigned* gate) {
+    if (gated_off(gate)) return;
+    if (!*a.unsorted) {  // the keys were in order already: the sort left them in gid / idx
+        a.gs = a.gid;
+        a.is = a.idx;
+    }
+    __shared__ u64 sb[2], sc[2];  // pass 0: the totals of this workgroup's tile and the next
+    if constexpr (PASS == 0) {
+        if (threadIdx.x < 2) sb[threadIdx.x] = sc[threadIdx.x] = 0;
+        __syncthreads();
+    }
+    group_one<PASS>(a, (u64)blockIdx.x * 256 + threadIdx.x, sb, sc);
+    if constexpr (PASS == 0) {
+        __syncthreads();
+        if (threadIdx.x < 2 && (sb[threadIdx.x] | sc[threadIdx.x]))
+            raw::add_tile_total(a.agg_c, a.super_c, blockIdx.x + threadIdx.x, Pair{sb[threadIdx.x], sc[threadIdx.x]});
     }
 }
 
@@ -703,15 +732,6 @@ __device__ inline void block_scan_pair(Pair v, Pair& excl, Pair& tile_total) {
     }
     excl = Pair{pb + ib - v.bytes, pc + ic - v.count};
     tile_total = Pair{wb[0] + wb[1] + wb[2] + wb[3], wc[0] + wc[1] + wc[2] + wc[3]};
-}
-
-__global__ __launch_bounds__(256) void pair_tile_total_kernel(const Pair* v, u64 m, Pair* agg, Pair* super,
-                                                              const unsigned* gate) {
-    if (gated_off(gate)) return;
-    const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
-    Pair e, t;
-    block_scan_pair(i < m ? v[i] : Pair{0, 0}, e, t);
-    if (threadIdx.x == 0) raw::publish_tile_total(agg, super, blockIdx.x, t);
 }
 
 // The exclusive scan applied (tile prefixes from the two-level totals), and at the last entry (m - 1:
@@ -749,7 +769,7 @@ inline unsigned log2u(u64 t) {
 inline unsigned key_bits(u64 n) { return log2u(n + 1) + 1; }  // keys in [0, n]
 
 struct Layout {
-    size_t table, first, slot, rpc, meta, plen, gid, idx, gs, is, state, cnt, pre, agg, seg_src, seg_len, pre2, pre3, nseg, nseg2, flag, unsorted, nonmono, bar, sup_p, sup_c, zero_bytes, hist, rowtot, total;
+    size_t table, first, slot, rpc, meta, plen, gid, idx, gs, is, state, cnt, pre, agg, seg_src, seg_len, pre2, pre3, nseg, nseg2, flag, unsorted, nonmono, bar, sup_p, sup_c, agg_c, zero_bytes, hist, rowtot, total;
 };
 
 inline u64 sort_tiles(u64 n) { return (n + kSortTile - 1) / kSortTile; }
@@ -783,13 +803,14 @@ inline Layout layout(u64 n) {
     L.pre3 = take((tiles(n) + 1) * sizeof(Pair));  // the single-datagram path's own (it runs beside the general path)
     L.nseg = take(8);
     // the general path's segment count, the parse's flag, the key order and RPCID order flags, the
-    // sort's barrier, then the two two-level total arrays (the parse's, the group triples'): zeroed
-    // together, one memset per call
+    // sort's barrier, then the group totals of the parse's tile totals, the group totals and tile
+    // totals of the general path's triples: zeroed together, one memset per call
     const size_t sup = raw::super_bytes(tiles(n + 1));
-    L.zero_bytes = 128 + 2 * sup;
+    L.zero_bytes = 128 + 2 * sup + (tiles(n + 1) + 1) * sizeof(Pair);
     L.nseg2 = take(L.zero_bytes);
     L.sup_p = L.nseg2 + 128;  // (its own lines: the atomics on the totals stay off the flags' line)
     L.sup_c = L.sup_p + sup;
+    L.agg_c = L.sup_c + sup;
     L.flag = L.nseg2 + 8;
     L.unsorted = L.nseg2 + 12;
     L.nonmono = L.nseg2 + 16;
@@ -846,6 +867,7 @@ hipError_t launch_reassemble(const uint8_t* wire, const u64* dg_off, u64 n, uint
     a.agg = agg;
     a.super_p = (Pair*)(w + L.sup_p);
     a.super_c = (Pair*)(w + L.sup_c);
+    a.agg_c = (Pair*)(w + L.agg_c);
     // the payload segments' tile prefixes, then the gather (segment count on the device); gate:
     // the general path's copy, which does nothing for a simple batch
     // the payload gather (segment count and tile prefixes on the device); general: the general path's
@@ -879,7 +901,7 @@ hipError_t launch_reassemble(const uint8_t* wire, const u64* dg_off, u64 n, uint
     if ((e = hipGetLastError()) != hipSuccess) return e;
     // The general path is queued for every batch; each of its kernels exits at once unless the
     // parse set the flag (no host read: the call stays asynchronous).  It runs on `aux`, forked
-    // here and joined at the end, so for a simple batch its nine empty launches overlap the copy
+    // here and joined at the end, so for a simple batch its eight empty launches overlap the copy
     // below.  The two branches share no buffer that both write for the same batch: every write of
     // the simple branch past this point is for a simple batch (its zero segment count for a complex
     // one excepted, in a word of its own), every write of the general branch for a complex one.
@@ -941,11 +963,8 @@ hipError_t launch_reassemble(const uint8_t* wire, const u64* dg_off, u64 n, uint
     }
     hipLaunchKernelGGL(rx::group_kernel<0>, gq, b256, 0, gs, a, flag);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(rx::pair_tile_total_kernel, dim3((unsigned)nt), b256, 0, gs, (const Pair*)a.cnt, n + 1, agg,
-                       a.super_c, flag);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(rx::pair_scan_apply_kernel, dim3((unsigned)nt), b256, 0, gs, (const Pair*)a.cnt, n + 1,
-                       (const Pair*)agg, (const Pair*)a.super_c, (Pair*)(w + L.pre), msg_off, nmsg, nseg2,
+                       (const Pair*)a.agg_c, (const Pair*)a.super_c, (Pair*)(w + L.pre), msg_off, nmsg, nseg2,
                        (Pair*)(w + L.pre2), flag);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(rx::group_kernel<1>, gq, b256, 0, gs, a, flag);
