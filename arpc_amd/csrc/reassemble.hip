@@ -99,19 +99,23 @@ struct Args {
     u64* seg_src;
     u64* seg_len;
     Pair* seg_pre;         // the segment gather's tile prefixes (the general path's): written where the
-                           // segments are, see emit_simple_kernel
+                           // segments are, see emit_kernel
 };
 
 __device__ inline void block_scan_pair(Pair v, Pair& excl, Pair& tile_total);
 __host__ __device__ inline u64 tiles(u64 m) { return (m + 255) / 256; }
 
-// The general path's kernels run only when the parse flagged the batch as not simple (uniform).
 __device__ __forceinline__ bool gated_off(const unsigned* gate) { return *gate == 0; }
+// The parse's words, consecutive from `flags` (all zeroed per call): [0] not simple, [1] keys out of
+// order (key_kernel), [2] not every datagram a DataPacket with RPCIDs non-decreasing, [3] a run that
+// is not the packetizer's.  The general path's kernels run only for a batch that is neither simple
+// nor runs (emit_kernel), i.e. [0] && ([2] || [3]) (uniform).
+__device__ __forceinline__ bool general_off(const unsigned* flags) { return flags[0] == 0 || (flags[2] | flags[3]) == 0; }
 
 // ---- 1a'. the hash table and first-arrival slots set to "empty" (general path, RPCIDs out of order)
 __global__ __launch_bounds__(256) void init_kernel(u64* table, u32* first, u64 ts, const unsigned* gate,
                                                    const unsigned* nonmono) {
-    if (gated_off(gate) || gated_off(nonmono)) return;
+    if (general_off(gate) || gated_off(nonmono)) return;
     for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; i <= ts; i += (u64)gridDim.x * 256) {
         if (i < ts) table[i] = kEmpty;
         first[i] = ~0u;
@@ -327,11 +331,17 @@ __global__ __launch_bounds__(256) void sort_all_kernel(SortArgs s) {
 }
 
 // ---- 1. parse (transport.go:266-283, builtin_packets.go:118-161): status, RPCID, meta, payload
-// length, and whether the batch is "simple" -- every DataPacket a whole message in one datagram
-// (TotalPackets 1, sequence 0, fragment 0, last).  Then each DataPacket completes its own message on
-// arrival whatever else the batch holds (no RPCID ever keeps state), so the messages are the
-// DataPackets in arrival order: cnt[i] = (payload bytes, one segment, one message) is already the
-// per-arrival triple the general path computes.
+// length, and which of two batch kinds that need no regrouping the batch is:
+//  * "simple": every DataPacket a whole message in one datagram (TotalPackets 1, sequence 0,
+//    fragment 0, last).  Then each DataPacket completes its own message on arrival whatever else
+//    the batch holds (no RPCID ever keeps state): the messages are the DataPackets in arrival order.
+//  * "runs" (round 6): every datagram a DataPacket, RPCIDs non-decreasing, and each run of equal
+//    RPCIDs what the packetizer sends for one message -- sequence numbers 0..k-1 in order, TotalPackets
+//    k, one fragment each.  An RPCID then appears in one run only, and ProcessFragment completes the
+//    run's message at its last datagram, with the run's payloads in arrival order as its bytes (group
+//    pass 0's fast case, made a batch-wide property): the messages are the runs in arrival order.
+// A datagram checks its run against its neighbours (the workgroup's edges parse theirs again).
+// cnt[i] = (payload bytes, 1 segment << 32 | 1 if the datagram ends its run) for a pending DataPacket.
 // One datagram's header (the parse below): status, RPCID, meta and payload length (the last three
 // only for a pending DataPacket).
 struct Parsed {
@@ -384,54 +394,77 @@ __device__ __forceinline__ Parsed parse_one(const Args& a, u64 i) {
     return q;
 }
 
-__global__ __launch_bounds__(256) void parse_kernel(Args a, unsigned* complex_flag) {
-    __shared__ u64 s_rpc[256];
+__global__ __launch_bounds__(256) void parse_kernel(Args a, unsigned* flags) {
+    __shared__ u64 s_rpc[256], s_meta[256];
     __shared__ uint8_t s_ok[256];
     const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
     Pair c = {0, 0};  // entries past the datagrams (entry n included) are zero
     bool simple = true, pend = false;
-    u64 r = 0;
+    u64 r = 0, m = 0;
+    u32 pl = 0;
     if (i < a.n) {
         const Parsed q = parse_one(a, i);
         pend = q.st == SYM_RX_PENDING;
         if (pend) {
             r = q.r;
+            m = q.m;
+            pl = q.pl;
             a.rpc[i] = q.r;
             a.meta[i] = q.m;
             a.plen[i] = q.pl;
             simple = m_total(q.m) == 1 && m_seq(q.m) == 0 && m_fidx(q.m) == 0 && !m_more(q.m);
-            c = Pair{q.pl, ((u64)1 << 32) | 1u};
         }
         a.status[i] = q.st;
     }
-    if (i <= a.n) a.cnt[i] = c;
-    // RPCID order (the general path's nonmono word): every datagram a pending DataPacket, RPCIDs never
-    // decreasing; the workgroup's first datagram compares with the previous one, parsed again here
     s_rpc[threadIdx.x] = r;
+    s_meta[threadIdx.x] = m;
     s_ok[threadIdx.x] = pend;
     __syncthreads();
-    bool bad = false;
+    bool bad = false, odd = false;  // RPCIDs out of order (or not a DataPacket); not a packetizer run
     if (i < a.n) {
-        bool pp = true;
-        u64 pr = 0;
+        bool pp = false, np = false;  // the neighbours: pending, RPCID, meta
+        u64 pr = 0, pm = 0, nr = 0;
         if (threadIdx.x > 0) {
             pp = s_ok[threadIdx.x - 1] != 0;
             pr = s_rpc[threadIdx.x - 1];
+            pm = s_meta[threadIdx.x - 1];
         } else if (i > 0) {
             const Parsed q = parse_one(a, i - 1);
             pp = q.st == SYM_RX_PENDING;
             pr = q.r;
+            pm = q.m;
+        }
+        if (i + 1 < a.n) {
+            if (threadIdx.x < 255) {
+                np = s_ok[threadIdx.x + 1] != 0;
+                nr = s_rpc[threadIdx.x + 1];
+            } else {
+                const Parsed q = parse_one(a, i + 1);
+                np = q.st == SYM_RX_PENDING;
+                nr = q.r;
+            }
         }
         bad = !pend || (i > 0 && (!pp || r < pr));
+        if (pend) {
+            const bool same_prev = i > 0 && pp && pr == r, same_next = np && nr == r;
+            const u32 sq = m_seq(m), T = m_total(m);
+            odd = m_fidx(m) != 0 || m_more(m) || sq != (same_prev ? m_seq(pm) + 1 : 0u) ||
+                  (same_prev && T != m_total(pm)) || (!same_next && sq + 1 != T);
+            c = Pair{pl, ((u64)1 << 32) | (u64)!same_next};
+        }
     }
-    if (__syncthreads_or(bad) && threadIdx.x == 0 && __hip_atomic_load(a.nonmono, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
-        atomicOr((unsigned*)a.nonmono, 1u);
+    if (i <= a.n) a.cnt[i] = c;
     // one flag check per workgroup, and the atomic only while the flag is still clear: a wave-level
     // atomicOr on one word serialised ~20k atomics per batch of multi-datagram messages (~200 us)
-    if (__syncthreads_or(!simple) && threadIdx.x == 0 &&
-        __hip_atomic_load(complex_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
-        atomicOr(complex_flag, 1u);
-    Pair e, t;  // this tile's totals, for the scan of the triples (simple batches)
+    auto raise = [&](bool any, int w) {
+        if (__syncthreads_or(any) && threadIdx.x == 0 &&
+            __hip_atomic_load(flags + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+            atomicOr(flags + w, 1u);
+    };
+    raise(!simple, 0);
+    raise(bad, 2);
+    raise(odd, 3);
+    Pair e, t;  // this tile's totals, for the scan of the triples (simple batches and runs)
     block_scan_pair(c, e, t);
     if (threadIdx.x == 0) raw::publish_tile_total(a.agg, a.super_p, blockIdx.x, t);
 }
@@ -441,7 +474,7 @@ __global__ __launch_bounds__(256) void parse_kernel(Args a, unsigned* complex_fl
 // so groups sort in order of first appearance and an in-order stream keeps its arrival order
 // through every later pass (coalesced).  The per-arrival triples are recomputed by group pass 0.
 __global__ __launch_bounds__(256) void hash_kernel(Args a, const unsigned* gate) {
-    if (gated_off(gate)) return;
+    if (general_off(gate)) return;
     const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
     if (i >= a.n) return;
     a.cnt[i] = Pair{0, 0};
@@ -467,46 +500,59 @@ __global__ __launch_bounds__(256) void hash_kernel(Args a, const unsigned* gate)
     if (g != kNoSlot) atomicMin(&a.first[g], (u32)i);
 }
 
-// ---- simple batches: each DataPacket is message number (its rank among the DataPackets).  The
-// kernel is queued before the host knows the batch kind and does nothing for other batches
-// (except zeroing the segment count, so the speculative gather after it is empty too).
-//   The segment gather's tile prefixes come from here too (round 6): segment mi is message mi, whose
-// output offset is known, so the first segment of every 256-segment tile writes its tile's prefix and
-// entry n the total at tile ceil(nseg / 256) -- no tile-total and scan launches before the gather.
-__global__ __launch_bounds__(256) void emit_simple_kernel(Args a, const unsigned* complex_flag, u64* nmsg, u64* nseg,
-                                                          Pair* seg_pre) {
+// ---- simple batches and runs (parse_kernel): the messages in arrival order, from the scan of the
+// parse's triples -- a simple batch's message m is its m-th DataPacket (the segment count), a run's
+// message is the run (the count of run ends).  The kernel is queued before the host knows the batch
+// kind and does nothing for other batches (except zeroing the segment count, so the gather after
+// it is empty too).
+//   The segment gather's tile prefixes come from here too (round 6): segment s's output offset is
+// known, so the first segment of every 256-segment tile writes its tile's prefix and entry n the
+// total at tile ceil(nseg / 256) -- no tile-total and scan launches before the gather.
+__global__ __launch_bounds__(256) void emit_kernel(Args a, const unsigned* flags, u64* nmsg, u64* nseg,
+                                                   Pair* seg_pre) {
     const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
-    if (*complex_flag) {
+    const bool simple = flags[0] == 0;
+    if (!simple && (flags[2] | flags[3]) != 0) {  // the general path's batch
         if (i == 0) *nseg = 0;
         return;
     }
     const bool data = i < a.n && a.status[i] == SYM_RX_PENDING;
-    const u32 pl = data ? a.plen[i] : 0u;
+    const Pair v = i <= a.n ? a.cnt[i] : Pair{0, 0};  // the parse's triple
     Pair e, t;
-    block_scan_pair(data ? Pair{pl, ((u64)1 << 32) | 1u} : Pair{0, 0}, e, t);
+    block_scan_pair(v, e, t);
     const Pair b = raw::tile_prefix_2l(a.agg, a.super_p, blockIdx.x, (a.n + 256) / 256);  // the parse's totals
-    const u64 bytes = b.bytes + e.bytes, mi = (b.count + e.count) & 0xffffffffull;
+    const u64 bytes = b.bytes + e.bytes, seg = (b.count + e.count) >> 32, ends = (b.count + e.count) & 0xffffffffull;
     if (data) {
-        a.msg_off[mi] = bytes;
-        a.msg_rpc[mi] = a.rpc[i];
-        a.msg_dg[mi] = i;
-        a.seg_src[mi] = a.dg_off[i] + kHdr;
-        a.seg_len[mi] = pl;
+        const u64 r = a.rpc[i];
+        a.seg_src[seg] = a.dg_off[i] + kHdr;
+        a.seg_len[seg] = v.bytes;
         a.status[i] = SYM_RX_CONSUMED;
-        if ((mi & 255) == 0) seg_pre[mi >> 8] = Pair{bytes, 0};
+        if ((seg & 255) == 0) seg_pre[seg >> 8] = Pair{bytes, 0};
+        if (simple) {
+            a.msg_off[seg] = bytes;
+            a.msg_rpc[seg] = r;
+            a.msg_dg[seg] = i;
+        } else {  // runs: every datagram pending, so the neighbours in arrival order are the run's
+            if (i == 0 || a.rpc[i - 1] != r) a.msg_off[ends] = bytes;  // the run's first datagram
+            if (v.count & 1) {                                          // its last
+                a.msg_rpc[ends] = r;
+                a.msg_dg[ends] = i;
+            }
+        }
     }
     if (i == a.n) {  // entry n: the totals
-        *nmsg = mi;
-        a.msg_off[mi] = bytes;
-        *nseg = mi;
-        seg_pre[tiles(mi)] = Pair{bytes, 0};
+        const u64 nm = simple ? seg : ends;
+        *nmsg = nm;
+        a.msg_off[nm] = bytes;
+        *nseg = seg;
+        seg_pre[tiles(seg)] = Pair{bytes, 0};
     }
 }
 
 // ---- 1b. group key = the RPCID's first arrival: groups sort in order of first appearance, so an
 // in-order stream keeps its arrival order and every later pass reads and writes it coalesced
 __global__ __launch_bounds__(256) void key_kernel(Args a, const unsigned* gate) {
-    if (gated_off(gate)) return;
+    if (general_off(gate)) return;
     const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
     bool down = false;  // a key below its predecessor's: the batch needs the sort
     if (i < a.n && !*a.nonmono) {  // the run head: every datagram is a pending DataPacket here
@@ -697,7 +743,7 @@ __device__ __forceinline__ void group_one(const Args& a, u64 q0, u64* lb, u64* l
 }
 template <int PASS>
 __global__ __launch_bounds__(256) void group_kernel(Args a, const unsigned* gate) {
-    if (gated_off(gate)) return;
+    if (general_off(gate)) return;
     if (!*a.unsorted) {  // the keys were in order already: the sort left them in gid / idx
         a.gs = a.gid;
         a.is = a.idx;
@@ -739,7 +785,7 @@ __device__ inline void block_scan_pair(Pair v, Pair& excl, Pair& tile_total) {
 __global__ __launch_bounds__(256) void pair_scan_apply_kernel(const Pair* v, u64 m, const Pair* agg, const Pair* super,
                                                               Pair* out, u64* msg_off, u64* nmsg, u64* nseg,
                                                               Pair* seg_pre, const unsigned* gate) {
-    if (gated_off(gate)) return;
+    if (general_off(gate)) return;
     const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
     Pair e, t;
     block_scan_pair(i < m ? v[i] : Pair{0, 0}, e, t);
@@ -812,9 +858,9 @@ inline Layout layout(u64 n) {
     L.sup_c = L.sup_p + sup;
     L.agg_c = L.sup_c + sup;
     L.flag = L.nseg2 + 8;
-    L.unsorted = L.nseg2 + 12;
+    L.unsorted = L.nseg2 + 12;  // (the flag words are consecutive: general_off)
     L.nonmono = L.nseg2 + 16;
-    L.bar = L.nseg2 + 20;
+    L.bar = L.nseg2 + 24;
     L.hist = take((size_t)kDigits * sort_tiles(n) * 4);
     L.rowtot = take(kDigits * 4);
     L.total = o;
@@ -911,8 +957,7 @@ hipError_t launch_reassemble(const uint8_t* wire, const u64* dg_off, u64 n, uint
         if ((e = hipStreamWaitEvent(aux, fork, 0)) != hipSuccess) return e;
         gs = aux;
     }
-    hipLaunchKernelGGL(rx::emit_simple_kernel, dim3((unsigned)nt), b256, 0, stream, a, flag, nmsg, nseg,
-                       (Pair*)(w + L.pre3));
+    hipLaunchKernelGGL(rx::emit_kernel, dim3((unsigned)nt), b256, 0, stream, a, flag, nmsg, nseg, (Pair*)(w + L.pre3));
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = seg_tail(nseg, false, stream)) != hipSuccess) return e;
     hipLaunchKernelGGL(rx::init_kernel, dim3((unsigned)std::min<u64>(rx::tiles(TS + 1), 4096)), b256, 0, gs, a.table,

@@ -165,7 +165,7 @@ def gcodec(gdev):
     c.close()
 
 
-def _gpu_vs_oracle(codec, dev, wire, dg_off, misalign=0):
+def _gpu_vs_oracle(codec, dev, wire, dg_off, misalign=0, cap=None):
     import torch
     want = oracle.reassemble(wire, dg_off)
     buf = torch.full((wire.size + misalign + 32,), 0xA5, dtype=torch.uint8, device=dev)
@@ -173,7 +173,7 @@ def _gpu_vs_oracle(codec, dev, wire, dg_off, misalign=0):
         buf[misalign:misalign + wire.size].copy_(torch.from_numpy(wire))
     w = buf[misalign:misalign + wire.size]
     o = torch.from_numpy(dg_off.view(np.int64).copy()).to(dev)
-    r = codec.reassemble(w, o)
+    r = codec.reassemble(w, o, cap=cap)
     codec.check()
     k = int(r.nmsg.item())
     assert k == len(want[2]), (k, len(want[2]))
@@ -323,3 +323,46 @@ def test_reassembly_one_rpcid_over_a_large_batch_gpu(gcodec, gdev):
     dgs.append(dgram(42, 2, 0, b"left open"))
     want = _gpu_vs_oracle(gcodec, gdev, *batch(dgs))
     assert len(want[2]) == n // 2
+
+
+@pytest.mark.gpu
+def test_reassembly_packetizer_runs_gpu(gcodec, gdev):
+    """Batches of packetizer runs (every datagram a DataPacket, RPCIDs non-decreasing, each run of
+    equal RPCIDs sequence numbers 0..k-1 of TotalPackets k, one fragment each) complete without the
+    general path (reassemble.hip parse_kernel / emit_kernel, "runs"); every near miss -- a run
+    reusing the previous RPCID, a missing or duplicated packet, interleaved RPCIDs, an error packet
+    between runs, a second fragment, a TotalPackets that changes inside a run, an incomplete last run --
+    takes the general path.  All against the oracle, then capacities: one the messages exceed (an
+    error), and one the wire exceeds but the messages fit."""
+    import torch
+    from arpc_amd import _native
+    runs = [dgram(1, 2, 0, b"ab"), dgram(1, 2, 1, b"cd"), dgram(2, 1, 0, b"e"), dgram(3, 3, 0, b"f"),
+            dgram(3, 3, 1, b""), dgram(3, 3, 2, b"h"), dgram(7, 1, 0, b"")]
+    near = [
+        runs[:2] + [dgram(1, 2, 0, b"AB"), dgram(1, 2, 1, b"CD")],        # the same RPCID again
+        runs[:1] + runs[2:],                                              # a missing packet
+        runs[:2] + [dgram(1, 2, 1, b"cd")] + runs[2:],                    # a duplicate
+        [dgram(1, 2, 0, b"ab"), dgram(2, 2, 0, b"xy"), dgram(1, 2, 1, b"cd"), dgram(2, 2, 1, b"zw")],
+        runs[:2] + [dgram(2, 1, 0, b"e", ptype=3)] + runs[3:],           # an error packet
+        runs[:2] + [dgram(2, 1, 0, b"e", fidx=1)] + runs[3:],            # a second fragment
+        runs[:3] + [dgram(3, 3, 0, b"f"), dgram(3, 2, 1, b""), dgram(3, 3, 2, b"h")],
+        runs + [dgram(9, 2, 0, b"open")],                                 # an incomplete last run
+        runs[:2] + [dgram(2, 1, 0, b"e", more=True)] + runs[3:],         # more fragments announced
+    ]
+    for dgs in [runs] + near:
+        _gpu_vs_oracle(gcodec, gdev, *batch(dgs))
+    for lo in range(1, 5):  # runs across workgroup edges
+        dgs = []
+        for r in range(600):
+            k = 1 + (r * 7 + lo) % 5
+            dgs += [dgram(100 + r, k, q, bytes([r & 255]) * ((r + q) % 9)) for q in range(k)]
+        _gpu_vs_oracle(gcodec, gdev, *batch(dgs), misalign=lo)
+    wire, off = batch(runs)
+    w, o = torch.from_numpy(wire).to(gdev), torch.from_numpy(off.view(np.int64).copy()).to(gdev)
+    gcodec.reassemble(w, o, cap=5)  # the messages hold 7 bytes
+    with pytest.raises(_native.SymphonyHipError):
+        gcodec.check()
+    gcodec.check()
+    big_open = [dgram(1, 2, 0, b"a" * 100), dgram(1, 2, 1, b"b" * 100), dgram(9, 2, 0, b"z" * 5000)]
+    want = _gpu_vs_oracle(gcodec, gdev, *batch(big_open), cap=300)  # the wire holds 5293 bytes, the messages 200
+    assert int(want[1][-1]) == 200
