@@ -267,10 +267,10 @@ __global__ __launch_bounds__(256) void sort_scatter_kernel(const u32* kin, const
     sort_scatter_tile(kin, vin, kout, vout, n, shift, hist, ntiles, rowtot, blockIdx.x);
 }
 
-// The whole sort in ONE launch (round 6): the passes' phases (tile counts, row scans, scatter) are
-// separated by a software grid barrier instead of launch boundaries, so a batch whose keys are in
-// order already -- an in-order stream, the common case -- pays one gated launch, not nine (~5 us
-// each).  The grid is at most one workgroup per CU, so all of it becomes resident; a barrier that
+// The whole sort in ONE launch (round 6, tuning builds only, SYMHIP_RX_VARIANT=2): the passes'
+// phases (tile counts, row scans, scatter) separated by a software grid barrier instead of launch
+// boundaries, so a batch whose keys are in order already pays one gated launch, not nine (~5 us
+// each) -- but a batch that needs the sort pays far more (launch_reassemble).  The grid is at most one workgroup per CU, so all of it becomes resident; a barrier that
 // still has not filled after kBarrierTicks (another stream's kernels holding the CUs that long) gives
 // up with kErrTimeout (SYM_ERR_DEVICE from sym_ctx_check), so the launch always ends.
 constexpr u64 kBarrierTicks = 50000000;  // 500 ms of s_memrealtime (100 MHz)
@@ -976,9 +976,13 @@ hipError_t launch_reassemble(const uint8_t* wire, const u64* dg_off, u64 n, uint
         u32* rowtot = (u32*)(w + L.rowtot);
         const unsigned bits = rx::key_bits(n);
         int cur = 0;
-        bool one_launch = true;
+        // three launches a pass: the one-launch form (sort_all_kernel) costs one empty launch instead of
+        // nine for a batch with its keys in order, but with its grid of one workgroup per CU each
+        // phase works through its tiles in rounds: config 3 shuffled within windows of 64, 1.05 ->
+        // 1.62 ms (profiles/r06_rx_sort_ab.txt), for 3-11 us on the batches that skip the sort
+        bool one_launch = false;
 #ifdef SYMHIP_TUNING
-        one_launch = tuning_variant("SYMHIP_RX_VARIANT") != 1;  // 1: the round-5 form, three launches a pass
+        one_launch = tuning_variant("SYMHIP_RX_VARIANT") == 2;
 #endif
         if (one_launch) {
             static int cus[16] = {0};

@@ -373,40 +373,70 @@ def packetize_leg(codec: Codec, data: torch.Tensor, rec_off: torch.Tensor, dev, 
                     "transport.go:146-201), device-resident, outside the timed region"}
 
 
-def reassembly_leg(codec: Codec, data: torch.Tensor, rec_off: torch.Tensor, dev, reps: int) -> dict:
+def byte_gather(src: torch.Tensor, start: torch.Tensor, length: torch.Tensor) -> torch.Tensor:
+    """src[start[i] : start[i] + length[i]] for every i, back to back (torch, for the bench's setup)."""
+    total = int(length.sum().item())
+    if total == 0:
+        return src[:0].clone()
+    dst0 = torch.cumsum(length, 0) - length
+    idx = torch.repeat_interleave(start - dst0, length) + torch.arange(total, device=src.device)
+    return src[idx]
+
+
+def reassembly_leg(codec: Codec, data: torch.Tensor, rec_off: torch.Tensor, dev, reps: int, window: int = 0) -> dict:
     """SURVEY.md 8f N3 beside the headline: the receive side of aRPC's transport (Receive parse +
-    DataReassembler.ProcessFragment) over the packetized batch, datagrams in send order,
-    device-resident, HIP events.  Algorithmic bytes: datagram offsets + every datagram read;
-    message bytes, message offsets / RPCIDs / completing datagrams and a status byte per datagram
-    written."""
+    DataReassembler.ProcessFragment) over the packetized batch, datagrams in send order (window 0) or
+    shuffled inside consecutive windows of `window` datagrams (UDP's local reordering: packets of a
+    message arrive out of order and RPCIDs interleave), device-resident, HIP events.  Algorithmic
+    bytes: datagram offsets + every datagram read; message bytes, message offsets / RPCIDs /
+    completing datagrams and a status byte per datagram written."""
     n = rec_off.numel() - 1
     rpc = torch.arange(n, dtype=torch.int64, device=dev)
     dg = codec.fragment(data, rec_off, rpc)
     torch.cuda.synchronize()
     codec.check()
     nd = dg.dg_off.numel() - 1
-    r = codec.reassemble(dg.wire, dg.dg_off)
+    wire, dg_off = dg.wire, dg.dg_off
+    if window:
+        g = torch.Generator(device=dev)
+        g.manual_seed(7)
+        key = torch.div(torch.arange(nd, device=dev), window, rounding_mode="floor").double() + \
+            torch.rand(nd, device=dev, dtype=torch.float64, generator=g)
+        perm = torch.argsort(key)
+        lens = (dg_off[1:] - dg_off[:-1])[perm]
+        wire = byte_gather(dg.wire, dg_off[:-1][perm], lens)
+        dg_off = torch.zeros(nd + 1, dtype=torch.int64, device=dev)
+        dg_off[1:] = torch.cumsum(lens, 0)
+        del perm, lens, key
+    r = codec.reassemble(wire, dg_off)
     torch.cuda.synchronize()
     codec.check()
     k = int(r.nmsg.item())
     mbytes = int(r.offsets[k].item())
-    ok = k == n and bool(torch.equal(r.data[:mbytes], data[:mbytes]))  # one datagram per record, in order
+    if window:  # every record, in completion order: message m is record rpc[m]
+        m_rpc = r.rpc_id[:k]
+        want = byte_gather(data, rec_off[:-1][m_rpc], (rec_off[1:] - rec_off[:-1])[m_rpc])
+        ok = k == n and bool(torch.equal(r.data[:mbytes], want))
+        del want
+    else:
+        ok = k == n and bool(torch.equal(r.data[:mbytes], data[:mbytes]))  # one message per record, in order
     ev = []
     for _ in range(reps):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        codec.reassemble(dg.wire, dg.dg_off)
+        codec.reassemble(wire, dg_off)
         e1.record()
         ev.append((e0, e1))
     torch.cuda.synchronize()
     codec.check()
     ms = float(np.median([a.elapsed_time(b) for a, b in ev]))
-    wire_b = int(dg.wire.numel())
+    wire_b = int(wire.numel())
     alg = 8 * (nd + 1) + wire_b + mbytes + 8 * (k + 1) + 16 * k + nd
     return {"datagrams": nd, "messages": k, "wire_bytes": wire_b, "message_bytes": mbytes, "round_trip_ok": ok,
             "reassemble_ms": round(ms, 4), "alg_bytes": alg, "gbps_algorithmic": round(alg / (ms * 1e-3) / 1e9, 1),
             "note": "UDPTransport.Receive + DataReassembler.ProcessFragment (pkg/transport/transport.go:253-317, "
-                    "fragmentation.go:49-183) batched; datagrams from sym_fragment_write, send order"}
+                    "fragmentation.go:49-183) batched; datagrams from sym_fragment_write, "
+                    + (f"shuffled within windows of {window}" if window else "send order")}
 
 
 def crypto_leg(codec: Codec, data: torch.Tensor, rec_off: torch.Tensor, dev, reps: int) -> dict:
@@ -1040,7 +1070,7 @@ def summary_of(line: dict) -> dict:
             out[k] = {"gbps": x["gbps_algorithmic"], "frac": rf.get("frac"),
                       "frac_of": "dec" if rf.get("kernel", "").startswith("decode") else "enc", "enc_ms": x["encode_ms"], "dec_ms": x["decode_ms"],
                       "ms_per_pair": x["ms_per_pair"]}
-    for k in ("reassembly", "reassembly_config3"):
+    for k in ("reassembly", "reassembly_config3", "reassembly_config3_reordered"):
         if k in line:
             out[k] = {"gbps": line[k]["gbps_algorithmic"], "frac": frac(line[k]["gbps_algorithmic"]),
                       "ms": line[k]["reassemble_ms"]}
@@ -1349,9 +1379,13 @@ def main():
         e3 = codec.encode(b3.schema, f3, v3, var_total=b3.encoded_size() - b3.n * b3.schema.overhead)
         del b3, f3, v3
         rc3 = reassembly_leg(codec, e3.data, e3.offsets, dev, args.reassembly_reps)
-        rc3["note"] = ("config 3 (V log-uniform 16-4096 B) packetized: records over 1369 payload bytes span "
-                       "several datagrams, so the general path runs (hash grouping, radix sort, group passes)")
+        rc3["note"] = ("config 3 (V log-uniform 16-4096 B) packetized, send order: records over 1369 payload bytes "
+                       "span several datagrams; the parse recognises the packetizer's runs, so no regrouping")
         line["reassembly_config3"] = rc3
+        rr = reassembly_leg(codec, e3.data, e3.offsets, dev, args.reassembly_reps, window=64)
+        rr["note"] = ("config 3 packetized, datagrams shuffled within windows of 64: the general path (hash "
+                      "grouping, radix sort, group passes, the exclusive scan in arrival order)")
+        line["reassembly_config3_reordered"] = rr
         del e3
     if world == 1 and args.trace_reps > 0:
         t3 = config3_leg(codec, dev, args.trace_reps, datagen.config3_trace())

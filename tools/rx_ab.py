@@ -2,8 +2,10 @@
 
   python tools/rx_ab.py [--variants 0,3] [--rounds 10]
 
-Workloads: N3 reassembly of config 3 packetized (the general path: multi-datagram messages, segments of
-~640 bytes) and of config 2 packetized (the simple path), and the N1 firewall (kept records gathered).
+Workloads: N3 reassembly of config 3 packetized (multi-datagram messages, segments of ~640 bytes: the
+packetizer-runs path), of config 2 packetized (single-datagram messages) and of config 3 packetized with
+the datagrams shuffled within windows of 64 (the general path), and the N1 firewall (kept records
+gathered).
 Each round runs every variant once per workload, HIP events around each call; prints median / min per
 variant and reports any defined output (message bytes, the first nmsg+1 offsets, ...) of a variant that
 differs from the first variant's.
@@ -12,6 +14,7 @@ import argparse
 import os
 import statistics
 import sys
+from types import SimpleNamespace
 
 import numpy as np
 import torch
@@ -22,6 +25,7 @@ os.environ.setdefault("SYMHIP_LIBRARY", os.path.join(ROOT, "tools", "lib", "libs
 
 from arpc_amd import datagen  # noqa: E402
 from arpc_amd.codec import Codec, to_device  # noqa: E402
+from bench import byte_gather  # noqa: E402
 
 
 def main():
@@ -34,12 +38,24 @@ def main():
     dev = torch.device("cuda", 0)
     codec = Codec(dev)
     work = {}
-    for name, cfg in (("rx_config3", datagen.CONFIG3), ("rx_config2", datagen.CONFIG2)):
+    for name, cfg, window in (("rx_config3", datagen.CONFIG3, 0), ("rx_config2", datagen.CONFIG2, 0),
+                              ("rx_config3_w64", datagen.CONFIG3, 64)):
         b = datagen.make_batch(**cfg)
         f, v = to_device(b, dev)
         e = codec.encode(b.schema, f, v, var_total=b.encoded_size() - b.n * b.schema.overhead)
         rpc = torch.arange(b.n, dtype=torch.int64, device=dev)
         dg = codec.fragment(e.data, e.offsets, rpc)
+        if window:  # bench.py reassembly_leg's reordering
+            nd = dg.dg_off.numel() - 1
+            g = torch.Generator(device=dev)
+            g.manual_seed(7)
+            key = torch.div(torch.arange(nd, device=dev), window, rounding_mode="floor").double() + \
+                torch.rand(nd, device=dev, dtype=torch.float64, generator=g)
+            perm = torch.argsort(key)
+            lens = (dg.dg_off[1:] - dg.dg_off[:-1])[perm]
+            off = torch.zeros(nd + 1, dtype=torch.int64, device=dev)
+            off[1:] = torch.cumsum(lens, 0)
+            dg = SimpleNamespace(wire=byte_gather(dg.wire, dg.dg_off[:-1][perm], lens), dg_off=off)
         torch.cuda.synchronize()
         work[name] = (lambda dg=dg: codec.reassemble(dg.wire, dg.dg_off),
                       lambda m: (lambda k: (m.data[:int(m.offsets[k].item())], m.offsets[:k + 1], m.rpc_id[:k],

@@ -2,7 +2,8 @@
 
   python tools/rx_hostbound.py [--reps 10]
 
-For config 3 (general path) and config 2 (simple path) packetized: the call's host time (perf_counter
+For config 3 (packetizer runs), config 2 (single-datagram messages) and config 3 with the datagrams
+shuffled within windows of 64 (the general path, as bench.py's reassembly_config3_reordered) packetized: the call's host time (perf_counter
 around codec.reassemble, no sync) and its GPU time (HIP events around it), once as is and once queued
 behind a ~3 ms spin kernel (torch.cuda._sleep), so that every launch of the call is submitted before
 the GPU reaches the first one.  If the second GPU time is much shorter, the host's submission rate,
@@ -13,6 +14,7 @@ import os
 import statistics
 import sys
 import time
+from types import SimpleNamespace
 
 import torch
 
@@ -21,21 +23,38 @@ sys.path.insert(0, ROOT)
 
 from arpc_amd import datagen  # noqa: E402
 from arpc_amd.codec import Codec, to_device  # noqa: E402
+from bench import byte_gather  # noqa: E402
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--only", default="", help="run only the workloads whose name contains this")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     codec = Codec(dev)
-    for name, cfg in (("config3", datagen.CONFIG3), ("config2", datagen.CONFIG2)):
+    for name, cfg, window in (("config3", datagen.CONFIG3, 0), ("config2", datagen.CONFIG2, 0),
+                              ("config3 reordered (windows of 64)", datagen.CONFIG3, 64)):
+        if a.only and a.only not in name:
+            continue
         b = datagen.make_batch(**cfg)
         f, v = to_device(b, dev)
         e = codec.encode(b.schema, f, v, var_total=b.encoded_size() - b.n * b.schema.overhead)
         rpc = torch.arange(b.n, dtype=torch.int64, device=dev)
         dg = codec.fragment(e.data, e.offsets, rpc)
         del f, v
+        if window:  # bench.py reassembly_leg's reordering
+            nd = dg.dg_off.numel() - 1
+            g = torch.Generator(device=dev)
+            g.manual_seed(7)
+            key = torch.div(torch.arange(nd, device=dev), window, rounding_mode="floor").double() + \
+                torch.rand(nd, device=dev, dtype=torch.float64, generator=g)
+            perm = torch.argsort(key)
+            lens = (dg.dg_off[1:] - dg.dg_off[:-1])[perm]
+            wire = byte_gather(dg.wire, dg.dg_off[:-1][perm], lens)
+            off = torch.zeros(nd + 1, dtype=torch.int64, device=dev)
+            off[1:] = torch.cumsum(lens, 0)
+            dg = type(dg)(wire, off, *dg[2:]) if hasattr(dg, "_fields") else SimpleNamespace(wire=wire, dg_off=off)
         codec.reassemble(dg.wire, dg.dg_off)
         torch.cuda.synchronize()
         for behind in (False, True):
