@@ -8,9 +8,9 @@
 //
 // The reassembler keeps one state per RPCID and its decisions for one RPCID depend only on that
 // RPCID's datagrams in arrival order, so the batch is regrouped rather than replayed:
-//  1. parse (thread per datagram): header checks, and the RPCID inserted into an open-addressing
-//     hash table (agent-scope CAS) that also keeps each RPCID's first arrival (atomicMin); that
-//     first arrival index is the group key, so groups sort in order of first appearance and an
+//  1. parse (thread per datagram): header checks; then the RPCID inserted into an open-addressing
+//     hash table (agent-scope CAS), whose claiming arrival's index is the group key -- or, when the
+//     RPCIDs never decrease, the run head -- so groups sort roughly in order of appearance and an
 //     in-order stream keeps its arrival order through every later pass (coalesced);
 //  2. a stable LSD radix sort of (group key, arrival index) on ~log2(n)+1 key bits, 8 bits a pass
 //     (sort_*_kernel below): each group becomes a contiguous run in arrival order;
@@ -24,10 +24,10 @@
 //  5. the group pass again, now writing message offsets / RPCIDs / completing datagrams and the
 //     message's payload segments (wire offset, length) in (seq, fragment index) order;
 //  6. the segment gather of raw_fields.hip copies the payloads into the message stream.
-// Most batches are "simple" (every DataPacket one whole message) and finish after step 1 with a
-// scan, an emit and the gather.  The call never waits on the host: steps 1a-6 are queued for every
-// batch and each of their kernels reads the parse's device flag first and exits at once for a
-// simple batch (the stream stays asynchronous and capturable).
+// Most batches are "simple" (every DataPacket one whole message) or packetizer "runs" (parse_kernel)
+// and finish after step 1 with an emit and the gather.  The call never waits on the host: steps 1a-6
+// are queued for every batch and each of their kernels reads the parse's device flags first and
+// exits at once for those (the stream stays asynchronous and capturable).
 
 #include "../../include/symphony_hip.h"
 #include "codec.hpp"
@@ -74,7 +74,7 @@ struct Args {
     u64* table;
     u64 tmask;
     u32 special, nodata;   // table slot of the RPCID == kEmpty; group key of non-DataPackets (= n)
-    u32* first;            // per table slot (+1 for `special`): the RPCID's first arrival index
+    u32* first;            // per table slot (+1 for `special`): the group key, the claiming arrival's index
     u32* slot;             // per datagram: its RPCID's table slot
     u64* rpc;
     u64* meta;
@@ -112,14 +112,13 @@ __device__ __forceinline__ bool gated_off(const unsigned* gate) { return *gate =
 // nor runs (emit_kernel), i.e. [0] && ([2] || [3]) (uniform).
 __device__ __forceinline__ bool general_off(const unsigned* flags) { return flags[0] == 0 || (flags[2] | flags[3]) == 0; }
 
-// ---- 1a'. the hash table and first-arrival slots set to "empty" (general path, RPCIDs out of order)
+// ---- 1a'. the hash table set to "empty" (general path, RPCIDs out of order)
 __global__ __launch_bounds__(256) void init_kernel(u64* table, u32* first, u64 ts, const unsigned* gate,
                                                    const unsigned* nonmono) {
     if (general_off(gate) || gated_off(nonmono)) return;
-    for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; i <= ts; i += (u64)gridDim.x * 256) {
-        if (i < ts) table[i] = kEmpty;
-        first[i] = ~0u;
-    }
+    for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; i < ts; i += (u64)gridDim.x * 256) table[i] = kEmpty;
+    if (blockIdx.x == 0 && threadIdx.x == 0) first[ts] = ~0u;  // (the special slot's key; the others are
+                                                               // written by the CAS that claims the slot)
 }
 
 // When every datagram is a DataPacket and the RPCIDs never decrease, each RPCID's datagrams form one
@@ -469,35 +468,80 @@ __global__ __launch_bounds__(256) void parse_kernel(Args a, unsigned* flags) {
     if (threadIdx.x == 0) raw::publish_tile_total(a.agg, a.super_p, blockIdx.x, t);
 }
 
-// ---- 1a. general path: the RPCID into an open-addressing hash table (agent-scope CAS) that
-// also keeps each RPCID's first arrival (atomicMin); that first arrival index is the group key,
-// so groups sort in order of first appearance and an in-order stream keeps its arrival order
-// through every later pass (coalesced).  The per-arrival triples are recomputed by group pass 0.
+// ---- 1a. general path: the RPCID into an open-addressing hash table (agent-scope CAS); the
+// thread whose CAS claims the slot writes its arrival index into first[slot], and that index is the
+// group key (any one arrival of the RPCID serves: every output is placed by the arrival-order scan,
+// so the order of the groups only matters for locality -- and the claiming arrival is usually an
+// early one, so the groups still sort roughly in order of appearance).  The datagrams of one
+// workgroup first meet in an LDS table, and only one of them per RPCID goes to the global table
+// (round 6: the batch's ~2.7M random atomics, one CAS and one atomicMin per datagram, ran at the
+// chip's atomic rate, ~120 us for config 3 shuffled within windows of 64).  The per-arrival triples
+// are recomputed by group pass 0.
+constexpr int kLocalSlots = 512;
+constexpr u32 kKeyLater = ~0u;  // gid of a datagram whose RPCID another workgroup claimed (keys are <= n)
 __global__ __launch_bounds__(256) void hash_kernel(Args a, const unsigned* gate) {
     if (general_off(gate)) return;
     const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
-    if (i >= a.n) return;
-    a.cnt[i] = Pair{0, 0};
-    a.idx[i] = (u32)i;
-    if (!*a.nonmono) return;  // runs of equal RPCIDs: key_kernel takes the run heads
-    u32 g = kNoSlot;  // table slot
-    if (a.status[i] == SYM_RX_PENDING) {
-        const u64 r = a.rpc[i];
-        if (r == kEmpty) {
-            g = a.special;
-        } else {  // open addressing; the table has >= 2n slots, so a free slot is always found
-            u64 h = mix64(r) & a.tmask;
-            for (;;) {
-                const u64 prev = atomicCAS((unsigned long long*)&a.table[h], (unsigned long long)kEmpty,
-                                           (unsigned long long)r);
-                if (prev == kEmpty || prev == r) break;
-                h = (h + 1) & a.tmask;
+    if (i < a.n) {
+        a.cnt[i] = Pair{0, 0};
+        a.idx[i] = (u32)i;
+    }
+    if (!*a.nonmono) return;  // (uniform) runs of equal RPCIDs: key_kernel takes the run heads
+    __shared__ u64 s_key[kLocalSlots];
+    __shared__ u32 s_slot[kLocalSlots], s_gkey[kLocalSlots];
+    for (int k = threadIdx.x; k < kLocalSlots; k += 256) s_key[k] = kEmpty;
+    __syncthreads();
+    const bool pend = i < a.n && a.status[i] == SYM_RX_PENDING;
+    const u64 r = pend ? a.rpc[i] : kEmpty;
+    int e = 0;
+    bool lead = false;  // the workgroup's first thread to hold this RPCID
+    if (r != kEmpty) {
+        u32 h = (u32)(mix64(r) >> 40) & (kLocalSlots - 1);
+        for (;;) {
+            const u64 prev = atomicCAS((unsigned long long*)&s_key[h], (unsigned long long)kEmpty, (unsigned long long)r);
+            if (prev == kEmpty) {
+                lead = true;
+                break;
             }
-            g = (u32)h;
+            if (prev == r) break;
+            h = (h + 1) & (kLocalSlots - 1);
+        }
+        e = (int)h;
+    }
+    u32 g = kNoSlot;  // table slot
+    if (lead) {       // open addressing; the table has >= 2n slots, so a free slot is always found
+        u64 h = mix64(r) & a.tmask;
+        bool claimed = false;
+        for (;;) {
+            const u64 prev = atomicCAS((unsigned long long*)&a.table[h], (unsigned long long)kEmpty, (unsigned long long)r);
+            if (prev == kEmpty) {
+                a.first[h] = (u32)i;  // the group key, for other workgroups' datagrams (key_kernel)
+                claimed = true;
+                break;
+            }
+            if (prev == r) break;
+            h = (h + 1) & a.tmask;
+        }
+        g = (u32)h;
+        s_slot[e] = g;
+        s_gkey[e] = claimed ? (u32)i : kKeyLater;
+    }
+    __syncthreads();
+    u32 key = a.nodata;
+    if (pend) {
+        if (r == kEmpty) {  // the RPCID equal to the empty marker: its own slot, claimed the same way
+            g = a.special;
+            atomicCAS(&a.first[g], ~0u, (u32)i);
+            key = kKeyLater;
+        } else {
+            if (!lead) g = s_slot[e];
+            key = s_gkey[e];
         }
     }
-    a.slot[i] = g;
-    if (g != kNoSlot) atomicMin(&a.first[g], (u32)i);
+    if (i < a.n) {
+        a.slot[i] = g;
+        a.gid[i] = key;  // kKeyLater: claimed by another workgroup, key_kernel reads first[slot]
+    }
 }
 
 // ---- simple batches and runs (parse_kernel): the messages in arrival order, from the scan of the
@@ -549,8 +593,8 @@ __global__ __launch_bounds__(256) void emit_kernel(Args a, const unsigned* flags
     }
 }
 
-// ---- 1b. group key = the RPCID's first arrival: groups sort in order of first appearance, so an
-// in-order stream keeps its arrival order and every later pass reads and writes it coalesced
+// ---- 1b. group key: the run head when the RPCIDs never decrease, so an in-order stream keeps its
+// arrival order and every later pass reads and writes it coalesced; else the hash table's key
 __global__ __launch_bounds__(256) void key_kernel(Args a, const unsigned* gate) {
     if (general_off(gate)) return;
     const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
@@ -581,16 +625,26 @@ __global__ __launch_bounds__(256) void key_kernel(Args a, const unsigned* gate) 
             h = (u64)hi;
         }
         a.gid[i] = (u32)h;  // non-decreasing
-    } else if (i < a.n) {
-        const u32 s = a.slot[i];
-        const u32 g = s == kNoSlot ? a.nodata : a.first[s];
-        a.gid[i] = g;
-        if (i > 0) {
-            const u32 sp = a.slot[i - 1];
-            down = g < (sp == kNoSlot ? a.nodata : a.first[sp]);
+    } else if (*a.nonmono) {  // (uniform) the key the hash kernel left -- or its slot's, claimed by
+                              // another workgroup -- and the previous one from LDS
+        __shared__ u32 s_gid[256];
+        auto key_of = [&](u64 j) {
+            const u32 k = a.gid[j];
+            return k == kKeyLater ? a.first[a.slot[j]] : k;
+        };
+        const u32 g = i < a.n ? key_of(i) : 0u;
+        s_gid[threadIdx.x] = g;
+        __syncthreads();
+        if (i < a.n) {
+            if (a.gid[i] != g) a.gid[i] = g;
+            if (i > 0) down = g < (threadIdx.x > 0 ? s_gid[threadIdx.x - 1] : key_of(i - 1));
         }
     }
-    if (__syncthreads_or(down) && threadIdx.x == 0) atomicOr(a.unsorted, 1u);
+    // the atomic only while the flag is clear: one per workgroup of a shuffled batch serialised on the
+    // word (~11 ns each at the memory side, ~55 us per batch)
+    if (__syncthreads_or(down) && threadIdx.x == 0 &&
+        __hip_atomic_load(a.unsorted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+        atomicOr(a.unsorted, 1u);
 }
 
 __device__ inline bool seq_complete(const SeqState& x) {
@@ -631,15 +685,20 @@ __device__ __forceinline__ void group_one(const Args& a, u64 q0, u64* lb, u64* l
     u64 e = q0 + 1;
     while (e < a.n && a.gs[e] == g) ++e;
     const u64 k = e - q0;                        // sequence numbers >= k can never complete
-    {  // the run the packetizer sends: one message of k packets, SeqNumber 0..k-1 in order,
-       // TotalPackets k, one fragment each.  The machine below completes it at its last packet
-       // with the packets in arrival order as the segments; say so without the per-sequence state.
-        bool fast = true;
-        u64 bytes = 0;
+    {  // one message of k packets, TotalPackets k, one fragment each, SeqNumbers 0..k-1 -- in order
+       // (the packetizer's run), or in any order for k <= 64 (a reordered one, round 6).  The machine
+       // below completes it at its last arrival (only then are all k sequence numbers in) with the
+       // packets in sequence order as the segments; say so without the per-sequence state.
+        bool fast = true, inorder = true;
+        u64 bytes = 0, seen = 0;
         for (u64 t = 0; t < k && fast; ++t) {
             const u32 j = a.is[q0 + t];
             const u64 m = a.meta[j];
-            fast = m_seq(m) == t && m_total(m) == k && m_fidx(m) == 0 && !m_more(m);
+            const u32 sq = m_seq(m);
+            inorder = inorder && sq == t;
+            fast = m_total(m) == k && m_fidx(m) == 0 && !m_more(m) &&
+                   (inorder || (k <= 64 && sq < k && !((seen >> sq) & 1)));
+            if (k <= 64) seen |= (u64)1 << (sq & 63);
             bytes += a.plen[j];
         }
         if (fast) {
@@ -653,13 +712,23 @@ __device__ __forceinline__ void group_one(const Args& a, u64 q0, u64* lb, u64* l
                 a.msg_off[mi] = pp.bytes;
                 a.msg_rpc[mi] = a.rpc[jl];
                 a.msg_dg[mi] = jl;
-                u64 at = pp.bytes;  // the segment's output offset
+                u64 at = pp.bytes;  // the segment's output offset (in order: a running sum)
                 for (u64 t = 0; t < k; ++t) {
                     const u32 j = a.is[q0 + t];
                     const u32 pl = a.plen[j];
-                    a.seg_src[sb + t] = a.dg_off[j] + kHdr;
-                    a.seg_len[sb + t] = pl;
-                    if (((sb + t) & 255) == 0) a.seg_pre[(sb + t) >> 8] = Pair{at, 0};
+                    u64 sg = sb + t;
+                    if (!inorder) {  // its place in sequence order, behind the packets of lower numbers
+                        const u32 sq = m_seq(a.meta[j]);
+                        sg = sb + sq;
+                        at = pp.bytes;
+                        for (u64 t2 = 0; t2 < k; ++t2) {
+                            const u32 j2 = a.is[q0 + t2];
+                            if (m_seq(a.meta[j2]) < sq) at += a.plen[j2];
+                        }
+                    }
+                    a.seg_src[sg] = a.dg_off[j] + kHdr;
+                    a.seg_len[sg] = pl;
+                    if ((sg & 255) == 0) a.seg_pre[sg >> 8] = Pair{at, 0};
                     at += pl;
                 }
             }
