@@ -379,11 +379,14 @@ int sym_firewall_filter(sym_ctx* ctx, const uint8_t* d_in, const uint64_t* d_rec
  * datagram: its header carries the packet type and addresses Receive returns); *d_nmsg; all
  * arrays sized for n messages (n+1 offsets).  d_status[n]: SYM_RX_*.  n < 2^31.
  * When every DataPacket is a whole message (TotalPackets 1, one fragment) the messages are the
- * DataPackets in arrival order, found on the device without grouping.  The general path --
- * grouping, sort, the ProcessFragment state machine -- is queued too and its kernels exit at once
- * for such a batch: the call is asynchronous on `stream` like the others (no host read).  It runs
- * on a stream of the ctx forked from `stream` after the parse and joined back before the call's
- * last operation (events; stream capture follows both). */
+ * DataPackets in arrival order; when every datagram is a DataPacket, the RPCIDs never decrease and
+ * each run of equal RPCIDs is one message as sym_fragment_write sends it (sequence numbers 0..k-1
+ * in order, TotalPackets k, one fragment each), the messages are the runs in arrival order.  Both
+ * are found on the device without grouping.  The general path -- grouping, sort, the
+ * ProcessFragment state machine -- is queued too and its kernels exit at once for such a batch:
+ * the call is asynchronous on `stream` like the others (no host read).  It runs on a stream of the
+ * ctx forked from `stream` after the parse and joined back before the call's last operation
+ * (events; stream capture follows both). */
 #define SYM_RX_CONSUMED 0   /* part of a returned message */
 #define SYM_RX_PENDING 1    /* still held by the reassembler after the batch */
 #define SYM_RX_NOT_DATA 2   /* not a Request / Response DataPacket: not reassembled */
