@@ -83,8 +83,10 @@ struct Args {
     u32* idx;
     const u32* gs;         // sorted group keys / arrival indices (gid / idx themselves when the
     const u32* is;         // keys came out non-decreasing: *unsorted == 0 and the sort did nothing)
-    unsigned* unsorted;
+    unsigned* unsorted;       // (sharded flag words, flag_set)
     const unsigned* nonmono;  // not every datagram a DataPacket with RPCIDs non-decreasing: hash them
+    unsigned* gen;            // single words written by emit_kernel: the general path runs; nonmono
+    unsigned* nm;
     SeqState* state;
     uint8_t* status;
     Pair* cnt;             // per arrival (n+1): (message bytes, segments << 32 | messages)
@@ -105,17 +107,38 @@ struct Args {
 __device__ inline void block_scan_pair(Pair v, Pair& excl, Pair& tile_total);
 __host__ __device__ inline u64 tiles(u64 m) { return (m + 255) / 256; }
 
+// The batch's flag words, each in kShards copies on lines of their own (flag w of shard s at flags[32 s
+// + w], all zeroed per call): [0] not simple, [1] keys out of order (key_kernel), [2] not every
+// datagram a DataPacket with RPCIDs non-decreasing, [3] a run that is not the packetizer's.  A
+// workgroup raises a flag in its own shard (blockIdx % kShards), and a reader ORs the shards.  (Round
+// 6: with one word per flag the ~2000 workgroups resident at once all found it clear and all
+// atomically set it, serialised at the memory side: ~17 us in key_kernel and ~20 in the parse of a
+// batch that sets a flag everywhere.)  The general path's kernels run only for a batch that is
+// neither simple nor runs (emit_kernel), i.e. [0] && ([2] || [3]) (uniform).
+constexpr int kShards = 16;
+constexpr size_t kFlagBytes = kShards * 128;
+__device__ __forceinline__ bool flag_set(const unsigned* w) {  // w: flag word of shard 0
+    unsigned v = 0;
+#pragma unroll
+    for (int s = 0; s < kShards; ++s) v |= w[32 * s];
+    return v != 0;
+}
+__device__ __forceinline__ void flag_raise(unsigned* w, bool any) {  // whole workgroup; the atomic only while clear
+    if (__syncthreads_or(any) && threadIdx.x == 0) {
+        unsigned* p = w + 32 * (blockIdx.x % kShards);
+        if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) atomicOr(p, 1u);
+    }
+}
+// The general path's kernels read one word instead, `gen` (and `nm`, flag [2]), which emit_kernel's
+// first thread writes from the shards before the general path is forked: an empty launch of a
+// single-datagram or runs batch then costs one load per workgroup, not 16-48 (those launches run
+// beside the payload copy and take CU slots from it while they last).
 __device__ __forceinline__ bool gated_off(const unsigned* gate) { return *gate == 0; }
-// The parse's words, consecutive from `flags` (all zeroed per call): [0] not simple, [1] keys out of
-// order (key_kernel), [2] not every datagram a DataPacket with RPCIDs non-decreasing, [3] a run that
-// is not the packetizer's.  The general path's kernels run only for a batch that is neither simple
-// nor runs (emit_kernel), i.e. [0] && ([2] || [3]) (uniform).
-__device__ __forceinline__ bool general_off(const unsigned* flags) { return flags[0] == 0 || (flags[2] | flags[3]) == 0; }
 
 // ---- 1a'. the hash table set to "empty" (general path, RPCIDs out of order)
-__global__ __launch_bounds__(256) void init_kernel(u64* table, u32* first, u64 ts, const unsigned* gate,
-                                                   const unsigned* nonmono) {
-    if (general_off(gate) || gated_off(nonmono)) return;
+__global__ __launch_bounds__(256) void init_kernel(u64* table, u32* first, u64 ts, const unsigned* gen,
+                                                   const unsigned* nm) {
+    if (gated_off(gen) || gated_off(nm)) return;
     for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; i < ts; i += (u64)gridDim.x * 256) table[i] = kEmpty;
     if (blockIdx.x == 0 && threadIdx.x == 0) first[ts] = ~0u;  // (the special slot's key; the others are
                                                                // written by the CAS that claims the slot)
@@ -169,8 +192,8 @@ __device__ __forceinline__ void sort_hist_tile(const u32* keys, u64 n, int shift
 }
 
 __global__ __launch_bounds__(256) void sort_hist_kernel(const u32* keys, u64 n, int shift, u32* hist, u64 ntiles,
-                                                        const unsigned* gate) {
-    if (gated_off(gate)) return;
+                                                        const unsigned* gen, const unsigned* unsorted) {
+    if (gated_off(gen) || !flag_set(unsorted)) return;
     sort_hist_tile(keys, n, shift, hist, ntiles, blockIdx.x);
 }
 
@@ -202,8 +225,9 @@ __device__ __forceinline__ void sort_rowscan_row(u32* hist, u64 ntiles, u32* row
     if (threadIdx.x == 0) rowtot[digit] = carry;
 }
 
-__global__ __launch_bounds__(256) void sort_rowscan_kernel(u32* hist, u64 ntiles, u32* rowtot, const unsigned* gate) {
-    if (gated_off(gate)) return;
+__global__ __launch_bounds__(256) void sort_rowscan_kernel(u32* hist, u64 ntiles, u32* rowtot, const unsigned* gen,
+                                                           const unsigned* unsorted) {
+    if (gated_off(gen) || !flag_set(unsorted)) return;
     sort_rowscan_row(hist, ntiles, rowtot, blockIdx.x);
 }
 
@@ -261,8 +285,8 @@ __device__ __forceinline__ void sort_scatter_tile(const u32* kin, const u32* vin
 
 __global__ __launch_bounds__(256) void sort_scatter_kernel(const u32* kin, const u32* vin, u32* kout, u32* vout, u64 n,
                                                            int shift, const u32* hist, u64 ntiles, const u32* rowtot,
-                                                           const unsigned* gate) {
-    if (gated_off(gate)) return;
+                                                           const unsigned* gen, const unsigned* unsorted) {
+    if (gated_off(gen) || !flag_set(unsorted)) return;
     sort_scatter_tile(kin, vin, kout, vout, n, shift, hist, ntiles, rowtot, blockIdx.x);
 }
 
@@ -280,6 +304,7 @@ struct SortArgs {
     u32* hist;
     u64 ntiles;
     u32* rowtot;
+    const unsigned* gen;
     const unsigned* unsorted;
     unsigned* bar;  // arrivals, zeroed per call
     unsigned* err;
@@ -308,7 +333,7 @@ __device__ __forceinline__ bool grid_barrier(unsigned* bar, unsigned target, uns
     return ok != 0;
 }
 __global__ __launch_bounds__(256) void sort_all_kernel(SortArgs s) {
-    if (gated_off(s.unsorted)) return;  // uniform: every workgroup leaves at once
+    if (gated_off(s.gen) || !flag_set(s.unsorted)) return;  // uniform: every workgroup leaves at once
     const u64 G = gridDim.x;
     unsigned arrivals = 0;
     int cur = 0;
@@ -453,16 +478,11 @@ __global__ __launch_bounds__(256) void parse_kernel(Args a, unsigned* flags) {
         }
     }
     if (i <= a.n) a.cnt[i] = c;
-    // one flag check per workgroup, and the atomic only while the flag is still clear: a wave-level
-    // atomicOr on one word serialised ~20k atomics per batch of multi-datagram messages (~200 us)
-    auto raise = [&](bool any, int w) {
-        if (__syncthreads_or(any) && threadIdx.x == 0 &&
-            __hip_atomic_load(flags + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
-            atomicOr(flags + w, 1u);
-    };
-    raise(!simple, 0);
-    raise(bad, 2);
-    raise(odd, 3);
+    // one raise per workgroup and flag (flag_raise; a wave-level atomicOr on one word serialised ~20k
+    // atomics per batch of multi-datagram messages, ~200 us)
+    flag_raise(flags, !simple);
+    flag_raise(flags + 2, bad);
+    flag_raise(flags + 3, odd);
     Pair e, t;  // this tile's totals, for the scan of the triples (simple batches and runs)
     block_scan_pair(c, e, t);
     if (threadIdx.x == 0) raw::publish_tile_total(a.agg, a.super_p, blockIdx.x, t);
@@ -480,13 +500,13 @@ __global__ __launch_bounds__(256) void parse_kernel(Args a, unsigned* flags) {
 constexpr int kLocalSlots = 512;
 constexpr u32 kKeyLater = ~0u;  // gid of a datagram whose RPCID another workgroup claimed (keys are <= n)
 __global__ __launch_bounds__(256) void hash_kernel(Args a, const unsigned* gate) {
-    if (general_off(gate)) return;
+    if (gated_off(gate)) return;
     const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
     if (i < a.n) {
         a.cnt[i] = Pair{0, 0};
         a.idx[i] = (u32)i;
     }
-    if (!*a.nonmono) return;  // (uniform) runs of equal RPCIDs: key_kernel takes the run heads
+    if (!*a.nm) return;  // (uniform) runs of equal RPCIDs: key_kernel takes the run heads
     __shared__ u64 s_key[kLocalSlots];
     __shared__ u32 s_slot[kLocalSlots], s_gkey[kLocalSlots];
     for (int k = threadIdx.x; k < kLocalSlots; k += 256) s_key[k] = kEmpty;
@@ -555,8 +575,13 @@ __global__ __launch_bounds__(256) void hash_kernel(Args a, const unsigned* gate)
 __global__ __launch_bounds__(256) void emit_kernel(Args a, const unsigned* flags, u64* nmsg, u64* nseg,
                                                    Pair* seg_pre) {
     const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
-    const bool simple = flags[0] == 0;
-    if (!simple && (flags[2] | flags[3]) != 0) {  // the general path's batch
+    const bool simple = !flag_set(flags), nonmono = flag_set(a.nonmono);
+    const bool general = !simple && (nonmono || flag_set(flags + 3));
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // the general path's gates (read after the fork)
+        *a.gen = general;
+        *a.nm = nonmono;
+    }
+    if (general) {  // the general path's batch
         if (i == 0) *nseg = 0;
         return;
     }
@@ -596,10 +621,11 @@ __global__ __launch_bounds__(256) void emit_kernel(Args a, const unsigned* flags
 // ---- 1b. group key: the run head when the RPCIDs never decrease, so an in-order stream keeps its
 // arrival order and every later pass reads and writes it coalesced; else the hash table's key
 __global__ __launch_bounds__(256) void key_kernel(Args a, const unsigned* gate) {
-    if (general_off(gate)) return;
+    if (gated_off(gate)) return;
     const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
     bool down = false;  // a key below its predecessor's: the batch needs the sort
-    if (i < a.n && !*a.nonmono) {  // the run head: every datagram is a pending DataPacket here
+    const bool nonmono = *a.nm != 0;
+    if (i < a.n && !nonmono) {  // the run head: every datagram is a pending DataPacket here
         // The RPCIDs never decrease on this path, so the head is the first index holding r: one load
         // when i starts its run (the common case), else a gallop back (steps 1, 2, 4, ...) to an index
         // below the run, then a binary search -- O(log run) loads, so one RPCID repeated over a whole
@@ -625,7 +651,7 @@ __global__ __launch_bounds__(256) void key_kernel(Args a, const unsigned* gate) 
             h = (u64)hi;
         }
         a.gid[i] = (u32)h;  // non-decreasing
-    } else if (*a.nonmono) {  // (uniform) the key the hash kernel left -- or its slot's, claimed by
+    } else if (nonmono) {  // (uniform) the key the hash kernel left -- or its slot's, claimed by
                               // another workgroup -- and the previous one from LDS
         __shared__ u32 s_gid[256];
         auto key_of = [&](u64 j) {
@@ -640,11 +666,7 @@ __global__ __launch_bounds__(256) void key_kernel(Args a, const unsigned* gate) 
             if (i > 0) down = g < (threadIdx.x > 0 ? s_gid[threadIdx.x - 1] : key_of(i - 1));
         }
     }
-    // the atomic only while the flag is clear: one per workgroup of a shuffled batch serialised on the
-    // word (~11 ns each at the memory side, ~55 us per batch)
-    if (__syncthreads_or(down) && threadIdx.x == 0 &&
-        __hip_atomic_load(a.unsorted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
-        atomicOr(a.unsorted, 1u);
+    flag_raise(a.unsorted, down);  // (one atomic per workgroup on one word had cost ~55 us per batch)
 }
 
 __device__ inline bool seq_complete(const SeqState& x) {
@@ -812,8 +834,8 @@ __device__ __forceinline__ void group_one(const Args& a, u64 q0, u64* lb, u64* l
 }
 template <int PASS>
 __global__ __launch_bounds__(256) void group_kernel(Args a, const unsigned* gate) {
-    if (general_off(gate)) return;
-    if (!*a.unsorted) {  // the keys were in order already: the sort left them in gid / idx
+    if (gated_off(gate)) return;
+    if (!flag_set(a.unsorted)) {  // the keys were in order already: the sort left them in gid / idx
         a.gs = a.gid;
         a.is = a.idx;
     }
@@ -854,7 +876,7 @@ __device__ inline void block_scan_pair(Pair v, Pair& excl, Pair& tile_total) {
 __global__ __launch_bounds__(256) void pair_scan_apply_kernel(const Pair* v, u64 m, const Pair* agg, const Pair* super,
                                                               Pair* out, u64* msg_off, u64* nmsg, u64* nseg,
                                                               Pair* seg_pre, const unsigned* gate) {
-    if (general_off(gate)) return;
+    if (gated_off(gate)) return;
     const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
     Pair e, t;
     block_scan_pair(i < m ? v[i] : Pair{0, 0}, e, t);
@@ -884,7 +906,7 @@ inline unsigned log2u(u64 t) {
 inline unsigned key_bits(u64 n) { return log2u(n + 1) + 1; }  // keys in [0, n]
 
 struct Layout {
-    size_t table, first, slot, rpc, meta, plen, gid, idx, gs, is, state, cnt, pre, agg, seg_src, seg_len, pre2, pre3, nseg, nseg2, flag, unsorted, nonmono, bar, sup_p, sup_c, agg_c, zero_bytes, hist, rowtot, total;
+    size_t table, first, slot, rpc, meta, plen, gid, idx, gs, is, state, cnt, pre, agg, seg_src, seg_len, pre2, pre3, nseg, nseg2, flag, unsorted, nonmono, gen, nm, bar, sup_p, sup_c, agg_c, zero_bytes, hist, rowtot, total;
 };
 
 inline u64 sort_tiles(u64 n) { return (n + kSortTile - 1) / kSortTile; }
@@ -921,14 +943,16 @@ inline Layout layout(u64 n) {
     // sort's barrier, then the group totals of the parse's tile totals, the group totals and tile
     // totals of the general path's triples: zeroed together, one memset per call
     const size_t sup = raw::super_bytes(tiles(n + 1));
-    L.zero_bytes = 128 + 2 * sup + (tiles(n + 1) + 1) * sizeof(Pair);
+    L.zero_bytes = 128 + kFlagBytes + 2 * sup + (tiles(n + 1) + 1) * sizeof(Pair);
     L.nseg2 = take(L.zero_bytes);
-    L.sup_p = L.nseg2 + 128;  // (its own lines: the atomics on the totals stay off the flags' line)
+    L.flag = L.nseg2 + 128;  // kShards lines of four flag words (flag_set)
+    L.sup_p = L.flag + kFlagBytes;  // (lines of their own: the atomics on the totals stay off the flags')
     L.sup_c = L.sup_p + sup;
     L.agg_c = L.sup_c + sup;
-    L.flag = L.nseg2 + 8;
-    L.unsorted = L.nseg2 + 12;  // (the flag words are consecutive: general_off)
-    L.nonmono = L.nseg2 + 16;
+    L.unsorted = L.flag + 4;
+    L.nonmono = L.flag + 8;
+    L.gen = L.nseg2 + 8;
+    L.nm = L.nseg2 + 12;
     L.bar = L.nseg2 + 24;
     L.hist = take((size_t)kDigits * sort_tiles(n) * 4);
     L.rowtot = take(kDigits * 4);
@@ -974,6 +998,9 @@ hipError_t launch_reassemble(const uint8_t* wire, const u64* dg_off, u64 n, uint
     a.seg_pre = (Pair*)(w + L.pre2);
     a.unsorted = (unsigned*)(w + L.unsorted);
     a.nonmono = (const unsigned*)(w + L.nonmono);
+    a.gen = (unsigned*)(w + L.gen);
+    a.nm = (unsigned*)(w + L.nm);
+    const unsigned* gen = a.gen;
     const dim3 b256(256);
     const unsigned* flag = (const unsigned*)(w + L.flag);
     const dim3 gq((unsigned)rx::tiles(n));
@@ -1014,27 +1041,28 @@ hipError_t launch_reassemble(const uint8_t* wire, const u64* dg_off, u64 n, uint
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(rx::parse_kernel, dim3((unsigned)nt), b256, 0, stream, a, (unsigned*)flag);
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(rx::emit_kernel, dim3((unsigned)nt), b256, 0, stream, a, flag, nmsg, nseg, (Pair*)(w + L.pre3));
+    if ((e = hipGetLastError()) != hipSuccess) return e;
     // The general path is queued for every batch; each of its kernels exits at once unless the
-    // parse set the flag (no host read: the call stays asynchronous).  It runs on `aux`, forked
-    // here and joined at the end, so for a simple batch its eight empty launches overlap the copy
-    // below.  The two branches share no buffer that both write for the same batch: every write of
-    // the simple branch past this point is for a simple batch (its zero segment count for a complex
-    // one excepted, in a word of its own), every write of the general branch for a complex one.
+    // emit's gate word says so (no host read: the call stays asynchronous).  It runs on `aux`,
+    // forked here (after the emit, which writes the gate words) and joined at the end, so for a
+    // single-datagram or runs batch its empty launches overlap the copy below.  The two branches
+    // share no buffer that both write for the same batch: every write of the main branch past this
+    // point is for a batch the general path skips (its zero segment count for the others excepted,
+    // in a word of its own), every write of the general branch for one it takes.
     hipStream_t gs = stream;
     if (aux && fork && join) {
         if ((e = hipEventRecord(fork, stream)) != hipSuccess) return e;
         if ((e = hipStreamWaitEvent(aux, fork, 0)) != hipSuccess) return e;
         gs = aux;
     }
-    hipLaunchKernelGGL(rx::emit_kernel, dim3((unsigned)nt), b256, 0, stream, a, flag, nmsg, nseg, (Pair*)(w + L.pre3));
-    if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = seg_tail(nseg, false, stream)) != hipSuccess) return e;
     hipLaunchKernelGGL(rx::init_kernel, dim3((unsigned)std::min<u64>(rx::tiles(TS + 1), 4096)), b256, 0, gs, a.table,
-                       a.first, TS, flag, a.nonmono);
+                       a.first, TS, gen, a.nm);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(rx::hash_kernel, gq, b256, 0, gs, a, flag);
+    hipLaunchKernelGGL(rx::hash_kernel, gq, b256, 0, gs, a, gen);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(rx::key_kernel, gq, b256, 0, gs, a, flag);
+    hipLaunchKernelGGL(rx::key_kernel, gq, b256, 0, gs, a, gen);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     {  // 2. the stable radix sort, ping-ponging between (gid, idx) and (gs, is); only when the keys
        // are out of order (set by key_kernel, so only for a batch on the general path)
@@ -1060,7 +1088,7 @@ hipError_t launch_reassemble(const uint8_t* wire, const u64* dg_off, u64 n, uint
             int& ncu = cus[dev & 15];
             if (ncu == 0 && (e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess)
                 return e;
-            rx::SortArgs sa{{kb[0], kb[1]}, {vb[0], vb[1]}, n, hist, st, rowtot, a.unsorted,
+            rx::SortArgs sa{{kb[0], kb[1]}, {vb[0], vb[1]}, n, hist, st, rowtot, gen, a.unsorted,
                             (unsigned*)(w + L.bar), err, bits};
             hipLaunchKernelGGL(rx::sort_all_kernel, dim3((unsigned)std::min<u64>(st, (u64)ncu)), b256, 0, gs, sa);
             if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -1068,24 +1096,25 @@ hipError_t launch_reassemble(const uint8_t* wire, const u64* dg_off, u64 n, uint
         } else {
             for (unsigned shift = 0; shift < bits; shift += 8, cur ^= 1) {
                 hipLaunchKernelGGL(rx::sort_hist_kernel, dim3((unsigned)st), b256, 0, gs, (const u32*)kb[cur], n,
-                                   (int)shift, hist, st, a.unsorted);
-                hipLaunchKernelGGL(rx::sort_rowscan_kernel, dim3(rx::kDigits), b256, 0, gs, hist, st, rowtot, a.unsorted);
+                                   (int)shift, hist, st, gen, a.unsorted);
+                hipLaunchKernelGGL(rx::sort_rowscan_kernel, dim3(rx::kDigits), b256, 0, gs, hist, st, rowtot, gen,
+                                   a.unsorted);
                 hipLaunchKernelGGL(rx::sort_scatter_kernel, dim3((unsigned)st), b256, 0, gs, (const u32*)kb[cur],
                                    (const u32*)vb[cur], kb[cur ^ 1], vb[cur ^ 1], n, (int)shift, (const u32*)hist, st,
-                                   (const u32*)rowtot, a.unsorted);
+                                   (const u32*)rowtot, gen, a.unsorted);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
             }
         }
         a.gs = kb[cur];
         a.is = vb[cur];
     }
-    hipLaunchKernelGGL(rx::group_kernel<0>, gq, b256, 0, gs, a, flag);
+    hipLaunchKernelGGL(rx::group_kernel<0>, gq, b256, 0, gs, a, gen);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(rx::pair_scan_apply_kernel, dim3((unsigned)nt), b256, 0, gs, (const Pair*)a.cnt, n + 1,
                        (const Pair*)a.agg_c, (const Pair*)a.super_c, (Pair*)(w + L.pre), msg_off, nmsg, nseg2,
-                       (Pair*)(w + L.pre2), flag);
+                       (Pair*)(w + L.pre2), gen);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(rx::group_kernel<1>, gq, b256, 0, gs, a, flag);
+    hipLaunchKernelGGL(rx::group_kernel<1>, gq, b256, 0, gs, a, gen);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = seg_tail(nseg2, true, gs)) != hipSuccess) return e;
     if (gs != stream) {
