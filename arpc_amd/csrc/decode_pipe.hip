@@ -1046,6 +1046,14 @@ hipError_t launch_decode_pipe(const DecodeParams& p, void* flags, unsigned epoch
         case 797: return launch_layout<PipeCfg{.sk = 1, .stg = 16384, .spec = true, .wpe = 8, .canon = true, .tilek = true}>(p, fl, epoch, stream, 1, 2);
         case 798: return launch_layout<PipeCfg{.sk = 1, .stg = 16384, .spec = true, .wpe = 8, .loc = true, .canon = true, .tilek = true}>(p, fl, epoch, stream, 1, 2);
         case 799: return launch_layout<PipeCfg{.sk = 1, .spec = true, .loc = true, .canon = true, .tilek = true}>(p, fl, epoch, stream, 1, 2);
+        // round 6, kv layouts with tile-key parsers (lighter): parsers on 1/4, 1/8, 3/8 of the CUs; a
+        // 2-tile scanner step; parser tiles per step 4 -- config 2 145.8 (default) vs 153.4 / 186.0 /
+        // 145.5 / 165.7 / 147.1 us (profiles/r06_kbench_tilek_parsers_c2.txt): the default kept
+        case 800: return launch_layout<PipeCfg{.sk = 1, .spec = true, .loc = true, .canon = true, .tilek = true}>(p, fl, epoch, stream, 1, 4);
+        case 801: return launch_layout<PipeCfg{.sk = 1, .spec = true, .loc = true, .canon = true, .tilek = true}>(p, fl, epoch, stream, 1, 8);
+        case 802: return launch_layout<PipeCfg{.sk = 1, .spec = true, .loc = true, .canon = true, .tilek = true}>(p, fl, epoch, stream, 3, 8);
+        case 803: return launch_layout<PipeCfg{.sk = 2, .spec = true, .loc = true, .canon = true, .tilek = true}>(p, fl, epoch, stream, 1, 4);
+        case 804: return launch_layout<PipeCfg{.sk = 1, .pr = 4, .spec = true, .loc = true, .canon = true, .tilek = true}>(p, fl, epoch, stream, 1, 4);
         default: break;
     }
 #endif

@@ -229,12 +229,28 @@ def test_reassembly_round_trip_gpu(gcodec, gdev, cfg, mtu):
 
 @pytest.mark.gpu
 def test_reassembly_large_shuffled_gpu(gcodec, gdev):
-    """More sort tiles (2048 datagrams each) than the one-launch sort has workgroups (one per CU):
-    every workgroup takes several tiles per phase, across the grid barriers of three passes."""
+    """Single-datagram messages in a random order: still a simple batch (every DataPacket completes its
+    own message on arrival), whatever the order."""
     stream, off, rpc, wire, dg_off = packetized(datagen.CONFIG2, 600000, 1400)
     perm = np.random.default_rng(11).permutation(len(dg_off) - 1)
     want = _gpu_vs_oracle(gcodec, gdev, *shuffled(wire, dg_off, perm))
     assert len(want[2]) == 600000 and (want[4] == C).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,mtu,window", [(300000, 1400, 0), (60000, 300, 64)])
+def test_reassembly_reordered_gpu(gcodec, gdev, n, mtu, window):
+    """Config-3 records packetized and reordered, the general path against the oracle: a full
+    permutation (~400k datagrams: ~200 sort tiles of 2048, three radix passes), or windows of 64 as
+    UDP's local reordering does (bench.py's reassembly_config3_reordered at a 300-byte MTU: messages of
+    up to ~16 packets in any order -- the group passes' permutation case -- and RPCIDs that another
+    workgroup's datagram claimed in the table -- key_kernel's lookup)."""
+    stream, off, rpc, wire, dg_off = packetized(datagen.CONFIG3, n, mtu)
+    nd = len(dg_off) - 1
+    rng = np.random.default_rng(n + window)
+    perm = np.argsort(np.arange(nd) // window + rng.random(nd), kind="stable") if window else rng.permutation(nd)
+    want = _gpu_vs_oracle(gcodec, gdev, *shuffled(wire, dg_off, perm))
+    assert len(want[2]) == n and (want[4] == C).all()
 
 
 @pytest.mark.gpu
@@ -269,8 +285,9 @@ def test_reassembly_one_fragment_makes_batch_general_gpu(gcodec, gdev, where):
 @pytest.mark.gpu
 @pytest.mark.parametrize("cfg,mtu", [("config2", 1400), ("config3", 1400), ("config3", 300)])
 def test_reassembly_send_order_gpu(gcodec, gdev, cfg, mtu):
-    """The packetizer's send order: RPCIDs never decrease, so the groups are the runs of equal RPCIDs
-    (no hash table) and each run is one message of packets 0..T-1 (no per-sequence state)."""
+    """The packetizer's send order with hashed RPCIDs (not increasing, so not packetizer runs): the
+    general path's hash table, whose claiming arrivals come out in order (no sort), and groups that are
+    one message of packets 0..T-1 each (no per-sequence state)."""
     stream, off, rpc, wire, dg_off = packetized(datagen.CONFIG2 if cfg == "config2" else datagen.CONFIG3, 20000, mtu)
     want = _gpu_vs_oracle(gcodec, gdev, wire, dg_off)
     assert len(want[2]) == 20000 and (want[4] == C).all()
