@@ -129,16 +129,22 @@ __device__ __forceinline__ void flag_raise(unsigned* w, bool any) {  // whole wo
         if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) atomicOr(p, 1u);
     }
 }
-// The general path's kernels read one word instead, `gen` (and `nm`, flag [2]), which emit_kernel's
-// first thread writes from the shards before the general path is forked: an empty launch of a
-// single-datagram or runs batch then costs one load per workgroup, not 16-48 (those launches run
-// beside the payload copy and take CU slots from it while they last).
+// The general path's later kernels read one word instead, `gen` (and `nm`, flag [2]), which its first
+// launch (init_kernel) writes from the shards: an empty launch of a single-datagram or runs batch
+// then costs one load per workgroup, not 16-48 (those launches run beside the payload copy and take
+// CU slots from it while they last).
 __device__ __forceinline__ bool gated_off(const unsigned* gate) { return *gate == 0; }
 
 // ---- 1a'. the hash table set to "empty" (general path, RPCIDs out of order)
-__global__ __launch_bounds__(256) void init_kernel(u64* table, u32* first, u64 ts, const unsigned* gen,
-                                                   const unsigned* nm) {
-    if (gated_off(gen) || gated_off(nm)) return;
+// (The general path's first launch: it also writes the gate words from the parse's flag shards.)
+__global__ __launch_bounds__(256) void init_kernel(u64* table, u32* first, u64 ts, const unsigned* flags,
+                                                   unsigned* gen, unsigned* nm) {
+    const bool nonmono = flag_set(flags + 2), general = flag_set(flags) && (nonmono || flag_set(flags + 3));
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // read by the general path's later launches
+        *gen = general;
+        *nm = nonmono;
+    }
+    if (!general || !nonmono) return;
     for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; i < ts; i += (u64)gridDim.x * 256) table[i] = kEmpty;
     if (blockIdx.x == 0 && threadIdx.x == 0) first[ts] = ~0u;  // (the special slot's key; the others are
                                                                // written by the CAS that claims the slot)
@@ -577,10 +583,6 @@ __global__ __launch_bounds__(256) void emit_kernel(Args a, const unsigned* flags
     const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
     const bool simple = !flag_set(flags), nonmono = flag_set(a.nonmono);
     const bool general = !simple && (nonmono || flag_set(flags + 3));
-    if (blockIdx.x == 0 && threadIdx.x == 0) {  // the general path's gates (read after the fork)
-        *a.gen = general;
-        *a.nm = nonmono;
-    }
     if (general) {  // the general path's batch
         if (i == 0) *nseg = 0;
         return;
@@ -1041,24 +1043,24 @@ hipError_t launch_reassemble(const uint8_t* wire, const u64* dg_off, u64 n, uint
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(rx::parse_kernel, dim3((unsigned)nt), b256, 0, stream, a, (unsigned*)flag);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(rx::emit_kernel, dim3((unsigned)nt), b256, 0, stream, a, flag, nmsg, nseg, (Pair*)(w + L.pre3));
-    if ((e = hipGetLastError()) != hipSuccess) return e;
     // The general path is queued for every batch; each of its kernels exits at once unless the
-    // emit's gate word says so (no host read: the call stays asynchronous).  It runs on `aux`,
-    // forked here (after the emit, which writes the gate words) and joined at the end, so for a
-    // single-datagram or runs batch its empty launches overlap the copy below.  The two branches
-    // share no buffer that both write for the same batch: every write of the main branch past this
-    // point is for a batch the general path skips (its zero segment count for the others excepted,
-    // in a word of its own), every write of the general branch for one it takes.
+    // parse's flags say so (no host read: the call stays asynchronous).  It runs on `aux`, forked
+    // here and joined at the end, so for a single-datagram or runs batch its empty launches overlap
+    // the emit and the copy below.  The two branches share no buffer that both write for the same
+    // batch: every write of the main branch past this point is for a batch the general path skips
+    // (its zero segment count for the others excepted, in a word of its own), every write of the
+    // general branch for one it takes.
     hipStream_t gs = stream;
     if (aux && fork && join) {
         if ((e = hipEventRecord(fork, stream)) != hipSuccess) return e;
         if ((e = hipStreamWaitEvent(aux, fork, 0)) != hipSuccess) return e;
         gs = aux;
     }
+    hipLaunchKernelGGL(rx::emit_kernel, dim3((unsigned)nt), b256, 0, stream, a, flag, nmsg, nseg, (Pair*)(w + L.pre3));
+    if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = seg_tail(nseg, false, stream)) != hipSuccess) return e;
     hipLaunchKernelGGL(rx::init_kernel, dim3((unsigned)std::min<u64>(rx::tiles(TS + 1), 4096)), b256, 0, gs, a.table,
-                       a.first, TS, gen, a.nm);
+                       a.first, TS, flag, a.gen, a.nm);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(rx::hash_kernel, gq, b256, 0, gs, a, gen);
     if ((e = hipGetLastError()) != hipSuccess) return e;
