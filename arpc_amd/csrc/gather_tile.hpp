@@ -167,7 +167,7 @@ __device__ __forceinline__ void gather_tile(const GatherArgs& a, u64 tile, u64 n
     const int slot = __builtin_amdgcn_mbcnt_hi((u32)(lm >> 32), __builtin_amdgcn_mbcnt_lo((u32)lm, 0u));
     const int nl = __popcll(lm);
     const int span = (int)(D1 - D0);
-    const bool nt = NT && span <= kNtSpan;  // (st16)
+    const bool nt = NT && (span <= kNtSpan || a.nt == 2);  // (st16; nt 2: at any span)
     if (live) {
         S.addr[slot] = (u64)(uintptr_t)(a.in + src);
         S.o[slot] = (int)(d - D0);

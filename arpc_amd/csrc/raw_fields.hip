@@ -254,7 +254,8 @@ hipError_t launch_segment_gather(const raw::GatherArgs& a, hipStream_t stream) {
 #ifdef SYMHIP_TUNING
     if (const int v = tuning_variant("SYMHIP_GATHER_VARIANT")) ku = v == 1 ? 2 : v == 2 ? 8 : 4;
 #endif
-    if (ku == 2) hipLaunchKernelGGL((raw::gather_kernel<false, 2>), grid, dim3(256), 0, stream, a);
+    if (ku == 2 && a.nt) hipLaunchKernelGGL((raw::gather_kernel<false, 2, true>), grid, dim3(256), 0, stream, a);
+    else if (ku == 2) hipLaunchKernelGGL((raw::gather_kernel<false, 2>), grid, dim3(256), 0, stream, a);
 #ifdef SYMHIP_TUNING
     else if (ku == 8) hipLaunchKernelGGL((raw::gather_kernel<false, 8>), grid, dim3(256), 0, stream, a);
 #endif
