@@ -175,7 +175,7 @@ struct GatherArgs {
     uint64_t* nkept;       // FW
     unsigned* err;
     uint64_t seg_bytes_hint;  // VAR: the caller's estimate of the mean segment length (0: none)
-    int nt;                   // nontemporal stores for wave spans of at most kNtSpan bytes (st16; 4-chunk kernel)
+    int nt;                   // nontemporal stores: 1 for wave spans of at most kNtSpan bytes, 2 at any span (st16)
 };
 }  // namespace raw
 hipError_t launch_tile_scan(const raw::Pair* agg, raw::Pair* pre, uint64_t ntiles, hipStream_t stream);
