@@ -1031,7 +1031,7 @@ hipError_t launch_reassemble(const uint8_t* wire, const u64* dg_off, u64 n, uint
         ga.cap = msg_cap;
         ga.err = err;
         ga.seg_bytes_hint = msg_cap / n;  // (the capacity is usually the wire size)
-        ga.nt = general ? 0 : 2;  // the single-datagram / runs gather: nontemporal at any span (see DESIGN)
+        ga.nt = 2;  // nontemporal at any span (see DESIGN)
         return launch_segment_gather(ga, st);
     };
     // Simple batches (every DataPacket one whole message) complete here: parse (with the tile
